@@ -1,0 +1,272 @@
+#!/usr/bin/env python3
+"""bench.py -- device-resident batched MD5 throughput on MI355X.
+
+Metric (BASELINE.json): device-resident MD5 GiB/s on batched 16 KiB chunks.
+A "step" = one pass of the batched-MD5 kernel over the rank's whole batch
+(default 1,048,576 x 16 KiB = 16 GiB, BASELINE config C2), inputs already in
+HBM (filled on the device by md5hip_fill_synthetic, per-rank seed).
+
+    python bench.py [--gpus N --steps K --warmup W] [--config c2|c3|c5]
+
+N > 1: one process per GPU (torch.distributed.run); each rank hashes its own
+shard of independent chunks (weak scaling, no data-path collective); barrier +
+device sync bracket the K timed steps and the MAX time over ranks is used.
+Rank 0 prints ONE JSON line.  The cpu_baseline leg (rank 0, N=1 only) runs the
+reference md5.c (oracle/_ref, else the oracle port) on the C1 sample; it is the
+only use of oracle/ here.
+"""
+import argparse
+import json
+import os
+import platform
+import subprocess
+import sys
+import time
+
+import torch
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+from sproxy_amd import md5 as m  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+PCIE_PEAK_GBS = 63.0           # PCIe Gen5 x16 (spec)
+METRIC = "device-resident MD5 GiB/s on batched 16 KiB chunks at 1/2/4/8 MI355X"
+GIB = float(1 << 30)
+
+
+def dist_setup(ngpus):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != ngpus and world > 1:
+        raise SystemExit(f"--gpus {ngpus} but WORLD_SIZE={world}")
+    torch.cuda.set_device(local)
+    if world > 1:
+        import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    return rank, world, local
+
+
+def barrier(world):
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+
+
+def max_over_ranks(x, world):
+    if world == 1:
+        return x
+    import torch.distributed as dist
+    t = torch.tensor([x], dtype=torch.float64, device="cuda")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def timed_steps(fn, steps, warmup, world):
+    """W untimed steps, then exactly K steps between barrier+sync pairs.
+    Returns (wall seconds for K steps, avg device ms per step from HIP events
+    recorded on the stream the kernels run on)."""
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize()
+    stream = torch.cuda.current_stream()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    barrier(world)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    e0.record(stream)
+    for _ in range(steps):
+        fn()
+    e1.record(stream)
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    barrier(world)
+    return t1 - t0, e0.elapsed_time(e1) / steps
+
+
+def cpu_model():
+    try:
+        for ln in open("/proc/cpuinfo"):
+            if ln.startswith("model name"):
+                return ln.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or "unknown"
+
+
+def cpu_baseline(reps=5):
+    """Host md5.c on the C1 sample: 65,536 x 16 KiB xorshift64,
+    Init/Update/Final per chunk, 1 thread, median of `reps`."""
+    ref = os.path.join(REPO, "oracle", "_ref", "md5_cpu_bench")
+    port = os.path.join(REPO, "oracle", "_build", "md5_cpu_bench_port")
+    exe, kind = (ref, "reference") if os.path.exists(ref) else (port, "port")
+    if not os.path.exists(exe):
+        return None
+    out = subprocess.run([exe, "65536", "16384", str(reps), "1"], capture_output=True, text=True,
+                         timeout=600, check=True).stdout
+    r = json.loads(out.strip().splitlines()[-1])
+    return {"value": round(r["gib_s"], 4), "unit": "GiB/s", "cores": 1, "kind": kind,
+            "sample": (f"C1: 65,536 x 16 KiB xorshift64 (1 GiB), MD5Init/Update/Final per chunk, "
+                       f"median of {reps}, 1 thread of {cpu_model()} ({os.cpu_count()} logical CPUs); "
+                       f"fold {r['fold']} (expect 53a0a616)"),
+            "fold_ok": r["fold"] == "53a0a616"}
+
+
+def load_traffic(path, variant):
+    """HBM bytes per launch from a committed rocprofv3 PMC summary (profiles/)."""
+    if not path or not os.path.exists(path):
+        return None
+    try:
+        d = json.load(open(path))
+        return d.get(variant, d.get("default"))
+    except Exception:
+        return None
+
+
+def run_c2(a, rank, world):
+    n, L = a.chunks, a.len
+    data = torch.empty(n * L, dtype=torch.uint8, device="cuda")
+    m.fill_synthetic(data, seed=0x5EED0000 + rank)
+    out = torch.empty((n, 16), dtype=torch.uint8, device="cuda")
+    variant = m.VARIANTS[a.variant]
+    fn = lambda: m.digest_fixed(data, n, L, out=out, variant=variant)  # noqa: E731
+    wall, dev_ms = timed_steps(fn, a.steps, a.warmup, world)
+    wall_max = max_over_ranks(wall, world)
+    dev_ms_max = max_over_ranks(dev_ms, world)
+    total_bytes = float(n) * L * world * a.steps
+    value = total_bytes / wall_max / GIB
+    alg_bytes = float(n) * (L + 16)            # read every chunk once + 16-B digest write
+    achieved = alg_bytes / (dev_ms_max * 1e-3) / 1e9
+    vname = m.variant_name(m.resolve_variant(variant))
+    res = {
+        "metric": METRIC, "value": round(value, 2), "unit": "GiB/s", "n_gpus": world,
+        "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(wall_max / a.steps * 1e3, 4),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32",
+        "data": "synthetic (device-generated splitmix words, per-rank seed)",
+        "config": {"workload": "C2: 1,048,576 x 16 KiB chunks per GPU, device-resident"
+                   if (n, L) == (1 << 20, 16384) else f"{n} x {L} B chunks per GPU, device-resident",
+                   "chunks_per_gpu": n, "chunk_bytes": L, "kernel_variant": vname,
+                   "parallelism": f"dp{world} (independent chunk shards, no collective)"},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                     "traffic": load_traffic(a.traffic, vname),
+                     "kernel": "md5hip " + vname, "avg_launch_ms": round(dev_ms_max, 4),
+                     "alg_bytes_per_launch": int(alg_bytes)},
+    }
+    return res
+
+
+def run_c3(a, rank, world):
+    """Mixed lengths 4 KiB..1 MiB (netcache chunk_size range, httpd.c:7968) with
+    1-in-8 ragged tails, packed 16-B aligned, lanes packed longest-first."""
+    import numpy as np
+    rng = np.random.default_rng(1000 + rank)
+    classes = np.array([4096 << k for k in range(9)], dtype=np.int64)
+    target = a.c3_bytes
+    lens = []
+    tot = 0
+    while tot < target:
+        c = int(classes[rng.integers(0, 9)])
+        if rng.integers(0, 8) == 0:
+            c = int(rng.integers(1, c))
+        lens.append(c)
+        tot += c
+    lens = np.array(lens, dtype=np.int64)
+    offs = np.concatenate([[0], np.cumsum((lens + 15) // 16 * 16)[:-1]])
+    total = int(offs[-1] + lens[-1] + 16)
+    data = torch.empty((total + 15) // 16 * 16, dtype=torch.uint8, device="cuda")
+    m.fill_synthetic(data, seed=0xC3 + rank)
+    t0 = time.perf_counter()
+    order = m.plan_order(lens.astype(np.uint32))
+    plan_ms = (time.perf_counter() - t0) * 1e3
+    d_off = torch.from_numpy(offs).cuda()
+    d_len = torch.from_numpy(lens.astype(np.int32)).cuda()
+    d_ord = torch.from_numpy(order.astype(np.int32)).cuda()
+    out = torch.empty((lens.size, 16), dtype=torch.uint8, device="cuda")
+    fn = lambda: m.digest_desc(data, d_off, d_len, d_ord, out=out)  # noqa: E731
+    wall, dev_ms = timed_steps(fn, a.steps, a.warmup, world)
+    wall_max = max_over_ranks(wall, world)
+    payload = float(lens.sum())
+    value = payload * world * a.steps / wall_max / GIB
+    # the longest chunk bounds the step: a 1 MiB chunk is 16,385 dependent
+    # compressions on one lane
+    return {"metric": "device-resident MD5 GiB/s, mixed 4 KiB-1 MiB chunks (C3)",
+            "value": round(value, 2), "unit": "GiB/s", "n_gpus": world, "steps": a.steps,
+            "warmup": a.warmup, "ms_per_step": round(wall_max / a.steps * 1e3, 4),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32",
+            "data": "synthetic", "config": {"workload": "C3 mixed lengths", "chunks": int(lens.size),
+                                            "payload_bytes": int(payload),
+                                            "longest": int(lens.max()), "plan_ms": round(plan_ms, 3)},
+            "roofline": {"bound": "hbm", "achieved": round(payload / (dev_ms * 1e-3) / 1e9, 1),
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(payload / (dev_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                         "traffic": None}}
+
+
+def run_c5(a, rank, world):
+    """End to end from pinned host memory: H2D -> MD5 -> D2H over pipelined
+    batcher slots (md5hip_batch_host_fixed)."""
+    import numpy as np
+    n, L = a.c5_chunks, a.len
+    host = torch.empty(n * L, dtype=torch.uint8, pin_memory=True)
+    host.view(torch.int64).random_(generator=torch.Generator().manual_seed(5))
+    arr = host.numpy()
+    # PCIe H2D alone (the denominator for this config)
+    dev = torch.empty(n * L, dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    dev.copy_(host, non_blocking=True)
+    torch.cuda.synchronize()
+    h2d_gbs = n * L / (time.perf_counter() - t0) / 1e9
+    del dev
+    with m.Batcher(device=torch.cuda.current_device(), slice_bytes=a.c5_slice, nslots=3) as b:
+        for _ in range(a.warmup):
+            b.host_fixed(arr, n, L)
+        t0 = time.perf_counter()
+        for _ in range(a.steps):
+            b.host_fixed(arr, n, L)
+        wall = time.perf_counter() - t0
+    gbs = n * L * a.steps / wall / 1e9
+    return {"metric": "end-to-end MD5 GiB/s from pinned host memory (C5)",
+            "value": round(n * L * a.steps / wall / GIB, 2), "unit": "GiB/s", "n_gpus": 1,
+            "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(wall / a.steps * 1e3, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32",
+            "data": "synthetic (host random)", "config": {"workload": "C5", "chunks": n,
+                                                          "chunk_bytes": L, "slice_bytes": a.c5_slice,
+                                                          "slots": 3},
+            "roofline": {"bound": "pcie", "achieved": round(gbs, 2), "peak": round(h2d_gbs, 2),
+                         "unit": "GB/s", "frac": round(gbs / h2d_gbs, 4),
+                         "peak_note": f"measured pinned H2D copy alone; spec {PCIE_PEAK_GBS} GB/s",
+                         "traffic": None}}
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--config", default="c2", choices=["c2", "c3", "c5"])
+    p.add_argument("--chunks", type=int, default=1 << 20, help="chunks per GPU (C2)")
+    p.add_argument("--len", type=int, default=16384)
+    p.add_argument("--variant", default="auto", choices=sorted(m.VARIANTS))
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--traffic", default=os.path.join(REPO, "profiles", "traffic.json"))
+    p.add_argument("--c3-bytes", type=int, default=16 << 30)
+    p.add_argument("--c5-chunks", type=int, default=1 << 18)
+    p.add_argument("--c5-slice", type=int, default=64 << 20)
+    a = p.parse_args()
+    rank, world, _ = dist_setup(a.gpus)
+    res = {"c2": run_c2, "c3": run_c3, "c5": run_c5}[a.config](a, rank, world)
+    if rank == 0 and world == 1 and a.config == "c2" and not a.no_cpu_baseline:
+        res["cpu_baseline"] = cpu_baseline()
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

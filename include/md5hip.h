@@ -1,0 +1,113 @@
+/*
+ * include/md5hip.h -- batched MD5 on MI355X (gfx950): the C-ABI boundary.
+ *
+ * sproxy has no batched digest entry; its chunk-granular checksum call site is
+ *   nc_crc_t blk_make_crc(fc_inode_t *inode, fc_blk_t *blk, ssize_t len, int fastcrc)
+ *   (netcache/common/blk_io.c:354-430, called from blk_io.c:665-704 on cache
+ *    read, blk_io.c:851-863 on origin read, bc_mgr.c:1464-1492 on write verify)
+ * which checksums ONE cache block per call.  The entries below replace that
+ * per-block call with a batch of independent chunks; every digest equals
+ * MD5Init/MD5Update(chunk)/MD5Final from md5.c:153-265 bit for bit.
+ *
+ * Conventions (all entries):
+ *   - plain C types only; `stream` is a hipStream_t passed as void* (NULL =
+ *     the null stream of the current device); device pointers are memory of
+ *     the current HIP device (hipMalloc, or a torch CUDA tensor's data_ptr);
+ *   - asynchronous w.r.t. the host unless stated; errors are returned as
+ *     0 / negative errno, checked BEFORE anything is enqueued:
+ *       -EINVAL  bad argument (NULL pointer with n > 0, len > stride, ...)
+ *       -ENODEV  no usable gfx950 device / HIP runtime failure
+ *       -EIO     the kernel launch itself failed
+ *   - digest i is 16 bytes, MD5 byte order (md5.c:262-263), at digests+16*i.
+ */
+#ifndef SPROXY_AMD_MD5HIP_H
+#define SPROXY_AMD_MD5HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MD5HIP_ABI_VERSION 1
+
+/* Kernel variants for md5hip_digest_fixed_variant (tuning / A-B benches). */
+enum md5hip_variant {
+    MD5HIP_AUTO = 0,        /* library's choice (measured best on MI355X) */
+    MD5HIP_DIRECT2 = 1,     /* lane-direct dwordx4 loads, 2-block register ring */
+    MD5HIP_DIRECT4 = 2,     /* lane-direct dwordx4 loads, 4-block register ring */
+    MD5HIP_LDS64 = 3,       /* wave LDS-DMA staging, 64 B per chunk per stage */
+    MD5HIP_LDS128 = 4,      /* wave LDS-DMA staging, 128 B per chunk per stage */
+    MD5HIP_NUM_VARIANTS = 5
+};
+
+int md5hip_abi_version(void);
+const char *md5hip_variant_name(int variant);
+/* The concrete variant MD5HIP_AUTO resolves to (env MD5HIP_VARIANT overrides). */
+int md5hip_resolve_variant(int variant);
+
+/*
+ * Fixed-length device batch (the hot path):
+ *   digests[i] = MD5(d_base + i*stride, len),  i in [0, n).
+ * Requires len <= stride.  Fast path: d_base and stride 16-byte aligned;
+ * otherwise the descriptor kernel is used.  Replaces n calls of
+ * blk_make_crc (blk_io.c:354) over equal-sized blocks.
+ */
+int md5hip_digest_fixed(const void *d_base, uint64_t n, uint32_t len, uint64_t stride,
+                        unsigned char *d_digests, void *stream);
+int md5hip_digest_fixed_variant(const void *d_base, uint64_t n, uint32_t len, uint64_t stride,
+                                unsigned char *d_digests, void *stream, int variant);
+
+/*
+ * Descriptor device batch (mixed lengths, any alignment; config C3):
+ *   digests[i] = MD5(d_base + d_offsets[i], d_lens[i]).
+ * d_order (optional, may be NULL) is a permutation of [0, n) giving the order
+ * in which chunks are packed onto lanes; pass md5hip_plan_order()'s output
+ * (longest first) so that a wave's 64 lanes carry similar block counts.
+ */
+int md5hip_digest_desc(const void *d_base, const uint64_t *d_offsets, const uint32_t *d_lens,
+                       const uint32_t *d_order, uint64_t n, unsigned char *d_digests,
+                       void *stream);
+
+/*
+ * Host helper: order[] = indices of lens[] sorted by MD5 block count,
+ * descending (stable counting sort, O(n)).  Synchronous, host memory.
+ */
+int md5hip_plan_order(const uint32_t *lens, uint64_t n, uint32_t *order);
+
+/*
+ * Synthetic-data generator for benches/tests: fills nbytes (multiple of 16)
+ * of device memory with word i = mix32(seed, i) (md5hip_kernels.hip).
+ */
+int md5hip_fill_synthetic(void *d_dst, uint64_t nbytes, uint64_t seed, void *stream);
+
+/*
+ * Host-memory batches (the blk_make_crc call site, blk_io.c:354; config C5).
+ * A batcher owns `nslots` pipeline slots (HIP stream + pinned staging of
+ * `slice_bytes` + device buffers); slices of the batch flow
+ * host gather -> H2D -> kernel -> D2H with slot k+1 overlapping slot k.
+ * Calls are synchronous: they return once every digest is in `digests`.
+ * A batcher is not thread-safe; use one per submitting thread.
+ */
+typedef struct md5hip_batcher md5hip_batcher;
+
+int md5hip_batcher_create(int device, uint64_t slice_bytes, uint32_t nslots,
+                          md5hip_batcher **out);
+void md5hip_batcher_destroy(md5hip_batcher *b);
+
+/* digests[i] = MD5(ptrs[i], lens[i]); any host memory.  -E2BIG if one chunk
+ * exceeds slice_bytes. */
+int md5_batch_submit(md5hip_batcher *b, const void *const *ptrs, const uint32_t *lens,
+                     uint64_t n, unsigned char *digests);
+
+/* digests[i] = MD5(h_base + i*stride, len) from one contiguous host buffer
+ * (pinned for full PCIe rate), copied slice by slice with no host gather. */
+int md5hip_batch_host_fixed(md5hip_batcher *b, const void *h_base, uint64_t n, uint32_t len,
+                            uint64_t stride, unsigned char *digests);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* SPROXY_AMD_MD5HIP_H */

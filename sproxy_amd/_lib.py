@@ -1,0 +1,86 @@
+"""ctypes binding of libmd5hip.so (the C ABI declared in include/md5.h and
+include/md5hip.h).
+
+The library is built in-tree by ``__graft_entry__.build()`` (make -C
+sproxy_amd/csrc).  There is NO fallback: if the shared object is missing or a
+call fails, the error surfaces -- the product never routes through the oracle
+or a host-side hash.
+
+torch is imported first when available so that libmd5hip.so binds to the same
+libamdhip64.so.7 instance torch uses (both carry that SONAME), which makes torch
+streams and torch-allocated device pointers valid handles for our entries.
+"""
+import ctypes
+import errno
+import os
+
+try:  # share torch's HIP runtime (see module docstring)
+    import torch  # noqa: F401
+except Exception:  # pragma: no cover - torch is plumbing, not required for the C path
+    torch = None
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "lib", "libmd5hip.so")
+
+_lib = None
+
+c_u8p = ctypes.c_void_p
+
+
+class MD5Context(ctypes.Structure):
+    """struct MD5Context, md5.h:33-38 (88 bytes)."""
+    _fields_ = [("buf", ctypes.c_uint32 * 4), ("bits", ctypes.c_uint32 * 2),
+                ("in_", ctypes.c_ubyte * 64)]
+
+
+class MD5HipError(RuntimeError):
+    def __init__(self, fn, rc):
+        name = errno.errorcode.get(-rc, str(rc))
+        super().__init__(f"{fn} failed: {rc} ({name})")
+        self.rc = rc
+
+
+def lib():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"{LIB_PATH} is not built: run `python -c 'import __graft_entry__ as g; g.build()'`")
+    L = ctypes.CDLL(LIB_PATH)
+    u64, u32, vp, i = ctypes.c_uint64, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_int
+    sig = {
+        "MD5Init": (None, [ctypes.POINTER(MD5Context)]),
+        "MD5Update": (None, [ctypes.POINTER(MD5Context), vp, ctypes.c_uint]),
+        "MD5Final": (None, [vp, ctypes.POINTER(MD5Context)]),
+        "md5hip_abi_version": (i, []),
+        "md5hip_variant_name": (ctypes.c_char_p, [i]),
+        "md5hip_resolve_variant": (i, [i]),
+        "md5hip_digest_fixed": (i, [vp, u64, u32, u64, vp, vp]),
+        "md5hip_digest_fixed_variant": (i, [vp, u64, u32, u64, vp, vp, i]),
+        "md5hip_digest_desc": (i, [vp, vp, vp, vp, u64, vp, vp]),
+        "md5hip_plan_order": (i, [vp, u64, vp]),
+        "md5hip_fill_synthetic": (i, [vp, u64, u64, vp]),
+        "md5hip_batcher_create": (i, [i, u64, u32, ctypes.POINTER(vp)]),
+        "md5hip_batcher_destroy": (None, [vp]),
+        "md5_batch_submit": (i, [vp, vp, vp, u64, vp]),
+        "md5hip_batch_host_fixed": (i, [vp, vp, u64, u32, u64, vp]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    _lib = L
+    return L
+
+
+# Every symbol include/*.h declares (checked by tests/test_abi.py).
+EXPORTS = ["MD5Init", "MD5Update", "MD5Final", "md5hip_abi_version", "md5hip_variant_name",
+           "md5hip_resolve_variant",
+           "md5hip_digest_fixed", "md5hip_digest_fixed_variant", "md5hip_digest_desc",
+           "md5hip_plan_order", "md5hip_fill_synthetic", "md5hip_batcher_create",
+           "md5hip_batcher_destroy", "md5_batch_submit", "md5hip_batch_host_fixed"]
+
+
+def check(fn, rc):
+    if rc != 0:
+        raise MD5HipError(fn, rc)

@@ -1,0 +1,205 @@
+/*
+ * md5_submit.c -- host-memory batched submit (include/md5hip.h).
+ *
+ * Serves the netcache block-completion checksum site (blk_make_crc,
+ * netcache/common/blk_io.c:354-430): chunks live in host memory (cache pages,
+ * socket buffers), so the batch is staged H2D, hashed on the device and the
+ * 16-byte digests come back D2H.  A batcher owns `nslots` pipeline slots; slot
+ * k has its own HIP stream, pinned staging buffer, device buffer, descriptor
+ * arrays and completion event, so the host gather of slice k+1, the H2D copy
+ * of slice k and the kernel of slice k-1 overlap.
+ *
+ * Errors: 0 / negative errno (include/md5hip.h conventions); -E2BIG when one
+ * chunk alone exceeds the slot's staging capacity.
+ */
+#include <errno.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <hip/hip_runtime_api.h>
+
+#include "../../include/md5hip.h"
+
+struct slot {
+    hipStream_t stream;
+    hipEvent_t done;
+    unsigned char *h_data, *d_data;   /* staging, `cap` bytes */
+    uint64_t *h_off, *d_off;          /* descriptors, `maxn` entries */
+    uint32_t *h_len, *d_len;
+    uint32_t *h_ord, *d_ord;
+    unsigned char *h_dig, *d_dig;     /* 16 * maxn */
+    unsigned char *user_dig;          /* where this slot's digests go (NULL = idle) */
+    uint64_t ndig;
+    int busy;
+};
+
+struct md5hip_batcher {
+    int device;
+    uint32_t nslots;
+    uint64_t cap;      /* staging bytes per slot */
+    uint64_t maxn;     /* chunks per slot */
+    struct slot *s;
+};
+
+#define CK(x) do { if ((x) != hipSuccess) { rc = -ENODEV; goto fail; } } while (0)
+
+static int slot_retire(struct slot *sl)
+{
+    if (!sl->busy) return 0;
+    if (hipEventSynchronize(sl->done) != hipSuccess) return -EIO;
+    if (sl->user_dig) memcpy(sl->user_dig, sl->h_dig, 16 * sl->ndig);
+    sl->busy = 0;
+    sl->user_dig = NULL;
+    return 0;
+}
+
+void md5hip_batcher_destroy(md5hip_batcher *b)
+{
+    if (!b) return;
+    hipSetDevice(b->device);
+    for (uint32_t k = 0; b->s && k < b->nslots; k++) {
+        struct slot *sl = &b->s[k];
+        if (sl->busy) hipEventSynchronize(sl->done);
+        if (sl->stream) hipStreamDestroy(sl->stream);
+        if (sl->done) hipEventDestroy(sl->done);
+        hipHostFree(sl->h_data); hipHostFree(sl->h_off); hipHostFree(sl->h_len);
+        hipHostFree(sl->h_ord); hipHostFree(sl->h_dig);
+        hipFree(sl->d_data); hipFree(sl->d_off); hipFree(sl->d_len);
+        hipFree(sl->d_ord); hipFree(sl->d_dig);
+    }
+    free(b->s);
+    free(b);
+}
+
+int md5hip_batcher_create(int device, uint64_t slice_bytes, uint32_t nslots, md5hip_batcher **out)
+{
+    int rc = 0;
+    if (!out) return -EINVAL;
+    *out = NULL;
+    if (nslots == 0) nslots = 3;
+    if (nslots > 16) return -EINVAL;
+    if (slice_bytes == 0) slice_bytes = 64ull << 20;
+    slice_bytes = (slice_bytes + 4095) & ~4095ull;
+    if (hipSetDevice(device) != hipSuccess) return -ENODEV;
+    md5hip_batcher *b = calloc(1, sizeof *b);
+    if (!b) return -ENOMEM;
+    b->device = device;
+    b->nslots = nslots;
+    b->cap = slice_bytes;
+    b->maxn = slice_bytes / 64 < 4096 ? 4096 : slice_bytes / 64;
+    b->s = calloc(nslots, sizeof *b->s);
+    if (!b->s) { free(b); return -ENOMEM; }
+    for (uint32_t k = 0; k < nslots; k++) {
+        struct slot *sl = &b->s[k];
+        CK(hipStreamCreateWithFlags(&sl->stream, hipStreamNonBlocking));
+        CK(hipEventCreateWithFlags(&sl->done, hipEventDisableTiming));
+        CK(hipHostMalloc((void **)&sl->h_data, b->cap, hipHostMallocDefault));
+        CK(hipHostMalloc((void **)&sl->h_off, 8 * b->maxn, hipHostMallocDefault));
+        CK(hipHostMalloc((void **)&sl->h_len, 4 * b->maxn, hipHostMallocDefault));
+        CK(hipHostMalloc((void **)&sl->h_ord, 4 * b->maxn, hipHostMallocDefault));
+        CK(hipHostMalloc((void **)&sl->h_dig, 16 * b->maxn, hipHostMallocDefault));
+        CK(hipMalloc((void **)&sl->d_data, b->cap));
+        CK(hipMalloc((void **)&sl->d_off, 8 * b->maxn));
+        CK(hipMalloc((void **)&sl->d_len, 4 * b->maxn));
+        CK(hipMalloc((void **)&sl->d_ord, 4 * b->maxn));
+        CK(hipMalloc((void **)&sl->d_dig, 16 * b->maxn));
+    }
+    *out = b;
+    return 0;
+fail:
+    md5hip_batcher_destroy(b);
+    return rc;
+}
+
+/* Enqueue slot `sl` holding `n` chunks, `bytes` staged bytes. */
+static int slot_launch(struct slot *sl, uint64_t n, uint64_t bytes, unsigned char *user_dig)
+{
+    int rc;
+    if (md5hip_plan_order(sl->h_len, n, sl->h_ord) != 0) return -EINVAL;
+    if (hipMemcpyAsync(sl->d_data, sl->h_data, bytes, hipMemcpyHostToDevice, sl->stream) ||
+        hipMemcpyAsync(sl->d_off, sl->h_off, 8 * n, hipMemcpyHostToDevice, sl->stream) ||
+        hipMemcpyAsync(sl->d_len, sl->h_len, 4 * n, hipMemcpyHostToDevice, sl->stream) ||
+        hipMemcpyAsync(sl->d_ord, sl->h_ord, 4 * n, hipMemcpyHostToDevice, sl->stream))
+        return -EIO;
+    rc = md5hip_digest_desc(sl->d_data, sl->d_off, sl->d_len, sl->d_ord, n, sl->d_dig, sl->stream);
+    if (rc) return rc;
+    if (hipMemcpyAsync(sl->h_dig, sl->d_dig, 16 * n, hipMemcpyDeviceToHost, sl->stream) ||
+        hipEventRecord(sl->done, sl->stream))
+        return -EIO;
+    sl->busy = 1;
+    sl->user_dig = user_dig;
+    sl->ndig = n;
+    return 0;
+}
+
+int md5_batch_submit(md5hip_batcher *b, const void *const *ptrs, const uint32_t *lens, uint64_t n,
+                     unsigned char *digests)
+{
+    if (!b) return -EINVAL;
+    if (n == 0) return 0;
+    if (!ptrs || !lens || !digests) return -EINVAL;
+    for (uint64_t i = 0; i < n; i++) {
+        if (!ptrs[i] && lens[i]) return -EINVAL;
+        if (((uint64_t)lens[i] + 15) / 16 * 16 > b->cap) return -E2BIG;
+    }
+    if (hipSetDevice(b->device) != hipSuccess) return -ENODEV;
+    int rc = 0;
+    uint32_t k = 0;
+    uint64_t i = 0;
+    while (i < n) {
+        struct slot *sl = &b->s[k];
+        if ((rc = slot_retire(sl))) return rc;
+        uint64_t used = 0, m = 0, first = i;
+        while (i < n && m < b->maxn) {
+            const uint64_t sz = ((uint64_t)lens[i] + 15) & ~15ull;   /* 16-B aligned packing */
+            if (used + sz > b->cap) break;
+            if (lens[i]) memcpy(sl->h_data + used, ptrs[i], lens[i]);
+            sl->h_off[m] = used;
+            sl->h_len[m] = lens[i];
+            used += sz;
+            m++;
+            i++;
+        }
+        if ((rc = slot_launch(sl, m, used ? used : 16, digests + 16 * first))) return rc;
+        k = (k + 1) % b->nslots;
+    }
+    for (uint32_t j = 0; j < b->nslots; j++)
+        if ((rc = slot_retire(&b->s[j]))) return rc;
+    return 0;
+}
+
+int md5hip_batch_host_fixed(md5hip_batcher *b, const void *h_base, uint64_t n, uint32_t len,
+                            uint64_t stride, unsigned char *digests)
+{
+    if (!b) return -EINVAL;
+    if (n == 0) return 0;
+    if (!h_base || !digests || len > stride) return -EINVAL;
+    if (stride > b->cap) return -E2BIG;
+    if (hipSetDevice(b->device) != hipSuccess) return -ENODEV;
+    const unsigned char *src = (const unsigned char *)h_base;
+    uint64_t per = b->cap / stride;
+    if (per > b->maxn) per = b->maxn;
+    int rc = 0;
+    uint32_t k = 0;
+    for (uint64_t i = 0; i < n; i += per) {
+        const uint64_t m = n - i < per ? n - i : per;
+        struct slot *sl = &b->s[k];
+        if ((rc = slot_retire(sl))) return rc;
+        const uint64_t bytes = (m - 1) * stride + len;
+        /* straight from the caller's (ideally pinned) buffer: no host gather */
+        if (hipMemcpyAsync(sl->d_data, src + i * stride, bytes, hipMemcpyHostToDevice, sl->stream))
+            return -EIO;
+        if ((rc = md5hip_digest_fixed(sl->d_data, m, len, stride, sl->d_dig, sl->stream))) return rc;
+        if (hipMemcpyAsync(sl->h_dig, sl->d_dig, 16 * m, hipMemcpyDeviceToHost, sl->stream) ||
+            hipEventRecord(sl->done, sl->stream))
+            return -EIO;
+        sl->busy = 1;
+        sl->user_dig = digests + 16 * i;
+        sl->ndig = m;
+        k = (k + 1) % b->nslots;
+    }
+    for (uint32_t j = 0; j < b->nslots; j++)
+        if ((rc = slot_retire(&b->s[j]))) return rc;
+    return 0;
+}

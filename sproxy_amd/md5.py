@@ -1,0 +1,235 @@
+"""Python host mirror of sproxy's MD5 interface (md5.h:31-51) plus the batched
+device entries (include/md5hip.h).
+
+Per-message API -- same names, argument order and behaviour as md5.c:153-265:
+    ctx = MD5Context(); MD5Init(ctx); MD5Update(ctx, buf, len); MD5Final(digest, ctx)
+(``MD5Final`` writes into ``digest`` -- a writable 16-byte buffer -- and also
+returns the digest as ``bytes``; it zeroes ``ctx`` like md5.c:264.)
+
+Batched device API (the hot path) -- torch CUDA tensors are only plumbing for
+device memory and streams; every byte is hashed by the HIP kernels of
+libmd5hip.so, and a CPU tensor is an error, never a fallback:
+    digest_fixed(data, n, length, stride=None)      -> uint8 [n, 16] on device
+    digest_desc(base, offsets, lens, order=None)     -> uint8 [n, 16] on device
+    plan_order(lens)                                 -> longest-first lane order
+Host-memory batches (the netcache block-checksum site, blk_io.c:354):
+    with Batcher(device=0) as b: b.submit([buf, ...]); b.host_fixed(arr, n, len)
+"""
+import ctypes
+
+import numpy as np
+
+from ._lib import MD5Context, MD5HipError, check, lib
+
+try:
+    import torch
+except Exception:  # pragma: no cover
+    torch = None
+
+MD5_DIGEST_SIZE = 16
+
+AUTO, DIRECT2, DIRECT4, LDS64, LDS128 = range(5)
+VARIANTS = {"auto": AUTO, "direct2": DIRECT2, "direct4": DIRECT4, "lds64": LDS64, "lds128": LDS128}
+
+
+# ---------------------------------------------------------------- per message
+def _addr(buf):
+    """(address, keepalive) of a bytes-like object."""
+    if isinstance(buf, np.ndarray):
+        a = np.ascontiguousarray(buf)
+        return a.ctypes.data, a
+    mv = memoryview(buf)
+    if mv.readonly:
+        b = ctypes.create_string_buffer(mv.tobytes(), max(mv.nbytes, 1))
+        return ctypes.addressof(b), b
+    c = (ctypes.c_char * max(mv.nbytes, 1)).from_buffer(mv) if mv.nbytes else ctypes.create_string_buffer(1)
+    return ctypes.addressof(c), (c, mv)
+
+
+def MD5Init(ctx: MD5Context) -> None:
+    lib().MD5Init(ctypes.byref(ctx))
+
+
+def MD5Update(ctx: MD5Context, buf, length: int = None) -> None:
+    mv = memoryview(buf)
+    n = mv.nbytes if length is None else int(length)
+    if n < 0 or n > mv.nbytes or n > 0xFFFFFFFF:
+        raise ValueError("length out of range (md5.h:47 takes an unsigned int)")
+    addr, keep = _addr(buf)
+    lib().MD5Update(ctypes.byref(ctx), addr, n)
+    del keep
+
+
+def MD5Final(digest, ctx: MD5Context) -> bytes:
+    out = (ctypes.c_ubyte * 16)()
+    lib().MD5Final(out, ctypes.byref(ctx))
+    d = bytes(out)
+    if digest is not None:
+        memoryview(digest)[:16] = d
+    return d
+
+
+def md5(data) -> bytes:
+    """One-shot convenience: Init/Update/Final over a bytes-like object."""
+    ctx = MD5Context()
+    MD5Init(ctx)
+    mv = memoryview(data).cast("B")
+    off = 0
+    while off < mv.nbytes or off == 0:
+        part = min(mv.nbytes - off, 1 << 30)
+        MD5Update(ctx, mv[off:off + part])
+        off += part
+        if part == 0:
+            break
+    return MD5Final(None, ctx)
+
+
+# ---------------------------------------------------------------- device batches
+def _need_cuda(t, what):
+    if torch is None or not isinstance(t, torch.Tensor):
+        raise TypeError(f"{what} must be a torch tensor on a HIP device")
+    if not t.is_cuda:
+        raise ValueError(f"{what} is on {t.device}; the batched MD5 runs only on the GPU")
+    if not t.is_contiguous():
+        raise ValueError(f"{what} must be contiguous")
+
+
+def _stream(stream):
+    if stream is None:
+        return torch.cuda.current_stream().cuda_stream
+    return getattr(stream, "cuda_stream", stream)
+
+
+def digest_fixed(data, n: int = None, length: int = None, stride: int = None, out=None,
+                 stream=None, variant=AUTO):
+    """digest[i] = MD5(data_bytes[i*stride : i*stride + length]).
+
+    ``data`` is a contiguous uint8 CUDA tensor; with ``n``/``length`` omitted it
+    must be 2-D [n, length]."""
+    _need_cuda(data, "data")
+    if data.dtype != torch.uint8:
+        raise TypeError("data must be uint8")
+    if n is None or length is None:
+        if data.dim() != 2:
+            raise ValueError("pass n and length, or a 2-D [n, length] tensor")
+        n, length = data.shape
+    stride = length if stride is None else stride
+    if n and (n - 1) * stride + length > data.numel():
+        raise ValueError("batch extends past the end of `data`")
+    if out is None:
+        out = torch.empty((n, 16), dtype=torch.uint8, device=data.device)
+    _need_cuda(out, "out")
+    if isinstance(variant, str):
+        variant = VARIANTS[variant]
+    rc = lib().md5hip_digest_fixed_variant(data.data_ptr(), n, length, stride, out.data_ptr(),
+                                           _stream(stream), variant)
+    check("md5hip_digest_fixed_variant", rc)
+    return out
+
+
+def digest_desc(base, offsets, lens, order=None, out=None, stream=None):
+    """digest[i] = MD5(base_bytes[offsets[i] : offsets[i] + lens[i]])."""
+    _need_cuda(base, "base")
+    _need_cuda(offsets, "offsets")
+    _need_cuda(lens, "lens")
+    if offsets.dtype != torch.int64 or lens.dtype not in (torch.int32, torch.uint32):
+        raise TypeError("offsets must be int64 and lens int32")
+    n = offsets.numel()
+    if lens.numel() != n:
+        raise ValueError("offsets and lens differ in length")
+    if order is not None:
+        _need_cuda(order, "order")
+        if order.numel() != n or order.dtype not in (torch.int32, torch.uint32):
+            raise ValueError("order must be an int32 permutation of range(n)")
+    if out is None:
+        out = torch.empty((n, 16), dtype=torch.uint8, device=base.device)
+    rc = lib().md5hip_digest_desc(base.data_ptr(), offsets.data_ptr(), lens.data_ptr(),
+                                  order.data_ptr() if order is not None else None, n,
+                                  out.data_ptr(), _stream(stream))
+    check("md5hip_digest_desc", rc)
+    return out
+
+
+def plan_order(lens) -> np.ndarray:
+    """Longest-first lane order (md5hip_plan_order), host arrays."""
+    L = np.ascontiguousarray(lens, dtype=np.uint32)
+    order = np.empty(max(L.size, 1), dtype=np.uint32)
+    check("md5hip_plan_order", lib().md5hip_plan_order(L.ctypes.data, L.size, order.ctypes.data))
+    return order[:L.size]
+
+
+def fill_synthetic(t, seed: int, stream=None):
+    _need_cuda(t, "t")
+    nbytes = t.numel() * t.element_size()
+    check("md5hip_fill_synthetic",
+          lib().md5hip_fill_synthetic(t.data_ptr(), nbytes, seed & (2**64 - 1), _stream(stream)))
+    return t
+
+
+def variant_name(v: int) -> str:
+    return lib().md5hip_variant_name(v).decode()
+
+
+def resolve_variant(v=AUTO) -> int:
+    """The concrete kernel variant that `v` (AUTO by default) runs."""
+    if isinstance(v, str):
+        v = VARIANTS[v]
+    return lib().md5hip_resolve_variant(v)
+
+
+# ---------------------------------------------------------------- host batches
+class Batcher:
+    """Host-memory batched submit (include/md5hip.h md5hip_batcher_*)."""
+
+    def __init__(self, device: int = 0, slice_bytes: int = 64 << 20, nslots: int = 3):
+        h = ctypes.c_void_p()
+        check("md5hip_batcher_create", lib().md5hip_batcher_create(device, slice_bytes, nslots,
+                                                                    ctypes.byref(h)))
+        self._h = h
+
+    def close(self):
+        if self._h:
+            lib().md5hip_batcher_destroy(self._h)
+            self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def submit(self, buffers) -> np.ndarray:
+        """digests[i] = MD5(buffers[i]) for a list of bytes-like host buffers."""
+        n = len(buffers)
+        keep, ptrs = [], (ctypes.c_void_p * max(n, 1))()
+        lens = np.empty(max(n, 1), dtype=np.uint32)
+        for i, b in enumerate(buffers):
+            a, k = _addr(b)
+            keep.append(k)
+            ptrs[i] = a
+            lens[i] = memoryview(b).nbytes
+        out = np.empty((max(n, 1), 16), dtype=np.uint8)
+        check("md5_batch_submit", lib().md5_batch_submit(self._h, ptrs, lens.ctypes.data, n,
+                                                          out.ctypes.data))
+        return out[:n]
+
+    def host_fixed(self, arr: np.ndarray, n: int, length: int, stride: int = None) -> np.ndarray:
+        stride = length if stride is None else stride
+        a = np.ascontiguousarray(arr).view(np.uint8).reshape(-1)
+        if n and (n - 1) * stride + length > a.size:
+            raise ValueError("batch extends past the end of the buffer")
+        out = np.empty((max(n, 1), 16), dtype=np.uint8)
+        check("md5hip_batch_host_fixed",
+              lib().md5hip_batch_host_fixed(self._h, a.ctypes.data, n, length, stride, out.ctypes.data))
+        return out[:n]
+
+
+__all__ = ["MD5Context", "MD5Init", "MD5Update", "MD5Final", "MD5_DIGEST_SIZE", "MD5HipError",
+           "md5", "digest_fixed", "digest_desc", "plan_order", "fill_synthetic", "Batcher",
+           "variant_name", "resolve_variant", "VARIANTS"]

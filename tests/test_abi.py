@@ -1,0 +1,146 @@
+"""The C-ABI boundary on CPU: libmd5hip.so loads, exports every symbol that
+include/*.h declares, keeps md5.h's struct layout, the per-message
+MD5Init/Update/Final entries (host path by design, include/md5.h) match the
+golden vectors, and argument errors come back as -errno before any device
+work is attempted."""
+import ctypes
+import errno
+import os
+import re
+import subprocess
+
+import numpy as np
+
+import gen
+from sproxy_amd import _lib
+from sproxy_amd import md5 as m
+
+INC = os.path.join(gen.REPO, "include")
+
+
+def declared_functions():
+    names = set()
+    for h in ("md5.h", "md5hip.h"):
+        text = open(os.path.join(INC, h)).read()
+        text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+        for mm in re.finditer(r"^\s*(?:const\s+)?[\w\s\*]+?\b(\w+)\s*\(", text, flags=re.M):
+            name = mm.group(1)
+            if name not in ("if", "sizeof", "defined"):
+                names.add(name)
+    return names
+
+
+def test_exports_every_declared_symbol():
+    decl = declared_functions()
+    assert {"MD5Init", "MD5Update", "MD5Final", "md5hip_digest_fixed", "md5_batch_submit"} <= decl
+    out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True,
+                         text=True, check=True).stdout
+    exported = {ln.split()[-1] for ln in out.splitlines() if " T " in ln}
+    missing = decl - exported
+    assert not missing, missing
+    assert set(_lib.EXPORTS) == decl
+    _lib.lib()   # binds every signature
+
+
+def test_abi_version_and_names():
+    L = _lib.lib()
+    assert L.md5hip_abi_version() == 1
+    assert [m.variant_name(v) for v in range(5)] == ["auto", "direct2", "direct4", "lds64", "lds128"]
+
+
+def test_header_compiles_as_c_and_layout():
+    src = r'''
+    #include <stddef.h>
+    #include "md5.h"
+    #include "md5hip.h"
+    _Static_assert(sizeof(struct MD5Context) == 88, "size");
+    _Static_assert(offsetof(struct MD5Context, bits) == 16, "bits");
+    _Static_assert(offsetof(struct MD5Context, in) == 24, "in");
+    int main(void) { return MD5_DIGEST_SIZE == 16 ? 0 : 1; }
+    '''
+    exe = os.path.join(gen.REPO, "build", "hdrcheck")
+    os.makedirs(os.path.dirname(exe), exist_ok=True)
+    subprocess.run(["gcc", "-std=c99", "-Wall", "-Werror", "-I", INC, "-x", "c", "-", "-o", exe],
+                   input=src, text=True, check=True)
+    assert subprocess.run([exe]).returncode == 0
+    assert ctypes.sizeof(_lib.MD5Context) == 88
+
+
+def test_streaming_api_matches_golden(golden):
+    for v in golden["kat"]:
+        msg = bytes.fromhex(v["hex"])
+        ctx = m.MD5Context()
+        m.MD5Init(ctx)
+        cut = len(msg) // 3
+        m.MD5Update(ctx, msg[:cut])
+        m.MD5Update(ctx, msg[cut:])
+        digest = bytearray(16)
+        assert m.MD5Final(digest, ctx).hex() == v["md5"] == digest.hex()
+        assert bytes(ctx) == b"\0" * 88          # md5.c:264
+    e = golden["edge"]
+    big = gen.mul_pattern(max(e["lengths"]))
+    for L, d in zip(e["lengths"], e["md5"]):
+        assert m.md5(big[:L]).hex() == d
+
+
+def test_streaming_api_random_splits(golden):
+    r = golden["random_lengths"]
+    data = gen.xorshift_bytes(max(r["lengths"]), seed=0x243F6A8885A308D3)
+    rng = np.random.default_rng(5)
+    for L, d in zip(r["lengths"], r["md5"]):
+        ctx = m.MD5Context()
+        m.MD5Init(ctx)
+        cuts = sorted(int(x) for x in rng.integers(0, L + 1, 4))
+        prev = 0
+        for c in cuts + [L]:
+            m.MD5Update(ctx, data[prev:c])
+            prev = c
+        assert m.MD5Final(None, ctx).hex() == d
+
+
+def test_bitcount_carry():
+    """bits[0] wraps at 2^32 bits (512 MiB) and carries into bits[1] (md5.c:179-182)."""
+    ctx = m.MD5Context()
+    m.MD5Init(ctx)
+    ctx.bits[0] = 0xFFFFFFF8
+    m.MD5Update(ctx, b"abc")
+    assert ctx.bits[0] == (0xFFFFFFF8 + 24) & 0xFFFFFFFF and ctx.bits[1] == 1
+
+
+def test_argument_errors_before_device_work():
+    L = _lib.lib()
+    EINVAL = -errno.EINVAL
+    assert L.md5hip_digest_fixed(None, 0, 16, 16, None, None) == 0          # empty batch: no-op
+    assert L.md5hip_digest_fixed(None, 5, 16, 16, None, None) == EINVAL
+    assert L.md5hip_digest_fixed(ctypes.c_void_p(16), 5, 32, 16, ctypes.c_void_p(16), None) == EINVAL
+    assert L.md5hip_digest_fixed(ctypes.c_void_p(16), 5, 16, 16, ctypes.c_void_p(8), None) == EINVAL
+    assert L.md5hip_digest_fixed_variant(ctypes.c_void_p(16), 5, 16, 16, ctypes.c_void_p(16), None, 9) == EINVAL
+    assert L.md5hip_digest_desc(None, None, None, None, 0, None, None) == 0
+    assert L.md5hip_digest_desc(None, None, None, None, 3, None, None) == EINVAL
+    assert L.md5hip_fill_synthetic(ctypes.c_void_p(16), 15, 1, None) == EINVAL
+    h = ctypes.c_void_p()
+    assert L.md5hip_batcher_create(0, 1 << 20, 99, ctypes.byref(h)) == EINVAL
+    assert L.md5_batch_submit(None, None, None, 1, None) == EINVAL
+
+
+def test_plan_order_longest_first():
+    rng = np.random.default_rng(1)
+    lens = rng.integers(0, 1 << 20, 5000).astype(np.uint32)
+    order = m.plan_order(lens)
+    assert sorted(order.tolist()) == list(range(5000))
+    blocks = (lens[order] >> 6)
+    assert np.all(np.diff(blocks.astype(np.int64)) <= 0)
+    # stable within equal block counts
+    for b in np.unique(blocks)[:50]:
+        idx = order[blocks == b]
+        assert np.all(np.diff(idx.astype(np.int64)) > 0)
+    huge = np.array([0xFFFFFFFF, 5, 1 << 31, 64], dtype=np.uint32)   # comparison-sort path
+    assert m.plan_order(huge).tolist() == [0, 2, 3, 1]
+    assert m.plan_order(np.array([], dtype=np.uint32)).size == 0
+
+
+def test_device_api_rejects_host_tensors():
+    import pytest
+    import torch
+    with pytest.raises(ValueError):
+        m.digest_fixed(torch.zeros((4, 64), dtype=torch.uint8))
