@@ -1,0 +1,78 @@
+#!/usr/bin/env python3
+"""Times every batched-MD5 kernel variant and the diagnostic ceilings
+(build/diag/libmd5hip_diag.so) on the C2 workload, interleaved in one process
+(cdna_hip_programming.md §5.4 rule 24).  Prints one JSON object.
+
+    python scripts/profile_kernels.py [--rounds R] [--chunks N] [--len L] [--only NAMES]
+
+Also the driver for rocprofv3 passes (scripts/gpu_profile.sh)."""
+import argparse
+import ctypes
+import json
+import os
+import sys
+
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+from sproxy_amd import md5 as m  # noqa: E402
+
+DIAG = ctypes.CDLL(os.path.join(REPO, "build", "diag", "libmd5hip_diag.so"))
+DIAG.md5diag_run.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32,
+                             ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p]
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--rounds", type=int, default=5)
+    p.add_argument("--reps", type=int, default=3)
+    p.add_argument("--chunks", type=int, default=1 << 20)
+    p.add_argument("--len", type=int, default=16384)
+    p.add_argument("--only", default="")
+    a = p.parse_args()
+    n, L = a.chunks, a.len
+    data = torch.empty(n * L, dtype=torch.uint8, device="cuda")
+    m.fill_synthetic(data, seed=1)
+    out = torch.empty((max(n, 8192 * 256), 16), dtype=torch.uint8, device="cuda")
+    stream = torch.cuda.current_stream()
+
+    def prod(v):
+        return lambda: m.digest_fixed(data, n, L, out=out[:n], variant=v)
+
+    def diag(kind):
+        def f():
+            rc = DIAG.md5diag_run(kind, data.data_ptr(), n, L, L, out.data_ptr(), stream.cuda_stream)
+            assert rc == 0, rc
+        return f
+
+    cases = {"direct2": prod("direct2"), "direct4": prod("direct4"), "lds64": prod("lds64"),
+             "lds128": prod("lds128"), "compute_only": diag(0), "load_direct2": diag(1),
+             "load_direct4": diag(2), "load_lds64": diag(3), "load_lds128": diag(4),
+             "stream_read": diag(5)}
+    if a.only:
+        cases = {k: v for k, v in cases.items() if k in a.only.split(",")}
+    times = {k: [] for k in cases}
+    for f in cases.values():
+        f()
+    torch.cuda.synchronize()
+    for _ in range(a.rounds):
+        for k, f in cases.items():
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            for _ in range(a.reps):
+                f()
+            e1.record(stream)
+            torch.cuda.synchronize()
+            times[k].append(e0.elapsed_time(e1) / a.reps)
+    res = {}
+    for k, t in times.items():
+        t = sorted(t)
+        med = t[len(t) // 2]
+        res[k] = {"ms_median": round(med, 4), "ms_min": round(t[0], 4),
+                  "payload_GBps": round(n * L / med / 1e6, 1)}
+    print(json.dumps({"chunks": n, "len": L, "results": res}))
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,344 @@
+// md5_kernels.h -- batched MD5 over independent chunks, hand-written for gfx950.
+//
+// One lane hashes one chunk (MD5 is a strict 64-step chain per block, so the
+// only parallelism is across chunks).  A 64-lane wave owns 64 chunks.  What
+// differs between the kernels is how message blocks travel HBM -> VGPRs:
+//
+//   md5_fixed_direct  each lane streams its own chunk with global_load_dwordx4
+//                     (4 per 64-B block), a D-deep register ring in flight.
+//   md5_fixed_lds     the wave fetches its 64 chunks' next block(s) with
+//                     LDS-DMA (global_load_lds_dwordx4: 4 or 8 lanes per chunk,
+//                     so each wave-instruction reads whole 64/128-B runs), then
+//                     every lane pulls its own row out of LDS with ds_read_b128.
+//                     Source-side XOR swizzle keeps the row reads conflict-free.
+//   md5_desc          per-chunk (offset, length) descriptors, optional
+//                     permutation (longest-first packing), any alignment.
+//
+// Reference semantics: md5.c:153-265 (Init/Update/Final) applied to each chunk
+// independently; digests are bit-exact with md5.c (tests/test_gpu_parity.py).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "md5_core.h"
+
+namespace md5hip {
+
+// ---------------------------------------------------------------------------
+// Final block(s): the r = len % 64 trailing bytes at `tail` (16-B aligned when
+// `aligned`), then 0x80, zeros, and the 64-bit bit count (md5.c:221-261).
+// Only granules that hold message bytes are read; a 16-B granule never
+// crosses a page, so reading its bytes past `len` cannot fault.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t keep_bytes(uint32_t w, int nbytes) {
+  // keep the low `nbytes` (0..4) bytes of w
+  return nbytes >= 4 ? w : nbytes <= 0 ? 0u : (w & ((1u << (8 * nbytes)) - 1u));
+}
+
+__device__ __forceinline__ void finish_message(State& st, const uint8_t* tail, uint32_t r,
+                                               uint64_t len_bytes) {
+  const uint32_t bits_lo = (uint32_t)(len_bytes << 3);
+  const uint32_t bits_hi = (uint32_t)(len_bytes >> 29);
+  if (r == 0) {
+    compress_pad_only(st, bits_lo, bits_hi);
+    return;
+  }
+  uint32_t w[16];
+  const uintptr_t addr = (uintptr_t)tail;
+  if ((addr & 15u) == 0) {
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      uint4 q = make_uint4(0, 0, 0, 0);
+      if ((uint32_t)g * 16u < r) q = *reinterpret_cast<const uint4*>(tail + 16 * g);
+      w[4 * g + 0] = q.x; w[4 * g + 1] = q.y; w[4 * g + 2] = q.z; w[4 * g + 3] = q.w;
+    }
+  } else {
+    // unaligned tail: aligned dword loads + funnel shift (v_alignbit_b32)
+    const uint32_t* base = reinterpret_cast<const uint32_t*>(addr & ~(uintptr_t)3);
+    const uint32_t sh = (uint32_t)(addr & 3u) * 8u;
+    const uint32_t nwords = (((uint32_t)(addr & 3u)) + r + 3u) >> 2;   // words touched
+    uint32_t prev = base[0];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      uint32_t next = ((uint32_t)j + 1u < nwords) ? base[j + 1] : 0u;
+      w[j] = __builtin_amdgcn_alignbit(next, prev, sh);
+      prev = next;
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    w[j] = keep_bytes(w[j], (int)r - 4 * j);
+    if ((uint32_t)j == (r >> 2)) w[j] |= 0x80u << (8 * (r & 3u));
+  }
+  if (r < 56) {
+    w[14] = bits_lo;
+    w[15] = bits_hi;
+    compress(st, [&](int i) __attribute__((always_inline)) { return w[i]; });
+  } else {
+    compress(st, [&](int i) __attribute__((always_inline)) { return w[i]; });
+    compress(st, [&](int i) __attribute__((always_inline)) -> uint32_t {
+      return i == 14 ? bits_lo : i == 15 ? bits_hi : 0u;
+    });
+  }
+}
+
+__device__ __forceinline__ void store_digest(uint4* out, uint64_t idx, const State& st) {
+  out[idx] = make_uint4(st.a, st.b, st.c, st.d);  // md5.c:262-263, LE bytes
+}
+
+// Per-block work.  MODE 0 is the product (MD5 compression); MODE 1 is a
+// diagnostic cheap fold that still consumes all 16 words, used only by the
+// load-path ceiling measurements in md5_diag.hip.
+template <int MODE>
+__device__ __forceinline__ void block_op(State& st, const uint4 (&w)[4]) {
+  if constexpr (MODE == 0) {
+    compress_regs(st, w);
+  } else {
+    st.a ^= w[0].x ^ w[0].y ^ w[0].z ^ w[0].w;
+    st.b ^= w[1].x ^ w[1].y ^ w[1].z ^ w[1].w;
+    st.c ^= w[2].x ^ w[2].y ^ w[2].z ^ w[2].w;
+    st.d ^= w[3].x ^ w[3].y ^ w[3].z ^ w[3].w;
+  }
+}
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ uint4 ld16(const uint4* p) {
+  const u32x4 v = *reinterpret_cast<const u32x4*>(p);
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+
+__device__ __forceinline__ void load_block(uint4 (&r)[4], const uint4* p) {
+#pragma unroll
+  for (int k = 0; k < 4; ++k) r[k] = ld16(p + k);
+}
+
+// ---------------------------------------------------------------------------
+// Fixed-length, lane-direct loads.  base/stride 16-B aligned, len <= stride.
+// ---------------------------------------------------------------------------
+template <int D, int MODE = 0>
+__global__ void __launch_bounds__(256)
+md5_fixed_direct(const uint8_t* __restrict__ base, uint64_t n, uint32_t len, uint64_t stride,
+                 uint4* __restrict__ out) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint8_t* chunk = base + i * stride;
+  const uint4* p = reinterpret_cast<const uint4*>(chunk);
+  const uint32_t nfull = len >> 6;
+  State st = initial_state();
+  if (nfull) {
+    // D-deep register ring.  Prefetch indices are clamped to the last block so
+    // every load is unconditional (no phi copies); the <= D re-reads at the end
+    // hit in L1/L2.
+    const uint32_t lastb = nfull - 1;
+    uint4 R[D][4];
+#pragma unroll
+    for (int j = 0; j < D; ++j) load_block(R[j], p + 4 * min((uint32_t)j, lastb));
+    uint32_t blk = 0;
+    for (; blk + D <= nfull; blk += D) {   // steady state: no conditionals, so
+#pragma unroll                              // the waits stay counted (vmcnt(4*(D-1)))
+      for (int j = 0; j < D; ++j) {
+        block_op<MODE>(st, R[j]);
+        load_block(R[j], p + 4 * min(blk + j + D, lastb));
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < D - 1; ++j)
+      if (blk + j < nfull) block_op<MODE>(st, R[j]);
+  }
+  finish_message(st, chunk + ((uint64_t)nfull << 6), len & 63u, len);
+  store_digest(out, i, st);
+}
+
+// ---------------------------------------------------------------------------
+// Fixed-length, wave-cooperative LDS-DMA staging (two stage buffers per wave).
+//   BB  bytes per chunk per stage (64 = one block, 128 = two blocks = one
+//       128-B line per chunk per stage)
+// LDS image of one stage: row L (= lane L's chunk) of BB bytes; 16-B slot q of
+// row L holds part q ^ g(L), g(L) = (L >> 2) & 3 for BB=64, (L >> 1) & 7 for
+// BB=128 -- distinct over every ds_read_b128 lane group (MI355X_MICROARCH §LDS),
+// so the row reads are conflict-free.  The swizzle is applied on the SOURCE
+// address because the DMA destination is lane-linear.
+// Order per stage: wait stage s -> ds_read it into VGPRs -> issue DMA of stage
+// s+1 into the other buffer -> compress.  Exactly one stage is in flight when
+// the explicit vmcnt(0) guards the next ds_read.
+// ---------------------------------------------------------------------------
+template <int BB>
+__device__ __forceinline__ uint32_t swz(uint32_t row) {
+  return BB == 64 ? ((row >> 2) & 3u) : ((row >> 1) & 7u);
+}
+
+template <int BB, int MODE = 0>
+__device__ __forceinline__ void fixed_lds_body(const uint8_t* __restrict__ base, uint64_t n,
+                                               uint32_t len, uint64_t stride,
+                                               uint4* __restrict__ out, uint8_t* lds) {
+  constexpr int LPC = BB / 16;         // lanes per chunk in one DMA instruction
+  constexpr int CPI = 64 / LPC;        // chunks per DMA instruction
+  constexpr int NI = 64 / CPI;         // DMA instructions per stage
+  constexpr int BPS = BB / 64;         // blocks per stage
+  constexpr int STAGE = 64 * BB;       // bytes per stage per wave
+
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t wave = threadIdx.x >> 6;
+  uint8_t* ring = lds + (size_t)wave * 2 * STAGE;
+  const uint64_t wave_first = ((uint64_t)blockIdx.x * blockDim.x) + wave * 64u;
+  if (wave_first >= n) return;         // whole wave out of range (wave-uniform)
+  const uint64_t last = n - 1;
+
+  const uint8_t* src[NI];
+#pragma unroll
+  for (int r = 0; r < NI; ++r) {
+    const uint32_t row = (uint32_t)r * CPI + lane / LPC;
+    const uint32_t q = lane % LPC;
+    const uint32_t part = q ^ (swz<BB>(row) & (LPC - 1));
+    uint64_t c = wave_first + row;
+    c = c > last ? last : c;           // tail lanes re-read the last chunk
+    src[r] = base + c * stride + part * 16u;
+  }
+  const uint32_t nfull = len >> 6;
+  const uint32_t nstage = nfull / BPS;   // whole stages; leftovers go direct
+
+  auto issue = [&](uint32_t stg) __attribute__((always_inline)) {
+    uint8_t* dst = ring + (stg & 1u) * STAGE;
+#pragma unroll
+    for (int r = 0; r < NI; ++r)
+      __builtin_amdgcn_global_load_lds(src[r] + (size_t)stg * BB, dst + r * 1024, 16, 0, 0);
+  };
+
+  State st = initial_state();
+  if (nstage) issue(0);
+  const uint32_t g = swz<BB>(lane) & (LPC - 1);
+  for (uint32_t stg = 0; stg < nstage; ++stg) {
+    const uint8_t* row = ring + (stg & 1u) * STAGE + lane * BB;
+    // The compiler does not reliably order ds_read after an LDS-DMA into the
+    // same bytes (it emitted no wait at all for BB=64), so wait explicitly:
+    // exactly one stage is in flight here, so vmcnt(0) costs no overlap.
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    uint4 w[BPS][4];
+#pragma unroll
+    for (int b = 0; b < BPS; ++b)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const uint32_t q = ((uint32_t)(b * 4 + k)) ^ g;
+        w[b][k] = *reinterpret_cast<const uint4*>(row + q * 16u);
+      }
+    if (stg + 1 < nstage) issue(stg + 1);
+#pragma unroll
+    for (int b = 0; b < BPS; ++b) block_op<MODE>(st, w[b]);
+  }
+  // leftover whole blocks (nfull % BPS), then the tail
+  const uint64_t i = wave_first + lane;
+  const uint64_t ci = i > last ? last : i;
+  const uint8_t* chunk = base + ci * stride;
+  for (uint32_t blk = nstage * BPS; blk < nfull; ++blk) {
+    uint4 w[4];
+    load_block(w, reinterpret_cast<const uint4*>(chunk + ((uint64_t)blk << 6)));
+    compress_regs(st, w);
+  }
+  finish_message(st, chunk + ((uint64_t)nfull << 6), len & 63u, len);
+  if (i <= last) store_digest(out, i, st);
+}
+
+// Non-template entry points (hipcc mis-handles explicitly instantiated
+// __global__ templates that declare extern __shared__).
+__global__ void __launch_bounds__(256)
+md5_fixed_lds64(const uint8_t* __restrict__ base, uint64_t n, uint32_t len, uint64_t stride,
+                uint4* __restrict__ out) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds_dyn[];
+  fixed_lds_body<64>(base, n, len, stride, out, lds_dyn);
+}
+
+__global__ void __launch_bounds__(256)
+md5_fixed_lds128(const uint8_t* __restrict__ base, uint64_t n, uint32_t len, uint64_t stride,
+                 uint4* __restrict__ out) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds_dyn[];
+  fixed_lds_body<128>(base, n, len, stride, out, lds_dyn);
+}
+
+// ---------------------------------------------------------------------------
+// Descriptor batch: chunk c = order ? order[i] : i at base + offs[c], lens[c].
+// Per-lane trip counts differ, so the host packs lanes longest-first
+// (md5hip_plan_order).  Lanes whose chunk start is 16-B aligned stream it
+// with dwordx4 loads through a 2-block ring; unaligned chunks take aligned
+// dword loads + v_alignbit_b32 (17 loads per block).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void load_block_unaligned(uint4 (&r)[4], const uint8_t* p) {
+  const uintptr_t addr = (uintptr_t)p;
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(addr & ~(uintptr_t)3);
+  const uint32_t sh = (uint32_t)(addr & 3u) * 8u;
+  uint32_t v[17];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) v[j] = w[j];
+  // The 17th word starts at addr - sh/8 + 64 < addr + 64 <= chunk end only when
+  // sh != 0; with sh == 0 it would lie past the block and is not needed.
+  v[16] = sh ? w[16] : 0u;
+  uint32_t o[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) o[j] = __builtin_amdgcn_alignbit(v[j + 1], v[j], sh);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) r[k] = make_uint4(o[4 * k], o[4 * k + 1], o[4 * k + 2], o[4 * k + 3]);
+}
+
+// kImplicit: chunk i at base + i*stride with length `flen` (the fixed-length
+// API's fallback for chunk starts that are not 16-B aligned).
+template <bool kImplicit>
+__global__ void __launch_bounds__(256)
+md5_desc(const uint8_t* __restrict__ base, const uint64_t* __restrict__ offs,
+         const uint32_t* __restrict__ lens, const uint32_t* __restrict__ order, uint64_t n,
+         uint64_t stride, uint32_t flen, uint4* __restrict__ out) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t c = (!kImplicit && order) ? (uint64_t)order[i] : i;
+  const uint8_t* chunk = base + (kImplicit ? c * stride : offs[c]);
+  const uint32_t len = kImplicit ? flen : lens[c];
+  const uint32_t nfull = len >> 6;
+  State st = initial_state();
+  if (((uintptr_t)chunk & 15u) == 0) {
+    const uint4* p = reinterpret_cast<const uint4*>(chunk);
+    if (nfull) {
+      const uint32_t lastb = nfull - 1;
+      uint4 R0[4], R1[4];
+      load_block(R0, p);
+      load_block(R1, p + 4 * min(1u, lastb));
+      uint32_t blk = 0;
+      for (; blk + 2 <= nfull; blk += 2) {
+        compress_regs(st, R0);
+        load_block(R0, p + 4 * min(blk + 2, lastb));
+        compress_regs(st, R1);
+        load_block(R1, p + 4 * min(blk + 3, lastb));
+      }
+      if (blk < nfull) compress_regs(st, R0);
+    }
+  } else {
+    for (uint32_t blk = 0; blk < nfull; ++blk) {
+      uint4 w[4];
+      load_block_unaligned(w, chunk + ((uint64_t)blk << 6));
+      compress_regs(st, w);
+    }
+  }
+  finish_message(st, chunk + ((uint64_t)nfull << 6), len & 63u, len);
+  store_digest(out, c, st);
+}
+
+// ---------------------------------------------------------------------------
+// Synthetic data: 32-bit word i of the buffer = mix32(seed, i) (a splitmix64
+// finaliser).  tests/gen.py has the numpy mirror.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t mix32(uint64_t seed, uint64_t i) {
+  uint64_t z = seed + (i + 1) * 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return (uint32_t)(z ^ (z >> 31));
+}
+
+__global__ void __launch_bounds__(256)
+fill_synthetic(uint4* __restrict__ dst, uint64_t n16, uint64_t seed) {
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += stride) {
+    const uint64_t w = 4 * i;
+    dst[i] = make_uint4(mix32(seed, w), mix32(seed, w + 1), mix32(seed, w + 2), mix32(seed, w + 3));
+  }
+}
+
+}  // namespace md5hip
+
