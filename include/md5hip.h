@@ -39,7 +39,9 @@ enum md5hip_variant {
     MD5HIP_DIRECT4 = 2,     /* lane-direct dwordx4 loads, 4-block register ring */
     MD5HIP_LDS64 = 3,       /* wave LDS-DMA staging, 64 B per chunk per stage */
     MD5HIP_LDS128 = 4,      /* wave LDS-DMA staging, 128 B per chunk per stage */
-    MD5HIP_NUM_VARIANTS = 5
+    MD5HIP_XPOSE1 = 5,      /* coalesced buffer loads, LDS transpose, 1 stage ahead */
+    MD5HIP_XPOSE2 = 6,      /* same, 2 stages ahead */
+    MD5HIP_NUM_VARIANTS = 7
 };
 
 int md5hip_abi_version(void);

@@ -49,7 +49,8 @@ def main():
     cases = {"direct2": prod("direct2"), "direct4": prod("direct4"), "lds64": prod("lds64"),
              "lds128": prod("lds128"), "compute_only": diag(0), "load_direct2": diag(1),
              "load_direct4": diag(2), "load_lds64": diag(3), "load_lds128": diag(4),
-             "stream_read": diag(5)}
+             "stream_read": diag(5), "xpose1": prod("xpose1"), "xpose2": prod("xpose2"),
+             "load_xpose1": diag(6), "load_xpose2": diag(7)}
     if a.only:
         cases = {k: v for k, v in cases.items() if k in a.only.split(",")}
     times = {k: [] for k in cases}

@@ -32,6 +32,20 @@ diag_lds128_load(const uint8_t* __restrict__ base, uint64_t n, uint32_t len, uin
   fixed_lds_body<128, 1>(base, n, len, stride, out, lds_dyn);
 }
 
+__global__ void __launch_bounds__(256)
+diag_xpose1_load(const uint8_t* __restrict__ base, uint64_t n, uint32_t len, uint64_t stride,
+                 uint4* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) uint8_t img[4 * 8192];
+  fixed_xpose_body<1, 1>(base, n, len, stride, out, img);
+}
+
+__global__ void __launch_bounds__(256)
+diag_xpose2_load(const uint8_t* __restrict__ base, uint64_t n, uint32_t len, uint64_t stride,
+                 uint4* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) uint8_t img[4 * 8192];
+  fixed_xpose_body<2, 1>(base, n, len, stride, out, img);
+}
+
 // Compute only: lane L hashes `nblocks` blocks whose words it re-reads from its
 // own 64-B LDS row every block (ds_read_b128 x4, like lds64), then the pad block.
 __global__ void __launch_bounds__(256)
@@ -108,6 +122,12 @@ extern "C" int md5diag_run(int kind, const void* base, uint64_t n, uint32_t len,
                          (const uint4*)b, n * (uint64_t)len / 16, o);
       break;
     }
+    case 6:
+      hipLaunchKernelGGL(diag_xpose1_load, dim3(grid), dim3(256), 0, s, b, n, len, stride, o);
+      break;
+    case 7:
+      hipLaunchKernelGGL(diag_xpose2_load, dim3(grid), dim3(256), 0, s, b, n, len, stride, o);
+      break;
     default:
       return -EINVAL;
   }

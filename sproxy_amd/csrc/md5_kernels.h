@@ -239,6 +239,98 @@ __device__ __forceinline__ void fixed_lds_body(const uint8_t* __restrict__ base,
   if (i <= last) store_digest(out, i, st);
 }
 
+// ---------------------------------------------------------------------------
+// Fixed-length, register-staged transpose ("xpose").
+// Each wave-instruction loads 8 chunks x 128 B (8 lanes per 128-B line) with
+// buffer_load_dwordx4 -- one wave-uniform buffer descriptor per 64-chunk group,
+// a per-(lane, instruction) 32-bit voffset fixed for the whole kernel, and the
+// stage offset in the scalar soffset, so the steady state spends no VALU on
+// addressing.  Loads run D stages (D x 128 B per chunk) ahead in VGPRs; per
+// stage the wave writes its 8 KiB image to LDS (ds_write_b128, conflict-free:
+// 8 lanes cover one 128-B row) and each lane reads back its own row
+// (ds_read_b128, source-swizzled as in md5_fixed_lds so the 16-lane groups hit
+// distinct 16-B slots).  LDS is only a per-wave transpose buffer (8 KiB), so
+// occupancy is set by VGPRs, not LDS, and all waits are compiler-counted.
+// Requires 64 * stride < 2^31 (checked by the launcher).
+// ---------------------------------------------------------------------------
+template <int D, int MODE = 0>
+__device__ __forceinline__ void fixed_xpose_body(const uint8_t* __restrict__ base, uint64_t n,
+                                                 uint32_t len, uint64_t stride,
+                                                 uint4* __restrict__ out, uint8_t* lds) {
+  const uint32_t lane = threadIdx.x & 63u;
+  // readfirstlane: the descriptor must be provably wave-uniform, or hipcc
+  // wraps every buffer load in a waterfall loop (cdna_hip_programming.md T20)
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  uint8_t* img = lds + (size_t)wave * 8192;
+  const uint64_t wave_first = ((uint64_t)blockIdx.x * blockDim.x) + wave * 64u;
+  if (wave_first >= n) return;
+  const uint64_t left = n - wave_first;
+  const uint32_t rows = left < 64 ? (uint32_t)left : 64u;
+  const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint8_t*>(base + wave_first * stride), (short)0, 0x7FFFFFFF, 0x00020000);
+  uint32_t voff[8];
+#pragma unroll
+  for (int r = 0; r < 8; ++r) {
+    const uint32_t row = (uint32_t)r * 8u + (lane >> 3);
+    const uint32_t rc = row < rows ? row : rows - 1u;          // ragged last wave
+    const uint32_t part = (lane & 7u) ^ ((row >> 1) & 7u);       // source swizzle
+    voff[r] = rc * (uint32_t)stride + part * 16u;
+  }
+  const uint32_t g = (lane >> 1) & 7u;
+  const uint32_t nfull = len >> 6;
+  const uint32_t nstage = nfull >> 1;                 // 128-B stages
+  State st = initial_state();
+
+  auto load_stage = [&](u32x4 (&R)[8], uint32_t stg) __attribute__((always_inline)) {
+#pragma unroll
+    for (int r = 0; r < 8; ++r)
+      R[r] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, (int)voff[r], (int)(stg * 128u), 0);
+  };
+  auto consume = [&](u32x4 (&R)[8], uint32_t next) __attribute__((always_inline)) {
+#pragma unroll
+    for (int r = 0; r < 8; ++r)
+      *reinterpret_cast<u32x4*>(img + r * 1024 + lane * 16) = R[r];
+    __builtin_amdgcn_wave_barrier();
+    uint4 w[2][4];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const u32x4 v = *reinterpret_cast<const u32x4*>(img + lane * 128 + ((q ^ g) * 16));
+      w[q >> 2][q & 3] = make_uint4(v.x, v.y, v.z, v.w);
+    }
+    __builtin_amdgcn_wave_barrier();
+    load_stage(R, next);                              // refill this ring slot
+    __builtin_amdgcn_sched_barrier(0);                // keep the refill ahead of the
+    block_op<MODE>(st, w[0]);                         // compression (hipcc sinks it)
+    block_op<MODE>(st, w[1]);
+  };
+
+  if (nstage) {
+    const uint32_t lasts = nstage - 1;
+    u32x4 R[D][8];
+#pragma unroll
+    for (int j = 0; j < D; ++j) load_stage(R[j], min((uint32_t)j, lasts));
+    uint32_t stg = 0;
+    for (; stg + D <= nstage; stg += D) {
+#pragma unroll
+      for (int j = 0; j < D; ++j) consume(R[j], min(stg + j + D, lasts));
+    }
+#pragma unroll
+    for (int j = 0; j < D - 1; ++j)
+      if (stg + j < nstage) consume(R[j], lasts);
+  }
+  // leftover odd block, then the tail
+  const uint64_t i = wave_first + lane;
+  const uint64_t ci = lane < rows ? i : n - 1;
+  const uint8_t* chunk = base + ci * stride;
+  if (nfull & 1u) {
+    uint4 w[4];
+    load_block(w, reinterpret_cast<const uint4*>(chunk + ((uint64_t)(nfull - 1) << 6)));
+    block_op<MODE>(st, w);
+  }
+  finish_message(st, chunk + ((uint64_t)nfull << 6), len & 63u, len);
+  if (lane < rows) store_digest(out, i, st);
+}
+
 // Non-template entry points (hipcc mis-handles explicitly instantiated
 // __global__ templates that declare extern __shared__).
 __global__ void __launch_bounds__(256)
@@ -246,6 +338,20 @@ md5_fixed_lds64(const uint8_t* __restrict__ base, uint64_t n, uint32_t len, uint
                 uint4* __restrict__ out) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds_dyn[];
   fixed_lds_body<64>(base, n, len, stride, out, lds_dyn);
+}
+
+__global__ void __launch_bounds__(256)
+md5_fixed_xpose1(const uint8_t* __restrict__ base, uint64_t n, uint32_t len, uint64_t stride,
+                 uint4* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) uint8_t img[4 * 8192];
+  fixed_xpose_body<1>(base, n, len, stride, out, img);
+}
+
+__global__ void __launch_bounds__(256)
+md5_fixed_xpose2(const uint8_t* __restrict__ base, uint64_t n, uint32_t len, uint64_t stride,
+                 uint4* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) uint8_t img[4 * 8192];
+  fixed_xpose_body<2>(base, n, len, stride, out, img);
 }
 
 __global__ void __launch_bounds__(256)

@@ -81,6 +81,8 @@ const char* md5hip_variant_name(int v) {
     case MD5HIP_DIRECT4: return "direct4";
     case MD5HIP_LDS64: return "lds64";
     case MD5HIP_LDS128: return "lds128";
+    case MD5HIP_XPOSE1: return "xpose1";
+    case MD5HIP_XPOSE2: return "xpose2";
     default: return "?";
   }
 }
@@ -133,6 +135,19 @@ int md5hip_digest_fixed_variant(const void* d_base, uint64_t n, uint32_t len, ui
       return launch_lds<64>(base, n, len, stride, out, s);
     case MD5HIP_LDS128:
       return launch_lds<128>(base, n, len, stride, out, s);
+    case MD5HIP_XPOSE1:
+    case MD5HIP_XPOSE2:
+      if (stride >= (1ull << 31) / 64) {   // 32-bit buffer offsets per 64-chunk group
+        hipLaunchKernelGGL((md5_fixed_direct<2, 0>), dim3((uint32_t)grid), dim3(kBlock), 0, s,
+                           base, n, len, stride, out);
+      } else if (variant == MD5HIP_XPOSE1) {
+        hipLaunchKernelGGL(md5_fixed_xpose1, dim3((uint32_t)grid), dim3(kBlock), 0, s, base, n,
+                           len, stride, out);
+      } else {
+        hipLaunchKernelGGL(md5_fixed_xpose2, dim3((uint32_t)grid), dim3(kBlock), 0, s, base, n,
+                           len, stride, out);
+      }
+      return launched();
   }
   return -EINVAL;
 }

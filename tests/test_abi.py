@@ -45,7 +45,8 @@ def test_exports_every_declared_symbol():
 def test_abi_version_and_names():
     L = _lib.lib()
     assert L.md5hip_abi_version() == 1
-    assert [m.variant_name(v) for v in range(5)] == ["auto", "direct2", "direct4", "lds64", "lds128"]
+    assert [m.variant_name(v) for v in range(7)] == ["auto", "direct2", "direct4", "lds64", "lds128",
+                                                     "xpose1", "xpose2"]
 
 
 def test_header_compiles_as_c_and_layout():
