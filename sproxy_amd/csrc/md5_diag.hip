@@ -84,6 +84,48 @@ diag_stream_read(const uint4* __restrict__ src, uint64_t n16, uint4* __restrict_
   out[(uint64_t)blockIdx.x * blockDim.x + threadIdx.x] = acc;
 }
 
+// VALU issue-rate probes: 8 independent chains per lane of one instruction
+// kind (asm so nothing folds).  `clk` receives per-wave (s_memtime delta,
+// s_memrealtime delta) for the in-kernel clock (MI355X_MICROARCH DVFS item 6).
+template <int KIND>
+__global__ void __launch_bounds__(256)
+diag_valu_rate(uint32_t iters, uint32_t* __restrict__ out, uint64_t* __restrict__ clk) {
+  uint32_t a[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) a[k] = threadIdx.x * 7u + (uint32_t)k;
+  float f[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) f[k] = (float)a[k];
+  const uint32_t sv = iters ^ blockIdx.x;
+  const uint64_t t0 = __builtin_amdgcn_s_memtime();
+  const uint64_t r0 = __builtin_amdgcn_s_memrealtime();
+  for (uint32_t i = 0; i < iters; ++i) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      if constexpr (KIND == 0)
+        asm volatile("v_add3_u32 %0, %0, %1, %2" : "+v"(a[k]) : "v"(sv), "v"(a[(k + 1) & 7]));
+      else if constexpr (KIND == 1)
+        asm volatile("v_alignbit_b32 %0, %0, %1, 7" : "+v"(a[k]) : "v"(a[(k + 1) & 7]));
+      else if constexpr (KIND == 2)
+        asm volatile("v_add_u32_e32 %0, %0, %1" : "+v"(a[k]) : "v"(a[(k + 1) & 7]));
+      else
+        asm volatile("v_fma_f32 %0, %0, %1, %2" : "+v"(f[k]) : "v"(f[(k + 1) & 7]), "v"(1.0f));
+    }
+  }
+  const uint64_t t1 = __builtin_amdgcn_s_memtime();
+  const uint64_t r1 = __builtin_amdgcn_s_memrealtime();
+  uint32_t x = 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) x ^= a[k] ^ __float_as_uint(f[k]);
+  const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
+  out[gid] = x;
+  if ((threadIdx.x & 63u) == 0) {
+    const uint32_t w = gid >> 6;
+    clk[2 * w] = t1 - t0;
+    clk[2 * w + 1] = r1 - r0;
+  }
+}
+
 }  // namespace md5hip
 
 using namespace md5hip;
@@ -128,6 +170,18 @@ extern "C" int md5diag_run(int kind, const void* base, uint64_t n, uint32_t len,
     case 7:
       hipLaunchKernelGGL(diag_xpose2_load, dim3(grid), dim3(256), 0, s, b, n, len, stride, o);
       break;
+    case 8: case 9: case 10: case 11: {
+      // n = waves to launch (multiple of 4), len = iterations; out needs
+      // 64*n u32 + 2*n u64 (clock pairs after the u32 area)
+      uint32_t* o32 = (uint32_t*)out;
+      uint64_t* clk = (uint64_t*)(o32 + 64 * n);
+      const dim3 g((uint32_t)(n / 4));
+      if (kind == 8) hipLaunchKernelGGL(diag_valu_rate<0>, g, dim3(256), 0, s, len, o32, clk);
+      if (kind == 9) hipLaunchKernelGGL(diag_valu_rate<1>, g, dim3(256), 0, s, len, o32, clk);
+      if (kind == 10) hipLaunchKernelGGL(diag_valu_rate<2>, g, dim3(256), 0, s, len, o32, clk);
+      if (kind == 11) hipLaunchKernelGGL(diag_valu_rate<3>, g, dim3(256), 0, s, len, o32, clk);
+      break;
+    }
     default:
       return -EINVAL;
   }
