@@ -15,9 +15,15 @@ D.md5diag_run.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64, ctypes
                           ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p]
 waves = 256 * 32          # 32 waves per CU
 iters = 20000
+waves = int(sys.argv[1]) if len(sys.argv) > 1 else waves
 buf = torch.zeros(64 * waves * 4 + 2 * waves * 8, dtype=torch.uint8, device="cuda")
 res = {}
-for kind, name in [(8, "v_add3_u32"), (9, "v_alignbit_b32"), (10, "v_add_u32"), (11, "v_fma_f32")]:
+NAMES = ["v_add3_u32(v,v,v)", "v_alignbit_b32(imm)", "v_add_u32_e32", "v_fma_f32", "v_add_u32_e64",
+         "v_add_u32_e32+literal", "v_bitop3_b32", "v_add3_u32(v,v,s)", "v_xor_b32_e32", "v_mov_b32",
+         "v_bfi_b32", "v_lshl_add_u32", "v_lshl_add_u64", "v_alignbit_b32(s)", "v_xad_u32",
+         "v_perm_b32", "v_add_u32_sdwa", "v_and_b32_e32", "v_lshlrev_b32_e32", "v_pk_add_u16"]
+waves = int(sys.argv[1]) if len(sys.argv) > 1 else waves
+for kind, name in [(100 + i, n) for i, n in enumerate(NAMES)]:
     for rep in range(3):
         s = torch.cuda.current_stream()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

@@ -108,8 +108,40 @@ diag_valu_rate(uint32_t iters, uint32_t* __restrict__ out, uint64_t* __restrict_
         asm volatile("v_alignbit_b32 %0, %0, %1, 7" : "+v"(a[k]) : "v"(a[(k + 1) & 7]));
       else if constexpr (KIND == 2)
         asm volatile("v_add_u32_e32 %0, %0, %1" : "+v"(a[k]) : "v"(a[(k + 1) & 7]));
-      else
+      else if constexpr (KIND == 3)
         asm volatile("v_fma_f32 %0, %0, %1, %2" : "+v"(f[k]) : "v"(f[(k + 1) & 7]), "v"(1.0f));
+      else if constexpr (KIND == 4)   // VOP3 encoding of a VOP2 op
+        asm volatile("v_add_u32_e64 %0, %0, %1" : "+v"(a[k]) : "v"(a[(k + 1) & 7]));
+      else if constexpr (KIND == 5)   // VOP2 with 32-bit literal (8-byte encoding)
+        asm volatile("v_add_u32_e32 %0, 0x12345678, %0" : "+v"(a[k]));
+      else if constexpr (KIND == 6)
+        asm volatile("v_bitop3_b32 %0, %0, %1, %2 bitop3:0xca" : "+v"(a[k]) : "v"(a[(k + 1) & 7]), "v"(a[(k + 2) & 7]));
+      else if constexpr (KIND == 7)   // add3 with two VGPR + SGPR
+        asm volatile("v_add3_u32 %0, %0, %1, %2" : "+v"(a[k]) : "v"(a[(k + 1) & 7]), "s"(sv));
+      else if constexpr (KIND == 8)
+        asm volatile("v_xor_b32_e32 %0, %0, %1" : "+v"(a[k]) : "v"(a[(k + 1) & 7]));
+      else if constexpr (KIND == 9)
+        asm volatile("v_mov_b32_e32 %0, %1" : "=v"(a[k]) : "v"(a[(k + 1) & 7]));
+      else if constexpr (KIND == 10)
+        asm volatile("v_bfi_b32 %0, %0, %1, %2" : "+v"(a[k]) : "v"(a[(k + 1) & 7]), "v"(a[(k + 2) & 7]));
+      else if constexpr (KIND == 11)
+        asm volatile("v_lshl_add_u32 %0, %0, 3, %1" : "+v"(a[k]) : "v"(a[(k + 1) & 7]));
+      else if constexpr (KIND == 12)   // 64-bit shift-add (gfx940+)
+        asm volatile("v_lshl_add_u64 %0, %0, 3, %1" : "+v"(*reinterpret_cast<uint64_t*>(&a[k & 6])) : "v"(*reinterpret_cast<uint64_t*>(&a[(k + 2) & 6])));
+      else if constexpr (KIND == 13)   // alignbit with SGPR shift
+        asm volatile("v_alignbit_b32 %0, %0, %1, %2" : "+v"(a[k]) : "v"(a[(k + 1) & 7]), "s"(sv));
+      else if constexpr (KIND == 14)   // xad
+        asm volatile("v_xad_u32 %0, %0, %1, %2" : "+v"(a[k]) : "v"(a[(k + 1) & 7]), "v"(a[(k + 2) & 7]));
+      else if constexpr (KIND == 15)   // perm
+        asm volatile("v_perm_b32 %0, %0, %1, %2" : "+v"(a[k]) : "v"(a[(k + 1) & 7]), "v"(sv));
+      else if constexpr (KIND == 16)   // SDWA add (word select)
+        asm volatile("v_add_u32_sdwa %0, %0, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1" : "+v"(a[k]) : "v"(a[(k + 1) & 7]));
+      else if constexpr (KIND == 17)   // VOP2 and
+        asm volatile("v_and_b32_e32 %0, %0, %1" : "+v"(a[k]) : "v"(a[(k + 1) & 7]));
+      else if constexpr (KIND == 18)   // VOP2 shift
+        asm volatile("v_lshlrev_b32_e32 %0, 5, %0" : "+v"(a[k]));
+      else if constexpr (KIND == 19)   // v_pk_add_u16
+        asm volatile("v_pk_add_u16 %0, %0, %1" : "+v"(a[k]) : "v"(a[(k + 1) & 7]));
     }
   }
   const uint64_t t1 = __builtin_amdgcn_s_memtime();
@@ -170,16 +202,16 @@ extern "C" int md5diag_run(int kind, const void* base, uint64_t n, uint32_t len,
     case 7:
       hipLaunchKernelGGL(diag_xpose2_load, dim3(grid), dim3(256), 0, s, b, n, len, stride, o);
       break;
-    case 8: case 9: case 10: case 11: {
+    case 100 ... 119: {
       // n = waves to launch (multiple of 4), len = iterations; out needs
       // 64*n u32 + 2*n u64 (clock pairs after the u32 area)
       uint32_t* o32 = (uint32_t*)out;
       uint64_t* clk = (uint64_t*)(o32 + 64 * n);
       const dim3 g((uint32_t)(n / 4));
-      if (kind == 8) hipLaunchKernelGGL(diag_valu_rate<0>, g, dim3(256), 0, s, len, o32, clk);
-      if (kind == 9) hipLaunchKernelGGL(diag_valu_rate<1>, g, dim3(256), 0, s, len, o32, clk);
-      if (kind == 10) hipLaunchKernelGGL(diag_valu_rate<2>, g, dim3(256), 0, s, len, o32, clk);
-      if (kind == 11) hipLaunchKernelGGL(diag_valu_rate<3>, g, dim3(256), 0, s, len, o32, clk);
+#define RATE(K) if (kind == 100 + K) hipLaunchKernelGGL(diag_valu_rate<K>, g, dim3(256), 0, s, len, o32, clk);
+      RATE(0) RATE(1) RATE(2) RATE(3) RATE(4) RATE(5) RATE(6) RATE(7) RATE(8) RATE(9)
+      RATE(10) RATE(11) RATE(12) RATE(13) RATE(14) RATE(15) RATE(16) RATE(17) RATE(18) RATE(19)
+#undef RATE
       break;
     }
     default:
