@@ -41,7 +41,10 @@ enum md5hip_variant {
     MD5HIP_LDS128 = 4,      /* wave LDS-DMA staging, 128 B per chunk per stage */
     MD5HIP_XPOSE1 = 5,      /* coalesced buffer loads, LDS transpose, 1 stage ahead */
     MD5HIP_XPOSE2 = 6,      /* same, 2 stages ahead */
-    MD5HIP_NUM_VARIANTS = 7
+    MD5HIP_XPOSE1NT = 7,    /* xpose1 with non-temporal loads */
+    MD5HIP_XPOSE2NT = 8,    /* xpose2 with non-temporal loads */
+    MD5HIP_LDS128NT = 9,    /* lds128 with non-temporal loads */
+    MD5HIP_NUM_VARIANTS = 10
 };
 
 int md5hip_abi_version(void);

@@ -50,6 +50,7 @@ def main():
              "lds128": prod("lds128"), "compute_only": diag(0), "load_direct2": diag(1),
              "load_direct4": diag(2), "load_lds64": diag(3), "load_lds128": diag(4),
              "stream_read": diag(5), "xpose1": prod("xpose1"), "xpose2": prod("xpose2"),
+             "xpose1nt": prod("xpose1nt"), "xpose2nt": prod("xpose2nt"), "lds128nt": prod("lds128nt"),
              "load_xpose1": diag(6), "load_xpose2": diag(7)}
     if a.only:
         cases = {k: v for k, v in cases.items() if k in a.only.split(",")}

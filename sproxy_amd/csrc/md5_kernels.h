@@ -168,7 +168,7 @@ __device__ __forceinline__ uint32_t swz(uint32_t row) {
   return BB == 64 ? ((row >> 2) & 3u) : ((row >> 1) & 7u);
 }
 
-template <int BB, int MODE = 0>
+template <int BB, int MODE = 0, int CP = 0>
 __device__ __forceinline__ void fixed_lds_body(const uint8_t* __restrict__ base, uint64_t n,
                                                uint32_t len, uint64_t stride,
                                                uint4* __restrict__ out, uint8_t* lds) {
@@ -202,7 +202,7 @@ __device__ __forceinline__ void fixed_lds_body(const uint8_t* __restrict__ base,
     uint8_t* dst = ring + (stg & 1u) * STAGE;
 #pragma unroll
     for (int r = 0; r < NI; ++r)
-      __builtin_amdgcn_global_load_lds(src[r] + (size_t)stg * BB, dst + r * 1024, 16, 0, 0);
+      __builtin_amdgcn_global_load_lds(src[r] + (size_t)stg * BB, dst + r * 1024, 16, 0, CP);
   };
 
   State st = initial_state();
@@ -253,7 +253,7 @@ __device__ __forceinline__ void fixed_lds_body(const uint8_t* __restrict__ base,
 // occupancy is set by VGPRs, not LDS, and all waits are compiler-counted.
 // Requires 64 * stride < 2^31 (checked by the launcher).
 // ---------------------------------------------------------------------------
-template <int D, int MODE = 0>
+template <int D, int MODE = 0, int CP = 0>
 __device__ __forceinline__ void fixed_xpose_body(const uint8_t* __restrict__ base, uint64_t n,
                                                  uint32_t len, uint64_t stride,
                                                  uint4* __restrict__ out, uint8_t* lds) {
@@ -284,7 +284,7 @@ __device__ __forceinline__ void fixed_xpose_body(const uint8_t* __restrict__ bas
   auto load_stage = [&](u32x4 (&R)[8], uint32_t stg) __attribute__((always_inline)) {
 #pragma unroll
     for (int r = 0; r < 8; ++r)
-      R[r] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, (int)voff[r], (int)(stg * 128u), 0);
+      R[r] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, (int)voff[r], (int)(stg * 128u), CP);
   };
   auto consume = [&](u32x4 (&R)[8], uint32_t next) __attribute__((always_inline)) {
 #pragma unroll
@@ -352,6 +352,29 @@ md5_fixed_xpose2(const uint8_t* __restrict__ base, uint64_t n, uint32_t len, uin
                  uint4* __restrict__ out) {
   __shared__ __attribute__((aligned(16))) uint8_t img[4 * 8192];
   fixed_xpose_body<2>(base, n, len, stride, out, img);
+}
+
+// Non-temporal ("nt", aux = 2) load policy: every byte is read exactly once,
+// so do not let the stream allocate in L2 / Infinity Cache.
+__global__ void __launch_bounds__(256)
+md5_fixed_xpose1nt(const uint8_t* __restrict__ base, uint64_t n, uint32_t len, uint64_t stride,
+                   uint4* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) uint8_t img[4 * 8192];
+  fixed_xpose_body<1, 0, 2>(base, n, len, stride, out, img);
+}
+
+__global__ void __launch_bounds__(256)
+md5_fixed_xpose2nt(const uint8_t* __restrict__ base, uint64_t n, uint32_t len, uint64_t stride,
+                   uint4* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) uint8_t img[4 * 8192];
+  fixed_xpose_body<2, 0, 2>(base, n, len, stride, out, img);
+}
+
+__global__ void __launch_bounds__(256)
+md5_fixed_lds128nt(const uint8_t* __restrict__ base, uint64_t n, uint32_t len, uint64_t stride,
+                   uint4* __restrict__ out) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds_dyn[];
+  fixed_lds_body<128, 0, 2>(base, n, len, stride, out, lds_dyn);
 }
 
 __global__ void __launch_bounds__(256)

@@ -49,11 +49,11 @@ int default_variant() {
   return v;
 }
 
-template <int BB>
+template <int BB, bool NT = false>
 int launch_lds(const uint8_t* base, uint64_t n, uint32_t len, uint64_t stride, uint4* out,
                hipStream_t s) {
   const size_t lds = (size_t)(kBlock / 64) * 2 * 64 * BB;
-  auto fn = BB == 64 ? md5_fixed_lds64 : md5_fixed_lds128;
+  auto fn = BB == 64 ? md5_fixed_lds64 : NT ? md5_fixed_lds128nt : md5_fixed_lds128;
   static bool attr = false;
   if (!attr) {
     if (hipFuncSetAttribute(reinterpret_cast<const void*>(fn),
@@ -83,6 +83,9 @@ const char* md5hip_variant_name(int v) {
     case MD5HIP_LDS128: return "lds128";
     case MD5HIP_XPOSE1: return "xpose1";
     case MD5HIP_XPOSE2: return "xpose2";
+    case MD5HIP_XPOSE1NT: return "xpose1nt";
+    case MD5HIP_XPOSE2NT: return "xpose2nt";
+    case MD5HIP_LDS128NT: return "lds128nt";
     default: return "?";
   }
 }
@@ -135,19 +138,20 @@ int md5hip_digest_fixed_variant(const void* d_base, uint64_t n, uint32_t len, ui
       return launch_lds<64>(base, n, len, stride, out, s);
     case MD5HIP_LDS128:
       return launch_lds<128>(base, n, len, stride, out, s);
+    case MD5HIP_LDS128NT:
+      return launch_lds<128, true>(base, n, len, stride, out, s);
     case MD5HIP_XPOSE1:
     case MD5HIP_XPOSE2:
-      if (stride >= (1ull << 31) / 64) {   // 32-bit buffer offsets per 64-chunk group
-        hipLaunchKernelGGL((md5_fixed_direct<2, 0>), dim3((uint32_t)grid), dim3(kBlock), 0, s,
-                           base, n, len, stride, out);
-      } else if (variant == MD5HIP_XPOSE1) {
-        hipLaunchKernelGGL(md5_fixed_xpose1, dim3((uint32_t)grid), dim3(kBlock), 0, s, base, n,
-                           len, stride, out);
-      } else {
-        hipLaunchKernelGGL(md5_fixed_xpose2, dim3((uint32_t)grid), dim3(kBlock), 0, s, base, n,
-                           len, stride, out);
-      }
+    case MD5HIP_XPOSE1NT:
+    case MD5HIP_XPOSE2NT: {
+      typedef void (*K)(const uint8_t*, uint64_t, uint32_t, uint64_t, uint4*);
+      K k = variant == MD5HIP_XPOSE1 ? md5_fixed_xpose1
+          : variant == MD5HIP_XPOSE2 ? md5_fixed_xpose2
+          : variant == MD5HIP_XPOSE1NT ? md5_fixed_xpose1nt : md5_fixed_xpose2nt;
+      if (stride >= (1ull << 31) / 64) k = md5_fixed_direct<2, 0>;  // 32-bit buffer offsets
+      hipLaunchKernelGGL(k, dim3((uint32_t)grid), dim3(kBlock), 0, s, base, n, len, stride, out);
       return launched();
+    }
   }
   return -EINVAL;
 }
