@@ -44,7 +44,7 @@ int default_variant() {
   if (v < 0) {
     const char* e = getenv("MD5HIP_VARIANT");
     int x = e ? atoi(e) : 0;
-    v = (x > 0 && x < MD5HIP_NUM_VARIANTS) ? x : MD5HIP_DIRECT2;
+    v = (x > 0 && x < MD5HIP_NUM_VARIANTS) ? x : MD5HIP_XPOSE1NT;   // measured best, DESIGN.md
   }
   return v;
 }
