@@ -106,6 +106,20 @@ void md5hip_batcher_destroy(md5hip_batcher *b);
 int md5_batch_submit(md5hip_batcher *b, const void *const *ptrs, const uint32_t *lens,
                      uint64_t n, unsigned char *digests);
 
+/* One segment of a chunk that lives in several buffers -- e.g. a netcache
+ * block, which is a list of 16 KiB pages (netcache/include/block.h:143-146,
+ * bc_mgr.c:1251) read through bs_read (bc_mgr.c:1117-1157). */
+struct md5hip_iov {
+    const void *base;
+    uint32_t len;
+};
+
+/* digests[i] = MD5(concat(segs[seg_first[i]] .. segs[seg_first[i+1]-1])),
+ * seg_first has n+1 entries (seg_first[0] = 0).  The segments are gathered
+ * into the pinned staging slice; -E2BIG if one chunk exceeds slice_bytes. */
+int md5_batch_submit_iov(md5hip_batcher *b, const struct md5hip_iov *segs,
+                         const uint64_t *seg_first, uint64_t n, unsigned char *digests);
+
 /* digests[i] = MD5(h_base + i*stride, len) from one contiguous host buffer
  * (pinned for full PCIe rate), copied slice by slice with no host gather. */
 int md5hip_batch_host_fixed(md5hip_batcher *b, const void *h_base, uint64_t n, uint32_t len,

@@ -33,6 +33,11 @@ class MD5Context(ctypes.Structure):
                 ("in_", ctypes.c_ubyte * 64)]
 
 
+class MD5HipIov(ctypes.Structure):
+    """struct md5hip_iov (include/md5hip.h)."""
+    _fields_ = [("base", ctypes.c_void_p), ("len", ctypes.c_uint32)]
+
+
 class MD5HipError(RuntimeError):
     def __init__(self, fn, rc):
         name = errno.errorcode.get(-rc, str(rc))
@@ -63,6 +68,7 @@ def lib():
         "md5hip_batcher_create": (i, [i, u64, u32, ctypes.POINTER(vp)]),
         "md5hip_batcher_destroy": (None, [vp]),
         "md5_batch_submit": (i, [vp, vp, vp, u64, vp]),
+        "md5_batch_submit_iov": (i, [vp, vp, vp, u64, vp]),
         "md5hip_batch_host_fixed": (i, [vp, vp, u64, u32, u64, vp]),
     }
     for name, (res, args) in sig.items():
@@ -78,7 +84,8 @@ EXPORTS = ["MD5Init", "MD5Update", "MD5Final", "md5hip_abi_version", "md5hip_var
            "md5hip_resolve_variant",
            "md5hip_digest_fixed", "md5hip_digest_fixed_variant", "md5hip_digest_desc",
            "md5hip_plan_order", "md5hip_fill_synthetic", "md5hip_batcher_create",
-           "md5hip_batcher_destroy", "md5_batch_submit", "md5hip_batch_host_fixed"]
+           "md5hip_batcher_destroy", "md5_batch_submit", "md5_batch_submit_iov",
+           "md5hip_batch_host_fixed"]
 
 
 def check(fn, rc):

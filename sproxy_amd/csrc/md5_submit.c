@@ -133,15 +133,42 @@ static int slot_launch(struct slot *sl, uint64_t n, uint64_t bytes, unsigned cha
     return 0;
 }
 
-int md5_batch_submit(md5hip_batcher *b, const void *const *ptrs, const uint32_t *lens, uint64_t n,
-                     unsigned char *digests)
+/* Chunk sources for the generic gather loop: a flat (ptr, len) list or an
+ * iovec list with per-chunk segment ranges. */
+struct chunk_src {
+    const void *const *ptrs;
+    const uint32_t *lens;
+    const struct md5hip_iov *segs;
+    const uint64_t *seg_first;
+};
+
+static uint64_t src_len(const struct chunk_src *s, uint64_t i)
 {
-    if (!b) return -EINVAL;
-    if (n == 0) return 0;
-    if (!ptrs || !lens || !digests) return -EINVAL;
+    if (s->ptrs) return s->lens[i];
+    uint64_t L = 0;
+    for (uint64_t j = s->seg_first[i]; j < s->seg_first[i + 1]; j++) L += s->segs[j].len;
+    return L;
+}
+
+static void src_copy(const struct chunk_src *s, uint64_t i, unsigned char *dst)
+{
+    if (s->ptrs) {
+        if (s->lens[i]) memcpy(dst, s->ptrs[i], s->lens[i]);
+        return;
+    }
+    for (uint64_t j = s->seg_first[i]; j < s->seg_first[i + 1]; j++) {
+        if (s->segs[j].len) memcpy(dst, s->segs[j].base, s->segs[j].len);
+        dst += s->segs[j].len;
+    }
+}
+
+static int submit_gather(md5hip_batcher *b, const struct chunk_src *src, uint64_t n,
+                         unsigned char *digests)
+{
     for (uint64_t i = 0; i < n; i++) {
-        if (!ptrs[i] && lens[i]) return -EINVAL;
-        if (((uint64_t)lens[i] + 15) / 16 * 16 > b->cap) return -E2BIG;
+        const uint64_t L = src_len(src, i);
+        if (L > 0xffffffffull) return -E2BIG;
+        if ((L + 15) / 16 * 16 > b->cap) return -E2BIG;
     }
     if (hipSetDevice(b->device) != hipSuccess) return -ENODEV;
     int rc = 0;
@@ -152,11 +179,12 @@ int md5_batch_submit(md5hip_batcher *b, const void *const *ptrs, const uint32_t 
         if ((rc = slot_retire(sl))) return rc;
         uint64_t used = 0, m = 0, first = i;
         while (i < n && m < b->maxn) {
-            const uint64_t sz = ((uint64_t)lens[i] + 15) & ~15ull;   /* 16-B aligned packing */
+            const uint64_t L = src_len(src, i);
+            const uint64_t sz = (L + 15) & ~15ull;   /* 16-B aligned packing */
             if (used + sz > b->cap) break;
-            if (lens[i]) memcpy(sl->h_data + used, ptrs[i], lens[i]);
+            src_copy(src, i, sl->h_data + used);
             sl->h_off[m] = used;
-            sl->h_len[m] = lens[i];
+            sl->h_len[m] = (uint32_t)L;
             used += sz;
             m++;
             i++;
@@ -167,6 +195,33 @@ int md5_batch_submit(md5hip_batcher *b, const void *const *ptrs, const uint32_t 
     for (uint32_t j = 0; j < b->nslots; j++)
         if ((rc = slot_retire(&b->s[j]))) return rc;
     return 0;
+}
+
+int md5_batch_submit(md5hip_batcher *b, const void *const *ptrs, const uint32_t *lens, uint64_t n,
+                     unsigned char *digests)
+{
+    if (!b) return -EINVAL;
+    if (n == 0) return 0;
+    if (!ptrs || !lens || !digests) return -EINVAL;
+    for (uint64_t i = 0; i < n; i++)
+        if (!ptrs[i] && lens[i]) return -EINVAL;
+    const struct chunk_src src = {ptrs, lens, NULL, NULL};
+    return submit_gather(b, &src, n, digests);
+}
+
+int md5_batch_submit_iov(md5hip_batcher *b, const struct md5hip_iov *segs,
+                         const uint64_t *seg_first, uint64_t n, unsigned char *digests)
+{
+    if (!b) return -EINVAL;
+    if (n == 0) return 0;
+    if (!segs || !seg_first || !digests || seg_first[0] != 0) return -EINVAL;
+    for (uint64_t i = 0; i < n; i++) {
+        if (seg_first[i + 1] < seg_first[i]) return -EINVAL;
+        for (uint64_t j = seg_first[i]; j < seg_first[i + 1]; j++)
+            if (!segs[j].base && segs[j].len) return -EINVAL;
+    }
+    const struct chunk_src src = {NULL, NULL, segs, seg_first};
+    return submit_gather(b, &src, n, digests);
 }
 
 int md5hip_batch_host_fixed(md5hip_batcher *b, const void *h_base, uint64_t n, uint32_t len,

@@ -19,7 +19,7 @@ import ctypes
 
 import numpy as np
 
-from ._lib import MD5Context, MD5HipError, check, lib
+from ._lib import MD5Context, MD5HipError, MD5HipIov, check, lib
 
 try:
     import torch
@@ -219,6 +219,27 @@ class Batcher:
         out = np.empty((max(n, 1), 16), dtype=np.uint8)
         check("md5_batch_submit", lib().md5_batch_submit(self._h, ptrs, lens.ctypes.data, n,
                                                           out.ctypes.data))
+        return out[:n]
+
+    def submit_iov(self, chunks) -> np.ndarray:
+        """digests[i] = MD5(b"".join(chunks[i])) for a list of segment lists
+        (a netcache block = its list of pages)."""
+        segs, first, keep = [], [0], []
+        for segl in chunks:
+            for sgm in segl:
+                a, k = _addr(sgm)
+                keep.append(k)
+                segs.append((a, memoryview(sgm).nbytes))
+            first.append(len(segs))
+        arr = (MD5HipIov * max(len(segs), 1))()
+        for j, (a, L) in enumerate(segs):
+            arr[j].base = a
+            arr[j].len = L
+        fa = np.asarray(first, dtype=np.uint64)
+        n = len(chunks)
+        out = np.empty((max(n, 1), 16), dtype=np.uint8)
+        check("md5_batch_submit_iov", lib().md5_batch_submit_iov(self._h, arr, fa.ctypes.data, n,
+                                                                  out.ctypes.data))
         return out[:n]
 
     def host_fixed(self, arr: np.ndarray, n: int, length: int, stride: int = None) -> np.ndarray:
