@@ -28,6 +28,7 @@ import torch
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 from sproxy_amd import md5 as m  # noqa: E402
+from sproxy_amd.shard import barrier, env_rank, max_over_ranks, shard_range  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 PCIE_PEAK_GBS = 63.0           # PCIe Gen5 x16 (spec)
@@ -36,9 +37,7 @@ GIB = float(1 << 30)
 
 
 def dist_setup(ngpus):
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    rank, world, local = env_rank()
     if world != ngpus and world > 1:
         raise SystemExit(f"--gpus {ngpus} but WORLD_SIZE={world}")
     torch.cuda.set_device(local)
@@ -47,21 +46,6 @@ def dist_setup(ngpus):
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     return rank, world, local
-
-
-def barrier(world):
-    if world > 1:
-        import torch.distributed as dist
-        dist.barrier()
-
-
-def max_over_ranks(x, world):
-    if world == 1:
-        return x
-    import torch.distributed as dist
-    t = torch.tensor([x], dtype=torch.float64, device="cuda")
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    return float(t.item())
 
 
 def timed_steps(fn, steps, warmup, world):
@@ -126,16 +110,22 @@ def load_traffic(path, variant):
 
 
 def run_c2(a, rank, world):
-    n, L = a.chunks, a.len
+    L = a.len
+    if a.total_chunks:       # strong / C4 form: one global batch split into contiguous shards
+        lo, hi = shard_range(a.total_chunks, rank, world)
+        n = hi - lo
+    else:                    # weak scaling: a fixed per-GPU batch (C2 shape on every GPU)
+        n = a.chunks
     data = torch.empty(n * L, dtype=torch.uint8, device="cuda")
     m.fill_synthetic(data, seed=0x5EED0000 + rank)
     out = torch.empty((n, 16), dtype=torch.uint8, device="cuda")
     variant = m.VARIANTS[a.variant]
     fn = lambda: m.digest_fixed(data, n, L, out=out, variant=variant)  # noqa: E731
     wall, dev_ms = timed_steps(fn, a.steps, a.warmup, world)
-    wall_max = max_over_ranks(wall, world)
-    dev_ms_max = max_over_ranks(dev_ms, world)
-    total_bytes = float(n) * L * world * a.steps
+    wall_max = max_over_ranks(wall, world, "cuda")
+    dev_ms_max = max_over_ranks(dev_ms, world, "cuda")
+    n_all = a.total_chunks if a.total_chunks else n * world
+    total_bytes = float(n_all) * L * a.steps
     value = total_bytes / wall_max / GIB
     alg_bytes = float(n) * (L + 16)            # read every chunk once + 16-B digest write
     achieved = alg_bytes / (dev_ms_max * 1e-3) / 1e9
@@ -143,10 +133,12 @@ def run_c2(a, rank, world):
     res = {
         "metric": METRIC, "value": round(value, 2), "unit": "GiB/s", "n_gpus": world,
         "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(wall_max / a.steps * 1e3, 4),
-        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32",
+        "higher_is_better": True, "scaling": "strong" if a.total_chunks else "weak",
+        "vs_baseline": None, "dtype": "u32",
         "data": "synthetic (device-generated splitmix words, per-rank seed)",
-        "config": {"workload": "C2: 1,048,576 x 16 KiB chunks per GPU, device-resident"
-                   if (n, L) == (1 << 20, 16384) else f"{n} x {L} B chunks per GPU, device-resident",
+        "config": {"workload": ("C2: 1,048,576 x 16 KiB chunks per GPU, device-resident"
+                                if (n, L) == (1 << 20, 16384) and not a.total_chunks else
+                                f"{n_all} x {L} B chunks total, {n} on rank 0, device-resident"),
                    "chunks_per_gpu": n, "chunk_bytes": L, "kernel_variant": vname,
                    "parallelism": f"dp{world} (independent chunk shards, no collective)"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
@@ -187,7 +179,7 @@ def run_c3(a, rank, world):
     out = torch.empty((lens.size, 16), dtype=torch.uint8, device="cuda")
     fn = lambda: m.digest_desc(data, d_off, d_len, d_ord, out=out)  # noqa: E731
     wall, dev_ms = timed_steps(fn, a.steps, a.warmup, world)
-    wall_max = max_over_ranks(wall, world)
+    wall_max = max_over_ranks(wall, world, "cuda")
     payload = float(lens.sum())
     value = payload * world * a.steps / wall_max / GIB
     # the longest chunk bounds the step: a 1 MiB chunk is 16,385 dependent
@@ -213,13 +205,17 @@ def run_c5(a, rank, world):
     host = torch.empty(n * L, dtype=torch.uint8, pin_memory=True)
     host.view(torch.int64).random_(generator=torch.Generator().manual_seed(5))
     arr = host.numpy()
-    # PCIe H2D alone (the denominator for this config)
-    dev = torch.empty(n * L, dtype=torch.uint8, device="cuda")
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    dev.copy_(host, non_blocking=True)
-    torch.cuda.synchronize()
-    h2d_gbs = n * L / (time.perf_counter() - t0) / 1e9
+    # PCIe H2D alone (the denominator for this config): same slices, warmed up
+    dev = torch.empty(a.c5_slice, dtype=torch.uint8, device="cuda")
+    per = a.c5_slice
+    for _ in range(2):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for off in range(0, n * L, per):
+            m_ = min(per, n * L - off)
+            dev[:m_].copy_(host[off:off + m_], non_blocking=True)
+        torch.cuda.synchronize()
+        h2d_gbs = n * L / (time.perf_counter() - t0) / 1e9
     del dev
     with m.Batcher(device=torch.cuda.current_device(), slice_bytes=a.c5_slice, nslots=3) as b:
         for _ in range(a.warmup):
@@ -248,7 +244,9 @@ def main():
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--config", default="c2", choices=["c2", "c3", "c5"])
-    p.add_argument("--chunks", type=int, default=1 << 20, help="chunks per GPU (C2)")
+    p.add_argument("--chunks", type=int, default=1 << 20, help="chunks per GPU (C2, weak scaling)")
+    p.add_argument("--total-chunks", type=int, default=0,
+                   help="one global batch split across ranks (C4: 16777216 on 8 GPUs)")
     p.add_argument("--len", type=int, default=16384)
     p.add_argument("--variant", default="auto", choices=sorted(m.VARIANTS))
     p.add_argument("--no-cpu-baseline", action="store_true")

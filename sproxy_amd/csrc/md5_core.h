@@ -49,15 +49,33 @@ __device__ __forceinline__ uint32_t f4(uint32_t x, uint32_t y, uint32_t z) {
 }
 
 // MD5STEP (md5.c:55-56): w += f(x,y,z) + data; w = rotl(w, s); w += x.
-// The w + M + K sum does not depend on the previous step, so it is formed
-// first (off the chain); the chain is f -> add -> alignbit -> add.
+// Cost model (profiles/r01_valu_rate_*): v_add_u32 / v_bitop3 ~2.8 cycles,
+// v_add3_u32 / v_alignbit ~4.4.  Two orderings of the same 5 instructions:
+//  kLat = false: hipcc's choice, add(w,M) off the chain, add3(.,F,K) on it
+//                (chain: bitop3 -> add3 -> alignbit -> add, two slow ops);
+//  kLat = true : add3(w,M,K) off the chain (an empty asm pins the partial
+//                sum so it is not re-associated with F), fast add on it
+//                (chain: bitop3 -> add -> alignbit -> add, one slow op).
+// The instruction count is equal; kLat shortens the serial chain, which is
+// what bounds a lane hashing a long chunk alone (config C3).
+template <bool kLat>
+__device__ __forceinline__ uint32_t md5_sum(uint32_t w, uint32_t m, uint32_t k, uint32_t f) {
+  if constexpr (kLat) {
+    uint32_t t = w + m + k;
+    asm("" : "+v"(t));
+    return t + f;
+  } else {
+    return (w + m + k) + f;
+  }
+}
+
 #define MD5HIP_STEP(F, w, x, y, z, m, k, s) \
-  w = x + rotl((w + (m) + (k)) + F(x, y, z), s)
+  w = x + rotl(md5_sum<kLat>(w, (m), (k), F(x, y, z)), s)
 
 // One 64-byte block, message words m[0..15] little-endian (byteReverse is a
 // no-op on little-endian gfx950, md5.c:24-25).  The 64 K literals are the
 // RFC 1321 T table (md5.c:74-139).
-template <typename MsgFn>
+template <bool kLat = false, typename MsgFn>
 __device__ __forceinline__ void compress(State& st, MsgFn M) {
   uint32_t a = st.a, b = st.b, c = st.c, d = st.d;
   MD5HIP_STEP(f1, a, b, c, d, M(0), 0xd76aa478u, 7);
@@ -137,8 +155,9 @@ __device__ __forceinline__ void compress(State& st, MsgFn M) {
 #undef MD5HIP_STEP
 
 // Compress 16 words held in four uint4 registers.
+template <bool kLat = false>
 __device__ __forceinline__ void compress_regs(State& st, const uint4 (&w)[4]) {
-  compress(st, [&](int i) __attribute__((always_inline)) -> uint32_t {
+  compress<kLat>(st, [&](int i) __attribute__((always_inline)) -> uint32_t {
     const uint4& q = w[i >> 2];
     switch (i & 3) {
       case 0: return q.x;
@@ -152,8 +171,9 @@ __device__ __forceinline__ void compress_regs(State& st, const uint4 (&w)[4]) {
 // The final padding block of a message whose length is a multiple of 64:
 // 0x80, 52 zero bytes, then the 64-bit bit count (md5.c:221-261).  All but
 // words 14/15 are compile-time constants, so M + K folds into one literal.
+template <bool kLat = false>
 __device__ __forceinline__ void compress_pad_only(State& st, uint32_t bits_lo, uint32_t bits_hi) {
-  compress(st, [&](int i) __attribute__((always_inline)) -> uint32_t {
+  compress<kLat>(st, [&](int i) __attribute__((always_inline)) -> uint32_t {
     return i == 0 ? 0x80u : i == 14 ? bits_lo : i == 15 ? bits_hi : 0u;
   });
 }

@@ -6,6 +6,10 @@
 //   kind 1..4  load only: the product's loaders (direct2, direct4, lds64,
 //           lds128) with the compression replaced by a 16-word xor fold
 //   kind 5  ideal coalesced read: each wave-instruction reads 1 KiB contiguous
+//   kind 6,7  load only for the xpose1 / xpose2 loaders
+//   kind 12   compute only with the latency-form step (md5_core.h kLat)
+//   kind 13,14 single-chain latency: few lanes, long chunks (kLat off / on)
+//   kind 100+K VALU issue-rate probes (instruction K of diag_valu_rate)
 //
 // C ABI: int md5diag_run(int kind, const void *base, uint64_t n, uint32_t len,
 //                        uint64_t stride, void *out, void *stream)
@@ -17,6 +21,12 @@ namespace md5hip {
 
 template __global__ void md5_fixed_direct<2, 1>(const uint8_t*, uint64_t, uint32_t, uint64_t, uint4*);
 template __global__ void md5_fixed_direct<4, 1>(const uint8_t*, uint64_t, uint32_t, uint64_t, uint4*);
+#define DESC_INST(L, P)                                                                     \
+  template __global__ void md5_desc<false, L, P>(const uint8_t*, const uint64_t*,          \
+                                                 const uint32_t*, const uint32_t*, uint64_t, \
+                                                 uint64_t, uint32_t, uint4*);
+DESC_INST(false, false) DESC_INST(false, true) DESC_INST(true, false) DESC_INST(true, true)
+#undef DESC_INST
 
 __global__ void __launch_bounds__(256)
 diag_lds64_load(const uint8_t* __restrict__ base, uint64_t n, uint32_t len, uint64_t stride,
@@ -48,6 +58,7 @@ diag_xpose2_load(const uint8_t* __restrict__ base, uint64_t n, uint32_t len, uin
 
 // Compute only: lane L hashes `nblocks` blocks whose words it re-reads from its
 // own 64-B LDS row every block (ds_read_b128 x4, like lds64), then the pad block.
+template <bool kLat>
 __global__ void __launch_bounds__(256)
 diag_compute(uint64_t n, uint32_t nblocks, uint4* __restrict__ out) {
   __shared__ __attribute__((aligned(16))) uint8_t rows[256 * 64];
@@ -65,7 +76,7 @@ diag_compute(uint64_t n, uint32_t nblocks, uint4* __restrict__ out) {
       const uint32_t q = ((uint32_t)k + b) & 3u;
       w[k] = *reinterpret_cast<const uint4*>(rows + threadIdx.x * 64 + q * 16);
     }
-    compress_regs(st, w);
+    compress_regs<kLat>(st, w);
   }
   compress_pad_only(st, nblocks * 512u, 0u);
   if (i < n) out[i] = make_uint4(st.a, st.b, st.c, st.d);
@@ -170,8 +181,19 @@ extern "C" int md5diag_run(int kind, const void* base, uint64_t n, uint32_t len,
   const uint32_t grid = (uint32_t)((n + 255) / 256);
   switch (kind) {
     case 0:
-      hipLaunchKernelGGL(diag_compute, dim3(grid), dim3(256), 0, s, n, len >> 6, o);
+      hipLaunchKernelGGL(diag_compute<false>, dim3(grid), dim3(256), 0, s, n, len >> 6, o);
       break;
+    case 12:
+      hipLaunchKernelGGL(diag_compute<true>, dim3(grid), dim3(256), 0, s, n, len >> 6, o);
+      break;
+    case 13: case 14: {
+      // single-chain latency: n lanes (one wave per CU at n = 16384), each
+      // hashing `len` bytes; 64-thread workgroups so every CU gets one wave
+      const dim3 g1((uint32_t)((n + 63) / 64));
+      if (kind == 13) hipLaunchKernelGGL(diag_compute<false>, g1, dim3(64), 0, s, n, len >> 6, o);
+      else hipLaunchKernelGGL(diag_compute<true>, g1, dim3(64), 0, s, n, len >> 6, o);
+      break;
+    }
     case 1:
       hipLaunchKernelGGL((md5_fixed_direct<2, 1>), dim3(grid), dim3(256), 0, s, b, n, len, stride, o);
       break;
@@ -216,6 +238,22 @@ extern "C" int md5diag_run(int kind, const void* base, uint64_t n, uint32_t len,
     }
     default:
       return -EINVAL;
+  }
+  return hipGetLastError() == hipSuccess ? 0 : -EIO;
+}
+
+// Descriptor-kernel A/B (C3): kind bit0 = kLat, bit1 = kPrio.
+extern "C" int md5diag_desc(int kind, const void* base, const uint64_t* offs, const uint32_t* lens,
+                            const uint32_t* order, uint64_t n, void* out, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  const dim3 g((uint32_t)((n + 255) / 256));
+  const uint8_t* b = (const uint8_t*)base;
+  uint4* o = (uint4*)out;
+  switch (kind & 3) {
+    case 0: hipLaunchKernelGGL((md5_desc<false, false, false>), g, dim3(256), 0, s, b, offs, lens, order, n, (uint64_t)0, 0u, o); break;
+    case 1: hipLaunchKernelGGL((md5_desc<false, true, false>), g, dim3(256), 0, s, b, offs, lens, order, n, (uint64_t)0, 0u, o); break;
+    case 2: hipLaunchKernelGGL((md5_desc<false, false, true>), g, dim3(256), 0, s, b, offs, lens, order, n, (uint64_t)0, 0u, o); break;
+    default: hipLaunchKernelGGL((md5_desc<false, true, true>), g, dim3(256), 0, s, b, offs, lens, order, n, (uint64_t)0, 0u, o); break;
   }
   return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }

@@ -408,9 +408,20 @@ __device__ __forceinline__ void load_block_unaligned(uint4 (&r)[4], const uint8_
   for (int k = 0; k < 4; ++k) r[k] = make_uint4(o[4 * k], o[4 * k + 1], o[4 * k + 2], o[4 * k + 3]);
 }
 
+// Wave-uniform max over the 64 lanes (butterfly), for the priority choice.
+__device__ __forceinline__ uint32_t wave_max(uint32_t v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, o, 64));
+  return __builtin_amdgcn_readfirstlane(v);
+}
+
 // kImplicit: chunk i at base + i*stride with length `flen` (the fixed-length
 // API's fallback for chunk starts that are not 16-B aligned).
-template <bool kImplicit>
+// kLat: latency-form step (md5_core.h).  kPrio: waves holding long chunks
+// raise their issue priority, so the longest serial chains -- which bound a
+// mixed batch -- progress at their latency limit while short-chunk waves fill
+// the remaining issue slots.
+template <bool kImplicit, bool kLat = true, bool kPrio = true>
 __global__ void __launch_bounds__(256)
 md5_desc(const uint8_t* __restrict__ base, const uint64_t* __restrict__ offs,
          const uint32_t* __restrict__ lens, const uint32_t* __restrict__ order, uint64_t n,
@@ -421,6 +432,12 @@ md5_desc(const uint8_t* __restrict__ base, const uint64_t* __restrict__ offs,
   const uint8_t* chunk = base + (kImplicit ? c * stride : offs[c]);
   const uint32_t len = kImplicit ? flen : lens[c];
   const uint32_t nfull = len >> 6;
+  if constexpr (kPrio) {
+    const uint32_t wmax = wave_max(nfull);
+    if (wmax >= 4096u) __builtin_amdgcn_s_setprio(3);        // >= 256 KiB
+    else if (wmax >= 1024u) __builtin_amdgcn_s_setprio(2);   // >= 64 KiB
+    else if (wmax >= 256u) __builtin_amdgcn_s_setprio(1);    // >= 16 KiB
+  }
   State st = initial_state();
   if (((uintptr_t)chunk & 15u) == 0) {
     const uint4* p = reinterpret_cast<const uint4*>(chunk);
@@ -431,18 +448,18 @@ md5_desc(const uint8_t* __restrict__ base, const uint64_t* __restrict__ offs,
       load_block(R1, p + 4 * min(1u, lastb));
       uint32_t blk = 0;
       for (; blk + 2 <= nfull; blk += 2) {
-        compress_regs(st, R0);
+        compress_regs<kLat>(st, R0);
         load_block(R0, p + 4 * min(blk + 2, lastb));
-        compress_regs(st, R1);
+        compress_regs<kLat>(st, R1);
         load_block(R1, p + 4 * min(blk + 3, lastb));
       }
-      if (blk < nfull) compress_regs(st, R0);
+      if (blk < nfull) compress_regs<kLat>(st, R0);
     }
   } else {
     for (uint32_t blk = 0; blk < nfull; ++blk) {
       uint4 w[4];
       load_block_unaligned(w, chunk + ((uint64_t)blk << 6));
-      compress_regs(st, w);
+      compress_regs<kLat>(st, w);
     }
   }
   finish_message(st, chunk + ((uint64_t)nfull << 6), len & 63u, len);
