@@ -62,7 +62,8 @@ def main():
     out = torch.empty((lens.size, 16), dtype=torch.uint8, device="cuda")
     st = torch.cuda.current_stream().cuda_stream
     ref = None
-    for kind, name in [(0, "base"), (1, "lat"), (2, "prio"), (3, "lat+prio")]:
+    for kind, name in [(0, "r1"), (1, "lat_prio_D2"), (2, "D4"), (3, "D8"), (4, "D8_noprio"),
+                       (5, "D12")]:
         f = lambda: D.md5diag_desc(kind, data.data_ptr(), d_off.data_ptr(), d_len.data_ptr(),  # noqa
                                    order.data_ptr(), lens.size, out.data_ptr(), st)
         ms = timeit(f, reps=2, rounds=3)
@@ -71,6 +72,21 @@ def main():
         assert torch.equal(out, ref), name
         res["c3_" + name] = {"ms": round(ms, 3), "GBps": round(lens.sum() / ms / 1e6, 1)}
     del data
+    torch.cuda.empty_cache()
+    # uniform small chunks through the descriptor kernel (occupancy check)
+    n4 = 1 << 22
+    lens4 = np.full(n4, 4096, dtype=np.int64)
+    offs4 = torch.arange(n4, dtype=torch.int64, device="cuda") * 4096
+    d4 = torch.empty(n4 * 4096, dtype=torch.uint8, device="cuda")
+    m.fill_synthetic(d4, seed=4)
+    l4 = torch.from_numpy(lens4.astype(np.int32)).cuda()
+    o4 = torch.empty((n4, 16), dtype=torch.uint8, device="cuda")
+    for kind, name in [(0, "r1"), (1, "lat_prio_D2"), (2, "D4"), (3, "D8"), (5, "D12")]:
+        f = lambda: D.md5diag_desc(kind, d4.data_ptr(), offs4.data_ptr(), l4.data_ptr(), None,  # noqa
+                                   n4, o4.data_ptr(), st)
+        ms = timeit(f, reps=3, rounds=3)
+        res["u4k_" + name] = {"ms": round(ms, 3), "GBps": round(n4 * 4096 / ms / 1e6, 1)}
+    del d4
     torch.cuda.empty_cache()
     # single-chain latency: 16384 lanes = one wave per CU, 1 MiB each (no HBM)
     buf = torch.empty(16384 * 16 + 1 << 20, dtype=torch.uint8, device="cuda")

@@ -21,11 +21,12 @@ namespace md5hip {
 
 template __global__ void md5_fixed_direct<2, 1>(const uint8_t*, uint64_t, uint32_t, uint64_t, uint4*);
 template __global__ void md5_fixed_direct<4, 1>(const uint8_t*, uint64_t, uint32_t, uint64_t, uint4*);
-#define DESC_INST(L, P)                                                                     \
-  template __global__ void md5_desc<false, L, P>(const uint8_t*, const uint64_t*,          \
-                                                 const uint32_t*, const uint32_t*, uint64_t, \
-                                                 uint64_t, uint32_t, uint4*);
-DESC_INST(false, false) DESC_INST(false, true) DESC_INST(true, false) DESC_INST(true, true)
+#define DESC_INST(L, P, D)                                                                  \
+  template __global__ void md5_desc<false, L, P, D>(const uint8_t*, const uint64_t*,       \
+                                                    const uint32_t*, const uint32_t*, uint64_t, \
+                                                    uint64_t, uint32_t, uint4*);
+DESC_INST(false, false, 2) DESC_INST(true, true, 2) DESC_INST(true, true, 4)
+DESC_INST(true, true, 8) DESC_INST(true, false, 8) DESC_INST(true, true, 12)
 #undef DESC_INST
 
 __global__ void __launch_bounds__(256)
@@ -242,18 +243,24 @@ extern "C" int md5diag_run(int kind, const void* base, uint64_t n, uint32_t len,
   return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }
 
-// Descriptor-kernel A/B (C3): kind bit0 = kLat, bit1 = kPrio.
+// Descriptor-kernel A/B (C3): 0 = (no kLat, no prio, D=2: round-1 kernel),
+// 1 = (kLat, prio, D=2), 2 = D=4, 3 = D=8, 4 = D=8 without prio, 5 = D=12.
 extern "C" int md5diag_desc(int kind, const void* base, const uint64_t* offs, const uint32_t* lens,
                             const uint32_t* order, uint64_t n, void* out, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   const dim3 g((uint32_t)((n + 255) / 256));
   const uint8_t* b = (const uint8_t*)base;
   uint4* o = (uint4*)out;
-  switch (kind & 3) {
-    case 0: hipLaunchKernelGGL((md5_desc<false, false, false>), g, dim3(256), 0, s, b, offs, lens, order, n, (uint64_t)0, 0u, o); break;
-    case 1: hipLaunchKernelGGL((md5_desc<false, true, false>), g, dim3(256), 0, s, b, offs, lens, order, n, (uint64_t)0, 0u, o); break;
-    case 2: hipLaunchKernelGGL((md5_desc<false, false, true>), g, dim3(256), 0, s, b, offs, lens, order, n, (uint64_t)0, 0u, o); break;
-    default: hipLaunchKernelGGL((md5_desc<false, true, true>), g, dim3(256), 0, s, b, offs, lens, order, n, (uint64_t)0, 0u, o); break;
+#define L(...) hipLaunchKernelGGL((md5_desc<__VA_ARGS__>), g, dim3(256), 0, s, b, offs, lens, order, n, (uint64_t)0, 0u, o)
+  switch (kind) {
+    case 0: L(false, false, false, 2); break;
+    case 1: L(false, true, true, 2); break;
+    case 2: L(false, true, true, 4); break;
+    case 3: L(false, true, true, 8); break;
+    case 4: L(false, true, false, 8); break;
+    case 5: L(false, true, true, 12); break;
+    default: return -EINVAL;
   }
+#undef L
   return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }

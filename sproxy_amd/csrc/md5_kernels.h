@@ -421,7 +421,10 @@ __device__ __forceinline__ uint32_t wave_max(uint32_t v) {
 // raise their issue priority, so the longest serial chains -- which bound a
 // mixed batch -- progress at their latency limit while short-chunk waves fill
 // the remaining issue slots.
-template <bool kImplicit, bool kLat = true, bool kPrio = true>
+// D: depth of the per-lane register ring (blocks in flight per lane).  Mixed
+// batches have few waves per SIMD (C3: ~1.2), so latency must be hidden by
+// prefetch depth, not by occupancy.
+template <bool kImplicit, bool kLat = true, bool kPrio = true, int D = 8>
 __global__ void __launch_bounds__(256)
 md5_desc(const uint8_t* __restrict__ base, const uint64_t* __restrict__ offs,
          const uint32_t* __restrict__ lens, const uint32_t* __restrict__ order, uint64_t n,
@@ -443,17 +446,20 @@ md5_desc(const uint8_t* __restrict__ base, const uint64_t* __restrict__ offs,
     const uint4* p = reinterpret_cast<const uint4*>(chunk);
     if (nfull) {
       const uint32_t lastb = nfull - 1;
-      uint4 R0[4], R1[4];
-      load_block(R0, p);
-      load_block(R1, p + 4 * min(1u, lastb));
+      uint4 R[D][4];
+#pragma unroll
+      for (int j = 0; j < D; ++j) load_block(R[j], p + 4 * min((uint32_t)j, lastb));
       uint32_t blk = 0;
-      for (; blk + 2 <= nfull; blk += 2) {
-        compress_regs<kLat>(st, R0);
-        load_block(R0, p + 4 * min(blk + 2, lastb));
-        compress_regs<kLat>(st, R1);
-        load_block(R1, p + 4 * min(blk + 3, lastb));
+      for (; blk + D <= nfull; blk += D) {
+#pragma unroll
+        for (int j = 0; j < D; ++j) {
+          compress_regs<kLat>(st, R[j]);
+          load_block(R[j], p + 4 * min(blk + j + D, lastb));
+        }
       }
-      if (blk < nfull) compress_regs<kLat>(st, R0);
+#pragma unroll
+      for (int j = 0; j < D - 1; ++j)
+        if (blk + j < nfull) compress_regs<kLat>(st, R[j]);
     }
   } else {
     for (uint32_t blk = 0; blk < nfull; ++blk) {
