@@ -264,3 +264,38 @@ extern "C" int md5diag_desc(int kind, const void* base, const uint64_t* offs, co
 #undef L
   return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }
+
+// Placement / timing trace of the descriptor kernel: per wave, HW_ID,
+// XCC_ID, s_memrealtime (100 MHz) at start and end.  rec[4*wave + 0..3].
+template <int TPB>
+__global__ void __launch_bounds__(256)
+diag_desc_trace(const uint8_t* __restrict__ base, const uint64_t* __restrict__ offs,
+                const uint32_t* __restrict__ lens, const uint32_t* __restrict__ order, uint64_t n,
+                uint4* __restrict__ out, uint64_t* __restrict__ rec) {
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  desc_body<false, true, true, 2>(base, offs, lens, order, n, 0, 0u, out);
+  const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
+  if ((threadIdx.x & 63u) == 0) {
+    uint32_t hw, xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    const uint64_t w = ((uint64_t)blockIdx.x * TPB + threadIdx.x) >> 6;
+    rec[4 * w + 0] = hw;
+    rec[4 * w + 1] = xcc;
+    rec[4 * w + 2] = t0;
+    rec[4 * w + 3] = t1;
+  }
+}
+
+extern "C" int md5diag_desc_trace(int tpb, const void* base, const uint64_t* offs,
+                                  const uint32_t* lens, const uint32_t* order, uint64_t n,
+                                  void* out, void* rec, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  if (tpb == 256)
+    hipLaunchKernelGGL(diag_desc_trace<256>, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s,
+                       (const uint8_t*)base, offs, lens, order, n, (uint4*)out, (uint64_t*)rec);
+  else
+    hipLaunchKernelGGL(diag_desc_trace<64>, dim3((uint32_t)((n + 63) / 64)), dim3(64), 0, s,
+                       (const uint8_t*)base, offs, lens, order, n, (uint4*)out, (uint64_t*)rec);
+  return hipGetLastError() == hipSuccess ? 0 : -EIO;
+}

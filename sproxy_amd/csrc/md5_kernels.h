@@ -425,10 +425,11 @@ __device__ __forceinline__ uint32_t wave_max(uint32_t v) {
 // batches have few waves per SIMD (C3: ~1.2), so latency must be hidden by
 // prefetch depth, not by occupancy.
 template <bool kImplicit, bool kLat = true, bool kPrio = true, int D = 8>
-__global__ void __launch_bounds__(256)
-md5_desc(const uint8_t* __restrict__ base, const uint64_t* __restrict__ offs,
-         const uint32_t* __restrict__ lens, const uint32_t* __restrict__ order, uint64_t n,
-         uint64_t stride, uint32_t flen, uint4* __restrict__ out) {
+__device__ __forceinline__ void desc_body(const uint8_t* __restrict__ base,
+                                          const uint64_t* __restrict__ offs,
+                                          const uint32_t* __restrict__ lens,
+                                          const uint32_t* __restrict__ order, uint64_t n,
+                                          uint64_t stride, uint32_t flen, uint4* __restrict__ out) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const uint64_t c = (!kImplicit && order) ? (uint64_t)order[i] : i;
@@ -470,6 +471,14 @@ md5_desc(const uint8_t* __restrict__ base, const uint64_t* __restrict__ offs,
   }
   finish_message(st, chunk + ((uint64_t)nfull << 6), len & 63u, len);
   store_digest(out, c, st);
+}
+
+template <bool kImplicit, bool kLat = true, bool kPrio = true, int D = 8>
+__global__ void __launch_bounds__(256)
+md5_desc(const uint8_t* __restrict__ base, const uint64_t* __restrict__ offs,
+         const uint32_t* __restrict__ lens, const uint32_t* __restrict__ order, uint64_t n,
+         uint64_t stride, uint32_t flen, uint4* __restrict__ out) {
+  desc_body<kImplicit, kLat, kPrio, D>(base, offs, lens, order, n, stride, flen, out);
 }
 
 // ---------------------------------------------------------------------------
