@@ -62,8 +62,8 @@ def main():
     out = torch.empty((lens.size, 16), dtype=torch.uint8, device="cuda")
     st = torch.cuda.current_stream().cuda_stream
     ref = None
-    for kind, name in [(0, "r1"), (1, "lat_prio_D2"), (2, "D4"), (3, "D8"), (4, "D8_noprio"),
-                       (5, "D12")]:
+    for kind, name in [(0, "r1"), (1, "lat_prio_D2"), (3, "D8"), (16, "r1_t64"),
+                       (17, "lat_prio_D2_t64"), (18, "D4_t64"), (19, "D8_t64"), (20, "D8_noprio_t64")]:
         f = lambda: D.md5diag_desc(kind, data.data_ptr(), d_off.data_ptr(), d_len.data_ptr(),  # noqa
                                    order.data_ptr(), lens.size, out.data_ptr(), st)
         ms = timeit(f, reps=2, rounds=3)
@@ -81,7 +81,8 @@ def main():
     m.fill_synthetic(d4, seed=4)
     l4 = torch.from_numpy(lens4.astype(np.int32)).cuda()
     o4 = torch.empty((n4, 16), dtype=torch.uint8, device="cuda")
-    for kind, name in [(0, "r1"), (1, "lat_prio_D2"), (2, "D4"), (3, "D8"), (5, "D12")]:
+    for kind, name in [(0, "r1"), (1, "lat_prio_D2"), (3, "D8"), (16, "r1_t64"), (17, "lat_prio_D2_t64"),
+                       (19, "D8_t64")]:
         f = lambda: D.md5diag_desc(kind, d4.data_ptr(), offs4.data_ptr(), l4.data_ptr(), None,  # noqa
                                    n4, o4.data_ptr(), st)
         ms = timeit(f, reps=3, rounds=3)

@@ -244,15 +244,17 @@ extern "C" int md5diag_run(int kind, const void* base, uint64_t n, uint32_t len,
 }
 
 // Descriptor-kernel A/B (C3): 0 = (no kLat, no prio, D=2: round-1 kernel),
-// 1 = (kLat, prio, D=2), 2 = D=4, 3 = D=8, 4 = D=8 without prio, 5 = D=12.
+// 1 = (kLat, prio, D=2), 2 = D=4, 3 = D=8, 4 = D=8 without prio, 5 = D=12;
+// +16: the same with 64-thread workgroups.
 extern "C" int md5diag_desc(int kind, const void* base, const uint64_t* offs, const uint32_t* lens,
                             const uint32_t* order, uint64_t n, void* out, void* stream) {
   hipStream_t s = (hipStream_t)stream;
-  const dim3 g((uint32_t)((n + 255) / 256));
+  const uint32_t tpb = (kind & 16) ? 64u : 256u;
+  const dim3 g((uint32_t)((n + tpb - 1) / tpb));
   const uint8_t* b = (const uint8_t*)base;
   uint4* o = (uint4*)out;
-#define L(...) hipLaunchKernelGGL((md5_desc<__VA_ARGS__>), g, dim3(256), 0, s, b, offs, lens, order, n, (uint64_t)0, 0u, o)
-  switch (kind) {
+#define L(...) hipLaunchKernelGGL((md5_desc<__VA_ARGS__>), g, dim3(tpb), 0, s, b, offs, lens, order, n, (uint64_t)0, 0u, o)
+  switch (kind & 15) {
     case 0: L(false, false, false, 2); break;
     case 1: L(false, true, true, 2); break;
     case 2: L(false, true, true, 4); break;
