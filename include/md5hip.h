@@ -76,6 +76,22 @@ int md5hip_digest_desc(const void *d_base, const uint64_t *d_offsets, const uint
                        void *stream);
 
 /*
+ * CRC-32 block checksums -- the checksum netcache itself computes at the
+ * block-completion site: nc_crc_t blk_make_crc(inode, blk, len, fastcrc)
+ * (netcache/common/blk_io.c:354-430, compiled with NC_ENABLE_CRC), CRC-32
+ * from netcache/netcache/crc32.c (zlib polynomial 0xEDB88320, crc32.c:22).
+ *   crcs[i] = fastcrc == 0 || len_i <= fastcrc ? crc32(chunk_i)
+ *           : crc32(first fastcrc bytes) ^ crc32(last fastcrc bytes)
+ * exactly as blk_io.c:408-424 combines them.  Same conventions as the MD5
+ * entries; fastcrc must be a multiple of 4 (cfs_apix.c:2222-2236).
+ */
+int crc32hip_fixed(const void *d_base, uint64_t n, uint32_t len, uint64_t stride,
+                   uint32_t fastcrc, uint32_t *d_crcs, void *stream);
+int crc32hip_desc(const void *d_base, const uint64_t *d_offsets, const uint32_t *d_lens,
+                  const uint32_t *d_order, uint64_t n, uint32_t fastcrc, uint32_t *d_crcs,
+                  void *stream);
+
+/*
  * Host helper: order[] = indices of lens[] sorted by MD5 block count,
  * descending (stable counting sort, O(n)).  Synchronous, host memory.
  */

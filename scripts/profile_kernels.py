@@ -40,6 +40,11 @@ def main():
     def prod(v):
         return lambda: m.digest_fixed(data, n, L, out=out[:n], variant=v)
 
+    crc_out = torch.empty(n, dtype=torch.int32, device="cuda")
+
+    def crc():
+        return lambda: m.crc32_fixed(data, n, L, out=crc_out)
+
     def diag(kind):
         def f():
             rc = DIAG.md5diag_run(kind, data.data_ptr(), n, L, L, out.data_ptr(), stream.cuda_stream)
@@ -51,7 +56,7 @@ def main():
              "load_direct4": diag(2), "load_lds64": diag(3), "load_lds128": diag(4),
              "stream_read": diag(5), "xpose1": prod("xpose1"), "xpose2": prod("xpose2"),
              "xpose1nt": prod("xpose1nt"), "xpose2nt": prod("xpose2nt"), "lds128nt": prod("lds128nt"),
-             "load_xpose1": diag(6), "load_xpose2": diag(7)}
+             "load_xpose1": diag(6), "load_xpose2": diag(7), "crc32": crc()}
     if a.only:
         cases = {k: v for k, v in cases.items() if k in a.only.split(",")}
     times = {k: [] for k in cases}

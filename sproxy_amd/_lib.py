@@ -64,6 +64,8 @@ def lib():
         "md5hip_digest_fixed_variant": (i, [vp, u64, u32, u64, vp, vp, i]),
         "md5hip_digest_desc": (i, [vp, vp, vp, vp, u64, vp, vp]),
         "md5hip_plan_order": (i, [vp, u64, vp]),
+        "crc32hip_fixed": (i, [vp, u64, u32, u64, u32, vp, vp]),
+        "crc32hip_desc": (i, [vp, vp, vp, vp, u64, u32, vp, vp]),
         "md5hip_fill_synthetic": (i, [vp, u64, u64, vp]),
         "md5hip_batcher_create": (i, [i, u64, u32, ctypes.POINTER(vp)]),
         "md5hip_batcher_destroy": (None, [vp]),
@@ -84,6 +86,7 @@ EXPORTS = ["MD5Init", "MD5Update", "MD5Final", "md5hip_abi_version", "md5hip_var
            "md5hip_resolve_variant",
            "md5hip_digest_fixed", "md5hip_digest_fixed_variant", "md5hip_digest_desc",
            "md5hip_plan_order", "md5hip_fill_synthetic", "md5hip_batcher_create",
+           "crc32hip_fixed", "crc32hip_desc",
            "md5hip_batcher_destroy", "md5_batch_submit", "md5_batch_submit_iov",
            "md5hip_batch_host_fixed"]
 

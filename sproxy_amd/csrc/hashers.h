@@ -1,0 +1,189 @@
+// hashers.h -- per-chunk digest policies plugged into the batched loaders of
+// md5_kernels.h.  A hasher H provides
+//   typename H::State, typename H::Out
+//   void setup(uint8_t* lds)            once per workgroup, all threads, before
+//                                       any early exit (may __syncthreads)
+//   State init()
+//   void block(State&, const uint4 (&w)[4])          one full 64-byte block
+//   void finish(State&, tail, r, len)                the last len % 64 bytes
+//   void store(Out* out, uint64_t i, const State&)
+//
+//   Md5Hasher<kLat>  md5.c:153-265 (MD5Init / Update / Final per chunk)
+//   Crc32Hasher      netcache crc32.c:186-240 (slicing-by-8 over LDS tables)
+//   FoldHasher       diagnostics only: 16-word xor fold (load-path ceilings)
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "md5_core.h"
+
+namespace md5hip {
+
+__device__ __forceinline__ uint32_t keep_bytes(uint32_t w, int nbytes) {
+  // keep the low `nbytes` (0..4) bytes of w
+  return nbytes >= 4 ? w : nbytes <= 0 ? 0u : (w & ((1u << (8 * nbytes)) - 1u));
+}
+
+// The r (< 64) bytes at `tail` as 16 little-endian words, bytes past r zero.
+// Only granules that hold message bytes are read; a 16-B (aligned) or 4-B
+// (unaligned) granule never crosses a page, so reading past r cannot fault.
+__device__ __forceinline__ void load_tail(const uint8_t* tail, uint32_t r, uint32_t (&w)[16]) {
+  const uintptr_t addr = (uintptr_t)tail;
+  if ((addr & 15u) == 0) {
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      uint4 q = make_uint4(0, 0, 0, 0);
+      if ((uint32_t)g * 16u < r) q = *reinterpret_cast<const uint4*>(tail + 16 * g);
+      w[4 * g + 0] = q.x; w[4 * g + 1] = q.y; w[4 * g + 2] = q.z; w[4 * g + 3] = q.w;
+    }
+  } else {
+    // unaligned tail: aligned dword loads + funnel shift (v_alignbit_b32)
+    const uint32_t* base = reinterpret_cast<const uint32_t*>(addr & ~(uintptr_t)3);
+    const uint32_t sh = (uint32_t)(addr & 3u) * 8u;
+    const uint32_t nwords = (((uint32_t)(addr & 3u)) + r + 3u) >> 2;   // words touched
+    uint32_t prev = r ? base[0] : 0u;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      uint32_t next = ((uint32_t)j + 1u < nwords) ? base[j + 1] : 0u;
+      w[j] = __builtin_amdgcn_alignbit(next, prev, sh);
+      prev = next;
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 16; ++j) w[j] = keep_bytes(w[j], (int)r - 4 * j);
+}
+
+// ---------------------------------------------------------------------------
+// MD5 (md5.c).  Digest = A,B,C,D little-endian (md5.c:262-263).
+// ---------------------------------------------------------------------------
+template <bool kLat = false>
+struct Md5Hasher {
+  using State = md5hip::State;
+  using Out = uint4;
+  __device__ __forceinline__ void setup(uint8_t*) {}
+  __device__ __forceinline__ State init() { return initial_state(); }
+  __device__ __forceinline__ void block(State& st, const uint4 (&w)[4]) { compress_regs<kLat>(st, w); }
+  // 0x80, zeros, 64-bit bit count (md5.c:221-261); one or two final blocks.
+  __device__ __forceinline__ void finish(State& st, const uint8_t* tail, uint32_t r,
+                                         uint64_t len_bytes) {
+    const uint32_t bits_lo = (uint32_t)(len_bytes << 3);
+    const uint32_t bits_hi = (uint32_t)(len_bytes >> 29);
+    if (r == 0) {
+      compress_pad_only(st, bits_lo, bits_hi);
+      return;
+    }
+    uint32_t w[16];
+    load_tail(tail, r, w);
+#pragma unroll
+    for (int j = 0; j < 16; ++j)
+      if ((uint32_t)j == (r >> 2)) w[j] |= 0x80u << (8 * (r & 3u));
+    if (r < 56) {
+      w[14] = bits_lo;
+      w[15] = bits_hi;
+      compress(st, [&](int i) __attribute__((always_inline)) { return w[i]; });
+    } else {
+      compress(st, [&](int i) __attribute__((always_inline)) { return w[i]; });
+      compress(st, [&](int i) __attribute__((always_inline)) -> uint32_t {
+        return i == 14 ? bits_lo : i == 15 ? bits_hi : 0u;
+      });
+    }
+  }
+  __device__ __forceinline__ void store(Out* out, uint64_t idx, const State& st) {
+    out[idx] = make_uint4(st.a, st.b, st.c, st.d);
+  }
+};
+
+// Diagnostics: consumes all 16 words with a cheap fold (no MD5).
+struct FoldHasher : Md5Hasher<false> {
+  __device__ __forceinline__ void block(State& st, const uint4 (&w)[4]) {
+    st.a ^= w[0].x ^ w[0].y ^ w[0].z ^ w[0].w;
+    st.b ^= w[1].x ^ w[1].y ^ w[1].z ^ w[1].w;
+    st.c ^= w[2].x ^ w[2].y ^ w[2].z ^ w[2].w;
+    st.d ^= w[3].x ^ w[3].y ^ w[3].z ^ w[3].w;
+  }
+};
+
+// ---------------------------------------------------------------------------
+// CRC-32 (netcache crc32.c): zlib polynomial 0xEDB88320 (crc32.c:22),
+// init ~0, final ~, slicing-by-8 little-endian form (crc32.c:186-240).  The
+// eight 256-entry tables (crc32.c:251+) are built at compile time and copied
+// into 8 KiB of LDS per workgroup; every byte costs one ds_read_b32.
+// ---------------------------------------------------------------------------
+struct CrcTables {
+  uint32_t t[8][256];
+  constexpr CrcTables() : t() {
+    for (uint32_t i = 0; i < 256; ++i) {
+      uint32_t c = i;
+      for (int k = 0; k < 8; ++k) c = (c & 1u) ? (c >> 1) ^ 0xEDB88320u : (c >> 1);
+      t[0][i] = c;
+    }
+    for (uint32_t i = 0; i < 256; ++i)
+      for (int s = 1; s < 8; ++s) t[s][i] = (t[s - 1][i] >> 8) ^ t[0][t[s - 1][i] & 0xFFu];
+  }
+};
+__constant__ const CrcTables kCrcTables{};
+
+struct Crc32State {
+  uint32_t c;
+};
+
+struct Crc32Hasher {
+  using State = Crc32State;
+  using Out = uint32_t;
+  const uint32_t* tab;   // 2048 words in LDS: table s at tab + 256*s
+  static constexpr int kLdsBytes = 8192;
+  __device__ __forceinline__ void setup(uint8_t* lds) {
+    uint32_t* t = reinterpret_cast<uint32_t*>(lds);
+    const uint32_t* src = &kCrcTables.t[0][0];
+    for (uint32_t k = threadIdx.x; k < 2048u; k += blockDim.x) t[k] = src[k];
+    __syncthreads();
+    tab = t;
+  }
+  __device__ __forceinline__ State init() { return State{0xFFFFFFFFu}; }
+  __device__ __forceinline__ uint32_t step8(uint32_t c, uint32_t one, uint32_t two) const {
+    one ^= c;
+    return tab[0 * 256 + (two >> 24)] ^ tab[1 * 256 + ((two >> 16) & 0xFFu)] ^
+           tab[2 * 256 + ((two >> 8) & 0xFFu)] ^ tab[3 * 256 + (two & 0xFFu)] ^
+           tab[4 * 256 + (one >> 24)] ^ tab[5 * 256 + ((one >> 16) & 0xFFu)] ^
+           tab[6 * 256 + ((one >> 8) & 0xFFu)] ^ tab[7 * 256 + (one & 0xFFu)];
+  }
+  __device__ __forceinline__ void block(State& st, const uint4 (&w)[4]) {
+    uint32_t c = st.c;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      c = step8(c, w[k].x, w[k].y);
+      c = step8(c, w[k].z, w[k].w);
+    }
+    st.c = c;
+  }
+  __device__ __forceinline__ void finish(State& st, const uint8_t* tail, uint32_t r, uint64_t) {
+    uint32_t c = st.c;
+    if (r) {
+      uint32_t w[16];
+      load_tail(tail, r, w);
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if ((uint32_t)(8 * j + 8) <= r) c = step8(c, w[2 * j], w[2 * j + 1]);
+      // remaining 1..7 bytes, one at a time (crc32.c:236-238)
+      const uint32_t done = r & ~7u;
+#pragma unroll
+      for (int b = 0; b < 7; ++b) {
+        const uint32_t pos = done + (uint32_t)b;
+        if (pos < r) {
+          uint32_t wd = w[0];
+#pragma unroll
+          for (int j = 1; j < 16; ++j)
+            if ((uint32_t)j == (pos >> 2)) wd = w[j];
+          const uint32_t byte = (wd >> (8 * (pos & 3u))) & 0xFFu;
+          c = tab[(c ^ byte) & 0xFFu] ^ (c >> 8);
+        }
+      }
+    }
+    st.c = ~c;
+  }
+  __device__ __forceinline__ void store(Out* out, uint64_t idx, const State& st) {
+    out[idx] = st.c;
+  }
+};
+
+}  // namespace md5hip

@@ -19,8 +19,8 @@
 
 namespace md5hip {
 
-template __global__ void md5_fixed_direct<2, 1>(const uint8_t*, uint64_t, uint32_t, uint64_t, uint4*);
-template __global__ void md5_fixed_direct<4, 1>(const uint8_t*, uint64_t, uint32_t, uint64_t, uint4*);
+template __global__ void md5_fixed_direct<2, FoldHasher>(const uint8_t*, uint64_t, uint32_t, uint64_t, uint4*);
+template __global__ void md5_fixed_direct<4, FoldHasher>(const uint8_t*, uint64_t, uint32_t, uint64_t, uint4*);
 #define DESC_INST(L, P, D)                                                                  \
   template __global__ void md5_desc<false, L, P, D>(const uint8_t*, const uint64_t*,       \
                                                     const uint32_t*, const uint32_t*, uint64_t, \
@@ -33,28 +33,28 @@ __global__ void __launch_bounds__(256)
 diag_lds64_load(const uint8_t* __restrict__ base, uint64_t n, uint32_t len, uint64_t stride,
                 uint4* __restrict__ out) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds_dyn[];
-  fixed_lds_body<64, 1>(base, n, len, stride, out, lds_dyn);
+  fixed_lds_body<64, FoldHasher>(base, n, len, stride, out, lds_dyn);
 }
 
 __global__ void __launch_bounds__(256)
 diag_lds128_load(const uint8_t* __restrict__ base, uint64_t n, uint32_t len, uint64_t stride,
                  uint4* __restrict__ out) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds_dyn[];
-  fixed_lds_body<128, 1>(base, n, len, stride, out, lds_dyn);
+  fixed_lds_body<128, FoldHasher>(base, n, len, stride, out, lds_dyn);
 }
 
 __global__ void __launch_bounds__(256)
 diag_xpose1_load(const uint8_t* __restrict__ base, uint64_t n, uint32_t len, uint64_t stride,
                  uint4* __restrict__ out) {
   __shared__ __attribute__((aligned(16))) uint8_t img[4 * 8192];
-  fixed_xpose_body<1, 1>(base, n, len, stride, out, img);
+  fixed_xpose_body<1, FoldHasher>(base, n, len, stride, out, img);
 }
 
 __global__ void __launch_bounds__(256)
 diag_xpose2_load(const uint8_t* __restrict__ base, uint64_t n, uint32_t len, uint64_t stride,
                  uint4* __restrict__ out) {
   __shared__ __attribute__((aligned(16))) uint8_t img[4 * 8192];
-  fixed_xpose_body<2, 1>(base, n, len, stride, out, img);
+  fixed_xpose_body<2, FoldHasher>(base, n, len, stride, out, img);
 }
 
 // Compute only: lane L hashes `nblocks` blocks whose words it re-reads from its
@@ -196,10 +196,10 @@ extern "C" int md5diag_run(int kind, const void* base, uint64_t n, uint32_t len,
       break;
     }
     case 1:
-      hipLaunchKernelGGL((md5_fixed_direct<2, 1>), dim3(grid), dim3(256), 0, s, b, n, len, stride, o);
+      hipLaunchKernelGGL((md5_fixed_direct<2, FoldHasher>), dim3(grid), dim3(256), 0, s, b, n, len, stride, o);
       break;
     case 2:
-      hipLaunchKernelGGL((md5_fixed_direct<4, 1>), dim3(grid), dim3(256), 0, s, b, n, len, stride, o);
+      hipLaunchKernelGGL((md5_fixed_direct<4, FoldHasher>), dim3(grid), dim3(256), 0, s, b, n, len, stride, o);
       break;
     case 3: {
       const size_t lds = 4 * 2 * 64 * 64;
@@ -275,7 +275,7 @@ diag_desc_trace(const uint8_t* __restrict__ base, const uint64_t* __restrict__ o
                 const uint32_t* __restrict__ lens, const uint32_t* __restrict__ order, uint64_t n,
                 uint4* __restrict__ out, uint64_t* __restrict__ rec) {
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-  desc_body<false, true, true, 2>(base, offs, lens, order, n, 0, 0u, out);
+  desc_body<false, Md5Hasher<true>, true, 2>(base, offs, lens, order, n, 0, 0u, out);
   const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
   if ((threadIdx.x & 63u) == 0) {
     uint32_t hw, xcc;

@@ -1,4 +1,5 @@
-// md5_kernels.h -- batched MD5 over independent chunks, hand-written for gfx950.
+// md5_kernels.h -- batched per-chunk digests (MD5, CRC32) over independent
+// chunks, hand-written for gfx950; the digest is a policy (hashers.h).
 //
 // One lane hashes one chunk (MD5 is a strict 64-step chain per block, so the
 // only parallelism is across chunks).  A 64-lane wave owns 64 chunks.  What
@@ -20,86 +21,10 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "hashers.h"
 #include "md5_core.h"
 
 namespace md5hip {
-
-// ---------------------------------------------------------------------------
-// Final block(s): the r = len % 64 trailing bytes at `tail` (16-B aligned when
-// `aligned`), then 0x80, zeros, and the 64-bit bit count (md5.c:221-261).
-// Only granules that hold message bytes are read; a 16-B granule never
-// crosses a page, so reading its bytes past `len` cannot fault.
-// ---------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t keep_bytes(uint32_t w, int nbytes) {
-  // keep the low `nbytes` (0..4) bytes of w
-  return nbytes >= 4 ? w : nbytes <= 0 ? 0u : (w & ((1u << (8 * nbytes)) - 1u));
-}
-
-__device__ __forceinline__ void finish_message(State& st, const uint8_t* tail, uint32_t r,
-                                               uint64_t len_bytes) {
-  const uint32_t bits_lo = (uint32_t)(len_bytes << 3);
-  const uint32_t bits_hi = (uint32_t)(len_bytes >> 29);
-  if (r == 0) {
-    compress_pad_only(st, bits_lo, bits_hi);
-    return;
-  }
-  uint32_t w[16];
-  const uintptr_t addr = (uintptr_t)tail;
-  if ((addr & 15u) == 0) {
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      uint4 q = make_uint4(0, 0, 0, 0);
-      if ((uint32_t)g * 16u < r) q = *reinterpret_cast<const uint4*>(tail + 16 * g);
-      w[4 * g + 0] = q.x; w[4 * g + 1] = q.y; w[4 * g + 2] = q.z; w[4 * g + 3] = q.w;
-    }
-  } else {
-    // unaligned tail: aligned dword loads + funnel shift (v_alignbit_b32)
-    const uint32_t* base = reinterpret_cast<const uint32_t*>(addr & ~(uintptr_t)3);
-    const uint32_t sh = (uint32_t)(addr & 3u) * 8u;
-    const uint32_t nwords = (((uint32_t)(addr & 3u)) + r + 3u) >> 2;   // words touched
-    uint32_t prev = base[0];
-#pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      uint32_t next = ((uint32_t)j + 1u < nwords) ? base[j + 1] : 0u;
-      w[j] = __builtin_amdgcn_alignbit(next, prev, sh);
-      prev = next;
-    }
-  }
-#pragma unroll
-  for (int j = 0; j < 16; ++j) {
-    w[j] = keep_bytes(w[j], (int)r - 4 * j);
-    if ((uint32_t)j == (r >> 2)) w[j] |= 0x80u << (8 * (r & 3u));
-  }
-  if (r < 56) {
-    w[14] = bits_lo;
-    w[15] = bits_hi;
-    compress(st, [&](int i) __attribute__((always_inline)) { return w[i]; });
-  } else {
-    compress(st, [&](int i) __attribute__((always_inline)) { return w[i]; });
-    compress(st, [&](int i) __attribute__((always_inline)) -> uint32_t {
-      return i == 14 ? bits_lo : i == 15 ? bits_hi : 0u;
-    });
-  }
-}
-
-__device__ __forceinline__ void store_digest(uint4* out, uint64_t idx, const State& st) {
-  out[idx] = make_uint4(st.a, st.b, st.c, st.d);  // md5.c:262-263, LE bytes
-}
-
-// Per-block work.  MODE 0 is the product (MD5 compression); MODE 1 is a
-// diagnostic cheap fold that still consumes all 16 words, used only by the
-// load-path ceiling measurements in md5_diag.hip.
-template <int MODE>
-__device__ __forceinline__ void block_op(State& st, const uint4 (&w)[4]) {
-  if constexpr (MODE == 0) {
-    compress_regs(st, w);
-  } else {
-    st.a ^= w[0].x ^ w[0].y ^ w[0].z ^ w[0].w;
-    st.b ^= w[1].x ^ w[1].y ^ w[1].z ^ w[1].w;
-    st.c ^= w[2].x ^ w[2].y ^ w[2].z ^ w[2].w;
-    st.d ^= w[3].x ^ w[3].y ^ w[3].z ^ w[3].w;
-  }
-}
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
@@ -116,16 +41,18 @@ __device__ __forceinline__ void load_block(uint4 (&r)[4], const uint4* p) {
 // ---------------------------------------------------------------------------
 // Fixed-length, lane-direct loads.  base/stride 16-B aligned, len <= stride.
 // ---------------------------------------------------------------------------
-template <int D, int MODE = 0>
+// (hashers without LDS state only: Md5Hasher, FoldHasher)
+template <int D, class H = Md5Hasher<false>>
 __global__ void __launch_bounds__(256)
 md5_fixed_direct(const uint8_t* __restrict__ base, uint64_t n, uint32_t len, uint64_t stride,
-                 uint4* __restrict__ out) {
+                 typename H::Out* __restrict__ out) {
+  H h;
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const uint8_t* chunk = base + i * stride;
   const uint4* p = reinterpret_cast<const uint4*>(chunk);
   const uint32_t nfull = len >> 6;
-  State st = initial_state();
+  typename H::State st = h.init();
   if (nfull) {
     // D-deep register ring.  Prefetch indices are clamped to the last block so
     // every load is unconditional (no phi copies); the <= D re-reads at the end
@@ -138,16 +65,16 @@ md5_fixed_direct(const uint8_t* __restrict__ base, uint64_t n, uint32_t len, uin
     for (; blk + D <= nfull; blk += D) {   // steady state: no conditionals, so
 #pragma unroll                              // the waits stay counted (vmcnt(4*(D-1)))
       for (int j = 0; j < D; ++j) {
-        block_op<MODE>(st, R[j]);
+        h.block(st, R[j]);
         load_block(R[j], p + 4 * min(blk + j + D, lastb));
       }
     }
 #pragma unroll
     for (int j = 0; j < D - 1; ++j)
-      if (blk + j < nfull) block_op<MODE>(st, R[j]);
+      if (blk + j < nfull) h.block(st, R[j]);
   }
-  finish_message(st, chunk + ((uint64_t)nfull << 6), len & 63u, len);
-  store_digest(out, i, st);
+  h.finish(st, chunk + ((uint64_t)nfull << 6), len & 63u, len);
+  h.store(out, i, st);
 }
 
 // ---------------------------------------------------------------------------
@@ -168,10 +95,11 @@ __device__ __forceinline__ uint32_t swz(uint32_t row) {
   return BB == 64 ? ((row >> 2) & 3u) : ((row >> 1) & 7u);
 }
 
-template <int BB, int MODE = 0, int CP = 0>
+template <int BB, class H = Md5Hasher<false>, int CP = 0>
 __device__ __forceinline__ void fixed_lds_body(const uint8_t* __restrict__ base, uint64_t n,
                                                uint32_t len, uint64_t stride,
-                                               uint4* __restrict__ out, uint8_t* lds) {
+                                               typename H::Out* __restrict__ out, uint8_t* lds) {
+  H h;
   constexpr int LPC = BB / 16;         // lanes per chunk in one DMA instruction
   constexpr int CPI = 64 / LPC;        // chunks per DMA instruction
   constexpr int NI = 64 / CPI;         // DMA instructions per stage
@@ -205,7 +133,7 @@ __device__ __forceinline__ void fixed_lds_body(const uint8_t* __restrict__ base,
       __builtin_amdgcn_global_load_lds(src[r] + (size_t)stg * BB, dst + r * 1024, 16, 0, CP);
   };
 
-  State st = initial_state();
+  typename H::State st = h.init();
   if (nstage) issue(0);
   const uint32_t g = swz<BB>(lane) & (LPC - 1);
   for (uint32_t stg = 0; stg < nstage; ++stg) {
@@ -224,7 +152,7 @@ __device__ __forceinline__ void fixed_lds_body(const uint8_t* __restrict__ base,
       }
     if (stg + 1 < nstage) issue(stg + 1);
 #pragma unroll
-    for (int b = 0; b < BPS; ++b) block_op<MODE>(st, w[b]);
+    for (int b = 0; b < BPS; ++b) h.block(st, w[b]);
   }
   // leftover whole blocks (nfull % BPS), then the tail
   const uint64_t i = wave_first + lane;
@@ -233,10 +161,10 @@ __device__ __forceinline__ void fixed_lds_body(const uint8_t* __restrict__ base,
   for (uint32_t blk = nstage * BPS; blk < nfull; ++blk) {
     uint4 w[4];
     load_block(w, reinterpret_cast<const uint4*>(chunk + ((uint64_t)blk << 6)));
-    compress_regs(st, w);
+    h.block(st, w);
   }
-  finish_message(st, chunk + ((uint64_t)nfull << 6), len & 63u, len);
-  if (i <= last) store_digest(out, i, st);
+  h.finish(st, chunk + ((uint64_t)nfull << 6), len & 63u, len);
+  if (i <= last) h.store(out, i, st);
 }
 
 // ---------------------------------------------------------------------------
@@ -253,10 +181,13 @@ __device__ __forceinline__ void fixed_lds_body(const uint8_t* __restrict__ base,
 // occupancy is set by VGPRs, not LDS, and all waits are compiler-counted.
 // Requires 64 * stride < 2^31 (checked by the launcher).
 // ---------------------------------------------------------------------------
-template <int D, int MODE = 0, int CP = 0>
+template <int D, class H = Md5Hasher<false>, int CP = 0>
 __device__ __forceinline__ void fixed_xpose_body(const uint8_t* __restrict__ base, uint64_t n,
                                                  uint32_t len, uint64_t stride,
-                                                 uint4* __restrict__ out, uint8_t* lds) {
+                                                 typename H::Out* __restrict__ out, uint8_t* lds,
+                                                 uint8_t* hlds = nullptr) {
+  H h;
+  h.setup(hlds);                     // before any early exit (may barrier)
   const uint32_t lane = threadIdx.x & 63u;
   // readfirstlane: the descriptor must be provably wave-uniform, or hipcc
   // wraps every buffer load in a waterfall loop (cdna_hip_programming.md T20)
@@ -279,7 +210,7 @@ __device__ __forceinline__ void fixed_xpose_body(const uint8_t* __restrict__ bas
   const uint32_t g = (lane >> 1) & 7u;
   const uint32_t nfull = len >> 6;
   const uint32_t nstage = nfull >> 1;                 // 128-B stages
-  State st = initial_state();
+  typename H::State st = h.init();
 
   auto load_stage = [&](u32x4 (&R)[8], uint32_t stg) __attribute__((always_inline)) {
 #pragma unroll
@@ -300,8 +231,8 @@ __device__ __forceinline__ void fixed_xpose_body(const uint8_t* __restrict__ bas
     __builtin_amdgcn_wave_barrier();
     load_stage(R, next);                              // refill this ring slot
     __builtin_amdgcn_sched_barrier(0);                // keep the refill ahead of the
-    block_op<MODE>(st, w[0]);                         // compression (hipcc sinks it)
-    block_op<MODE>(st, w[1]);
+    h.block(st, w[0]);                                // compression (hipcc sinks it)
+    h.block(st, w[1]);
   };
 
   if (nstage) {
@@ -325,10 +256,10 @@ __device__ __forceinline__ void fixed_xpose_body(const uint8_t* __restrict__ bas
   if (nfull & 1u) {
     uint4 w[4];
     load_block(w, reinterpret_cast<const uint4*>(chunk + ((uint64_t)(nfull - 1) << 6)));
-    block_op<MODE>(st, w);
+    h.block(st, w);
   }
-  finish_message(st, chunk + ((uint64_t)nfull << 6), len & 63u, len);
-  if (lane < rows) store_digest(out, i, st);
+  h.finish(st, chunk + ((uint64_t)nfull << 6), len & 63u, len);
+  if (lane < rows) h.store(out, i, st);
 }
 
 // Non-template entry points (hipcc mis-handles explicitly instantiated
@@ -360,21 +291,21 @@ __global__ void __launch_bounds__(256)
 md5_fixed_xpose1nt(const uint8_t* __restrict__ base, uint64_t n, uint32_t len, uint64_t stride,
                    uint4* __restrict__ out) {
   __shared__ __attribute__((aligned(16))) uint8_t img[4 * 8192];
-  fixed_xpose_body<1, 0, 2>(base, n, len, stride, out, img);
+  fixed_xpose_body<1, Md5Hasher<false>, 2>(base, n, len, stride, out, img);
 }
 
 __global__ void __launch_bounds__(256)
 md5_fixed_xpose2nt(const uint8_t* __restrict__ base, uint64_t n, uint32_t len, uint64_t stride,
                    uint4* __restrict__ out) {
   __shared__ __attribute__((aligned(16))) uint8_t img[4 * 8192];
-  fixed_xpose_body<2, 0, 2>(base, n, len, stride, out, img);
+  fixed_xpose_body<2, Md5Hasher<false>, 2>(base, n, len, stride, out, img);
 }
 
 __global__ void __launch_bounds__(256)
 md5_fixed_lds128nt(const uint8_t* __restrict__ base, uint64_t n, uint32_t len, uint64_t stride,
                    uint4* __restrict__ out) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds_dyn[];
-  fixed_lds_body<128, 0, 2>(base, n, len, stride, out, lds_dyn);
+  fixed_lds_body<128, Md5Hasher<false>, 2>(base, n, len, stride, out, lds_dyn);
 }
 
 __global__ void __launch_bounds__(256)
@@ -415,6 +346,42 @@ __device__ __forceinline__ uint32_t wave_max(uint32_t v) {
   return __builtin_amdgcn_readfirstlane(v);
 }
 
+// One lane digests [chunk, chunk + len) into st (blocks + finish): aligned
+// chunks through a D-deep dwordx4 register ring, unaligned ones through
+// dword loads + v_alignbit_b32.
+template <class H, int D>
+__device__ __forceinline__ void lane_range(H& h, typename H::State& st, const uint8_t* chunk,
+                                           uint32_t len) {
+  const uint32_t nfull = len >> 6;
+  if (((uintptr_t)chunk & 15u) == 0) {
+    const uint4* p = reinterpret_cast<const uint4*>(chunk);
+    if (nfull) {
+      const uint32_t lastb = nfull - 1;
+      uint4 R[D][4];
+#pragma unroll
+      for (int j = 0; j < D; ++j) load_block(R[j], p + 4 * min((uint32_t)j, lastb));
+      uint32_t blk = 0;
+      for (; blk + D <= nfull; blk += D) {
+#pragma unroll
+        for (int j = 0; j < D; ++j) {
+          h.block(st, R[j]);
+          load_block(R[j], p + 4 * min(blk + j + D, lastb));
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < D - 1; ++j)
+        if (blk + j < nfull) h.block(st, R[j]);
+    }
+  } else {
+    for (uint32_t blk = 0; blk < nfull; ++blk) {
+      uint4 w[4];
+      load_block_unaligned(w, chunk + ((uint64_t)blk << 6));
+      h.block(st, w);
+    }
+  }
+  h.finish(st, chunk + ((uint64_t)nfull << 6), len & 63u, len);
+}
+
 // kImplicit: chunk i at base + i*stride with length `flen` (the fixed-length
 // API's fallback for chunk starts that are not 16-B aligned).
 // kLat: latency-form step (md5_core.h).  kPrio: waves holding long chunks
@@ -424,12 +391,16 @@ __device__ __forceinline__ uint32_t wave_max(uint32_t v) {
 // D: depth of the per-lane register ring (blocks in flight per lane).  Mixed
 // batches have few waves per SIMD (C3: ~1.2), so latency must be hidden by
 // prefetch depth, not by occupancy.
-template <bool kImplicit, bool kLat = true, bool kPrio = true, int D = 8>
+template <bool kImplicit, class H = Md5Hasher<true>, bool kPrio = true, int D = 8>
 __device__ __forceinline__ void desc_body(const uint8_t* __restrict__ base,
                                           const uint64_t* __restrict__ offs,
                                           const uint32_t* __restrict__ lens,
                                           const uint32_t* __restrict__ order, uint64_t n,
-                                          uint64_t stride, uint32_t flen, uint4* __restrict__ out) {
+                                          uint64_t stride, uint32_t flen,
+                                          typename H::Out* __restrict__ out,
+                                          uint8_t* hlds = nullptr) {
+  H h;
+  h.setup(hlds);                     // before any early exit (may barrier)
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const uint64_t c = (!kImplicit && order) ? (uint64_t)order[i] : i;
@@ -442,35 +413,9 @@ __device__ __forceinline__ void desc_body(const uint8_t* __restrict__ base,
     else if (wmax >= 1024u) __builtin_amdgcn_s_setprio(2);   // >= 64 KiB
     else if (wmax >= 256u) __builtin_amdgcn_s_setprio(1);    // >= 16 KiB
   }
-  State st = initial_state();
-  if (((uintptr_t)chunk & 15u) == 0) {
-    const uint4* p = reinterpret_cast<const uint4*>(chunk);
-    if (nfull) {
-      const uint32_t lastb = nfull - 1;
-      uint4 R[D][4];
-#pragma unroll
-      for (int j = 0; j < D; ++j) load_block(R[j], p + 4 * min((uint32_t)j, lastb));
-      uint32_t blk = 0;
-      for (; blk + D <= nfull; blk += D) {
-#pragma unroll
-        for (int j = 0; j < D; ++j) {
-          compress_regs<kLat>(st, R[j]);
-          load_block(R[j], p + 4 * min(blk + j + D, lastb));
-        }
-      }
-#pragma unroll
-      for (int j = 0; j < D - 1; ++j)
-        if (blk + j < nfull) compress_regs<kLat>(st, R[j]);
-    }
-  } else {
-    for (uint32_t blk = 0; blk < nfull; ++blk) {
-      uint4 w[4];
-      load_block_unaligned(w, chunk + ((uint64_t)blk << 6));
-      compress_regs<kLat>(st, w);
-    }
-  }
-  finish_message(st, chunk + ((uint64_t)nfull << 6), len & 63u, len);
-  store_digest(out, c, st);
+  typename H::State st = h.init();
+  lane_range<H, D>(h, st, chunk, len);
+  h.store(out, c, st);
 }
 
 template <bool kImplicit, bool kLat = true, bool kPrio = true, int D = 8>
@@ -478,7 +423,53 @@ __global__ void __launch_bounds__(256)
 md5_desc(const uint8_t* __restrict__ base, const uint64_t* __restrict__ offs,
          const uint32_t* __restrict__ lens, const uint32_t* __restrict__ order, uint64_t n,
          uint64_t stride, uint32_t flen, uint4* __restrict__ out) {
-  desc_body<kImplicit, kLat, kPrio, D>(base, offs, lens, order, n, stride, flen, out);
+  desc_body<kImplicit, Md5Hasher<kLat>, kPrio, D>(base, offs, lens, order, n, stride, flen, out);
+}
+
+// ---------------------------------------------------------------------------
+// CRC-32 batches (netcache blk_make_crc, blk_io.c:354-430), same loaders.
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256)
+crc32_fixed_xpose(const uint8_t* __restrict__ base, uint64_t n, uint32_t len, uint64_t stride,
+                  uint32_t* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) uint8_t img[4 * 8192];
+  __shared__ __attribute__((aligned(16))) uint8_t tabs[Crc32Hasher::kLdsBytes];
+  fixed_xpose_body<1, Crc32Hasher, 2>(base, n, len, stride, out, img, tabs);
+}
+
+// fastcrc (blk_io.c:408-424): len <= f -> crc(all), else crc(first f bytes)
+// ^ crc(last f bytes).  kImplicit: chunk i at base + i*stride, length flen.
+template <bool kImplicit>
+__global__ void __launch_bounds__(256)
+crc32_fast(const uint8_t* __restrict__ base, const uint64_t* __restrict__ offs,
+           const uint32_t* __restrict__ lens, uint64_t n, uint64_t stride, uint32_t flen,
+           uint32_t fast, uint32_t* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) uint8_t tabs[Crc32Hasher::kLdsBytes];
+  Crc32Hasher h;
+  h.setup(tabs);
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint8_t* chunk = base + (kImplicit ? i * stride : offs[i]);
+  const uint32_t len = kImplicit ? flen : lens[i];
+  Crc32State a = h.init();
+  if (len <= fast) {
+    lane_range<Crc32Hasher, 2>(h, a, chunk, len);
+  } else {
+    lane_range<Crc32Hasher, 2>(h, a, chunk, fast);
+    Crc32State b = h.init();
+    lane_range<Crc32Hasher, 2>(h, b, chunk + (len - fast), fast);
+    a.c ^= b.c;
+  }
+  out[i] = a.c;
+}
+
+template <bool kImplicit>
+__global__ void __launch_bounds__(256)
+crc32_desc(const uint8_t* __restrict__ base, const uint64_t* __restrict__ offs,
+           const uint32_t* __restrict__ lens, const uint32_t* __restrict__ order, uint64_t n,
+           uint64_t stride, uint32_t flen, uint32_t* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) uint8_t tabs[Crc32Hasher::kLdsBytes];
+  desc_body<kImplicit, Crc32Hasher, true, 4>(base, offs, lens, order, n, stride, flen, out, tabs);
 }
 
 // ---------------------------------------------------------------------------

@@ -5,12 +5,22 @@
 namespace md5hip {
 // Explicit instantiations: kernels referenced only from host templates are
 // otherwise not emitted by hipcc (host stub and device code both missing).
-template __global__ void md5_fixed_direct<2, 0>(const uint8_t*, uint64_t, uint32_t, uint64_t, uint4*);
-template __global__ void md5_fixed_direct<4, 0>(const uint8_t*, uint64_t, uint32_t, uint64_t, uint4*);
+template __global__ void md5_fixed_direct<2, Md5Hasher<false>>(const uint8_t*, uint64_t, uint32_t, uint64_t, uint4*);
+template __global__ void md5_fixed_direct<4, Md5Hasher<false>>(const uint8_t*, uint64_t, uint32_t, uint64_t, uint4*);
 template __global__ void md5_desc<false>(const uint8_t*, const uint64_t*, const uint32_t*,
                                          const uint32_t*, uint64_t, uint64_t, uint32_t, uint4*);
 template __global__ void md5_desc<true>(const uint8_t*, const uint64_t*, const uint32_t*,
                                         const uint32_t*, uint64_t, uint64_t, uint32_t, uint4*);
+template __global__ void crc32_desc<false>(const uint8_t*, const uint64_t*, const uint32_t*,
+                                           const uint32_t*, uint64_t, uint64_t, uint32_t,
+                                           uint32_t*);
+template __global__ void crc32_desc<true>(const uint8_t*, const uint64_t*, const uint32_t*,
+                                          const uint32_t*, uint64_t, uint64_t, uint32_t,
+                                          uint32_t*);
+template __global__ void crc32_fast<false>(const uint8_t*, const uint64_t*, const uint32_t*,
+                                           uint64_t, uint64_t, uint32_t, uint32_t, uint32_t*);
+template __global__ void crc32_fast<true>(const uint8_t*, const uint64_t*, const uint32_t*,
+                                          uint64_t, uint64_t, uint32_t, uint32_t, uint32_t*);
 
 }  // namespace md5hip
 
@@ -133,11 +143,11 @@ int md5hip_digest_fixed_variant(const void* d_base, uint64_t n, uint32_t len, ui
   if (variant == MD5HIP_AUTO) variant = default_variant();
   switch (variant) {
     case MD5HIP_DIRECT2:
-      hipLaunchKernelGGL((md5_fixed_direct<2, 0>), dim3((uint32_t)grid), dim3(kBlock), 0, s, base, n,
+      hipLaunchKernelGGL((md5_fixed_direct<2, Md5Hasher<false>>), dim3((uint32_t)grid), dim3(kBlock), 0, s, base, n,
                          len, stride, out);
       return launched();
     case MD5HIP_DIRECT4:
-      hipLaunchKernelGGL((md5_fixed_direct<4, 0>), dim3((uint32_t)grid), dim3(kBlock), 0, s, base, n,
+      hipLaunchKernelGGL((md5_fixed_direct<4, Md5Hasher<false>>), dim3((uint32_t)grid), dim3(kBlock), 0, s, base, n,
                          len, stride, out);
       return launched();
     case MD5HIP_LDS64:
@@ -154,7 +164,7 @@ int md5hip_digest_fixed_variant(const void* d_base, uint64_t n, uint32_t len, ui
       K k = variant == MD5HIP_XPOSE1 ? md5_fixed_xpose1
           : variant == MD5HIP_XPOSE2 ? md5_fixed_xpose2
           : variant == MD5HIP_XPOSE1NT ? md5_fixed_xpose1nt : md5_fixed_xpose2nt;
-      if (stride >= (1ull << 31) / 64) k = md5_fixed_direct<2, 0>;  // 32-bit buffer offsets
+      if (stride >= (1ull << 31) / 64) k = md5_fixed_direct<2, Md5Hasher<false>>;  // 32-bit buffer offsets
       hipLaunchKernelGGL(k, dim3((uint32_t)grid), dim3(kBlock), 0, s, base, n, len, stride, out);
       return launched();
     }
@@ -165,6 +175,59 @@ int md5hip_digest_fixed_variant(const void* d_base, uint64_t n, uint32_t len, ui
 int md5hip_digest_fixed(const void* d_base, uint64_t n, uint32_t len, uint64_t stride,
                         unsigned char* d_digests, void* stream) {
   return md5hip_digest_fixed_variant(d_base, n, len, stride, d_digests, stream, MD5HIP_AUTO);
+}
+
+int crc32hip_fixed(const void* d_base, uint64_t n, uint32_t len, uint64_t stride,
+                   uint32_t fastcrc, uint32_t* d_crcs, void* stream) {
+  if (n == 0) return 0;
+  if (!d_base || !d_crcs || len > stride || (fastcrc & 3u)) return -EINVAL;
+  if (((uintptr_t)d_crcs & 3u) != 0) return -EINVAL;
+  if (int e = device_ok()) return e;
+  hipStream_t s = (hipStream_t)stream;
+  const uint8_t* base = (const uint8_t*)d_base;
+  if (fastcrc && len > fastcrc) {
+    const uint64_t g = (n + kDescBlock - 1) / kDescBlock;
+    if (g > 0x7fffffffull) return -EINVAL;
+    hipLaunchKernelGGL(crc32_fast<true>, dim3((uint32_t)g), dim3(kDescBlock), 0, s, base,
+                       (const uint64_t*)nullptr, (const uint32_t*)nullptr, n, stride, len,
+                       fastcrc, d_crcs);
+    return launched();
+  }
+  if (((uintptr_t)base & 15u) == 0 && (stride & 15u) == 0 && stride < (1ull << 31) / 64) {
+    const uint64_t g = (n + kBlock - 1) / kBlock;
+    if (g > 0x7fffffffull) return -EINVAL;
+    hipLaunchKernelGGL(crc32_fixed_xpose, dim3((uint32_t)g), dim3(kBlock), 0, s, base, n, len,
+                       stride, d_crcs);
+    return launched();
+  }
+  const uint64_t g = (n + kDescBlock - 1) / kDescBlock;
+  if (g > 0x7fffffffull) return -EINVAL;
+  hipLaunchKernelGGL(crc32_desc<true>, dim3((uint32_t)g), dim3(kDescBlock), 0, s, base,
+                     (const uint64_t*)nullptr, (const uint32_t*)nullptr,
+                     (const uint32_t*)nullptr, n, stride, len, d_crcs);
+  return launched();
+}
+
+int crc32hip_desc(const void* d_base, const uint64_t* d_offsets, const uint32_t* d_lens,
+                  const uint32_t* d_order, uint64_t n, uint32_t fastcrc, uint32_t* d_crcs,
+                  void* stream) {
+  if (n == 0) return 0;
+  if (!d_base || !d_offsets || !d_lens || !d_crcs || (fastcrc & 3u)) return -EINVAL;
+  if (((uintptr_t)d_crcs & 3u) != 0) return -EINVAL;
+  if (int e = device_ok()) return e;
+  hipStream_t s = (hipStream_t)stream;
+  const uint64_t g = (n + kDescBlock - 1) / kDescBlock;
+  if (g > 0x7fffffffull) return -EINVAL;
+  if (fastcrc) {
+    hipLaunchKernelGGL(crc32_fast<false>, dim3((uint32_t)g), dim3(kDescBlock), 0, s,
+                       (const uint8_t*)d_base, d_offsets, d_lens, n, (uint64_t)0, 0u, fastcrc,
+                       d_crcs);
+  } else {
+    hipLaunchKernelGGL(crc32_desc<false>, dim3((uint32_t)g), dim3(kDescBlock), 0, s,
+                       (const uint8_t*)d_base, d_offsets, d_lens, d_order, n, (uint64_t)0, 0u,
+                       d_crcs);
+  }
+  return launched();
 }
 
 int md5hip_fill_synthetic(void* d_dst, uint64_t nbytes, uint64_t seed, void* stream) {

@@ -152,6 +152,38 @@ def digest_desc(base, offsets, lens, order=None, out=None, stream=None):
     return out
 
 
+def crc32_fixed(data, n: int = None, length: int = None, stride: int = None, fastcrc: int = 0,
+                out=None, stream=None):
+    """crcs[i] = netcache block CRC-32 of chunk i (blk_make_crc semantics,
+    blk_io.c:354-430; fastcrc > 0 -> head ^ tail).  uint32 [n] on device."""
+    _need_cuda(data, "data")
+    if n is None or length is None:
+        if data.dim() != 2:
+            raise ValueError("pass n and length, or a 2-D [n, length] tensor")
+        n, length = data.shape
+    stride = length if stride is None else stride
+    if n and (n - 1) * stride + length > data.numel():
+        raise ValueError("batch extends past the end of `data`")
+    if out is None:
+        out = torch.empty(n, dtype=torch.int32, device=data.device)
+    check("crc32hip_fixed", lib().crc32hip_fixed(data.data_ptr(), n, length, stride, fastcrc,
+                                                 out.data_ptr(), _stream(stream)))
+    return out
+
+
+def crc32_desc(base, offsets, lens, order=None, fastcrc: int = 0, out=None, stream=None):
+    _need_cuda(base, "base")
+    _need_cuda(offsets, "offsets")
+    _need_cuda(lens, "lens")
+    n = offsets.numel()
+    if out is None:
+        out = torch.empty(n, dtype=torch.int32, device=base.device)
+    check("crc32hip_desc", lib().crc32hip_desc(base.data_ptr(), offsets.data_ptr(), lens.data_ptr(),
+                                               order.data_ptr() if order is not None else None, n,
+                                               fastcrc, out.data_ptr(), _stream(stream)))
+    return out
+
+
 def plan_order(lens) -> np.ndarray:
     """Longest-first lane order (md5hip_plan_order), host arrays."""
     L = np.ascontiguousarray(lens, dtype=np.uint32)
@@ -254,5 +286,5 @@ class Batcher:
 
 
 __all__ = ["MD5Context", "MD5Init", "MD5Update", "MD5Final", "MD5_DIGEST_SIZE", "MD5HipError",
-           "md5", "digest_fixed", "digest_desc", "plan_order", "fill_synthetic", "Batcher",
+           "md5", "digest_fixed", "digest_desc", "crc32_fixed", "crc32_desc", "plan_order", "fill_synthetic", "Batcher",
            "variant_name", "resolve_variant", "VARIANTS"]

@@ -108,3 +108,16 @@ def synthetic_bytes(nbytes: int, seed: int) -> np.ndarray:
         z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
         z = z ^ (z >> np.uint64(31))
     return (z & np.uint64(0xFFFFFFFF)).astype("<u4").view(np.uint8)
+
+
+def oracle_crc32_batch(buf: np.ndarray, offs, lens, fastcrc: int = 0) -> np.ndarray:
+    """netcache block CRC-32 per chunk (oracle/crc32_oracle.c)."""
+    L = oracle_lib()
+    L.oracle_crc32_batch.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                     ctypes.c_uint64, ctypes.c_uint32, ctypes.c_void_p]
+    offs = np.ascontiguousarray(offs, dtype=np.uint64)
+    lens = np.ascontiguousarray(lens, dtype=np.uint32)
+    out = np.empty(max(offs.size, 1), dtype=np.uint32)
+    L.oracle_crc32_batch(buf.ctypes.data, offs.ctypes.data, lens.ctypes.data, offs.size, fastcrc,
+                         out.ctypes.data)
+    return out[:offs.size]

@@ -1,0 +1,129 @@
+"""CRC-32 block checksums (netcache crc32.c + blk_make_crc fastcrc mode).
+
+CPU: the oracle (oracle/crc32_oracle.c) pinned to tests/golden/crc32_golden.json,
+which the reference crc32.c built in place produced (cross-checked with zlib).
+GPU (-m gpu): crc32hip_fixed / crc32hip_desc bit-exact against the goldens and
+the oracle, fastcrc head^tail included."""
+import ctypes
+import errno
+import json
+import os
+import struct
+import zlib
+
+import numpy as np
+import pytest
+
+import gen
+from sproxy_amd import _lib
+from sproxy_amd import md5 as m
+
+GOLD = json.load(open(os.path.join(gen.REPO, "tests", "golden", "crc32_golden.json")))
+
+
+def _crc(b: bytes, fast=0) -> int:
+    a = np.frombuffer(b + b"\0", dtype=np.uint8)
+    return int(gen.oracle_crc32_batch(a, [0], [len(b)], fast)[0])
+
+
+def test_oracle_kat_and_edges():
+    for k in GOLD["kat"]:
+        assert "%08x" % _crc(bytes.fromhex(k["hex"])) == k["crc"]
+    big = gen.mul_pattern(1 << 20)
+    for L, c in zip(GOLD["edge"]["lengths"], GOLD["edge"]["crc"]):
+        assert "%08x" % _crc(big[:L]) == c
+        assert "%08x" % zlib.crc32(big[:L]) == c
+
+
+def test_oracle_fastcrc():
+    data = gen.xorshift_bytes(100000, seed=0xC5C5)
+    for (L, f), c in zip(GOLD["fastcrc"]["cases"], GOLD["fastcrc"]["crc"]):
+        assert "%08x" % _crc(data[:L], f) == c, (L, f)
+
+
+def test_oracle_batches():
+    for b in GOLD["batches"]:
+        n, L = b["n"], b["len"]
+        buf = gen.xorshift_array(n * L)
+        crcs = gen.oracle_crc32_batch(buf, np.arange(n, dtype=np.uint64) * L, [L] * n)
+        assert "%08x" % gen.fold(b"".join(struct.pack("<I", int(c)) for c in crcs)) == b["fold"]
+        if "crc" in b:
+            assert ["%08x" % c for c in crcs] == b["crc"]
+
+
+def test_crc_abi_errors():
+    L = _lib.lib()
+    E = -errno.EINVAL
+    assert L.crc32hip_fixed(None, 0, 16, 16, 0, None, None) == 0
+    assert L.crc32hip_fixed(None, 4, 16, 16, 0, None, None) == E
+    assert L.crc32hip_fixed(ctypes.c_void_p(16), 4, 16, 16, 6, ctypes.c_void_p(16), None) == E
+    assert L.crc32hip_desc(None, None, None, None, 2, 0, None, None) == E
+
+
+# ----------------------------------------------------------------- GPU parity
+def _dev(a, cuda):
+    import torch
+    return torch.from_numpy(np.ascontiguousarray(a)).to(cuda)
+
+
+@pytest.mark.gpu
+def test_gpu_crc_batches(cuda):
+    for b in GOLD["batches"]:
+        n, L = b["n"], b["len"]
+        host = gen.xorshift_array(n * L)
+        got = m.crc32_fixed(_dev(host, cuda), n, L).cpu().numpy().view(np.uint32)
+        assert "%08x" % gen.fold(b"".join(struct.pack("<I", int(c)) for c in got)) == b["fold"], (n, L)
+        if "crc" in b:
+            assert ["%08x" % c for c in got] == b["crc"]
+
+
+@pytest.mark.gpu
+def test_gpu_crc_edges_fixed_and_unaligned(cuda):
+    big = np.frombuffer(gen.mul_pattern(1 << 20), dtype=np.uint8)
+    for L, want in zip(GOLD["edge"]["lengths"], GOLD["edge"]["crc"]):
+        if L > (1 << 17):
+            continue
+        for stride in ((L + 15) // 16 * 16 or 16, L + 3):
+            n = 70
+            host = np.zeros(n * stride + 16, dtype=np.uint8)
+            for i in range(n):
+                host[i * stride:i * stride + L] = big[:L]
+            got = m.crc32_fixed(_dev(host, cuda), n, L, stride).cpu().numpy().view(np.uint32)
+            assert all("%08x" % c == want for c in got), (L, stride)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fast", [0, 4, 128, 4096])
+def test_gpu_crc_desc_fastcrc(cuda, fast):
+    import torch
+    lens = gen.mixed_lengths(300, seed=31, max_len=1 << 17) + [0, 1, 4, 127, 128, 129, 4095, 4097]
+    offs, total = gen.pack_offsets(lens, align=4)
+    buf = gen.xorshift_array(total + 64, seed=88)
+    want = gen.oracle_crc32_batch(buf, offs, lens, fast)
+    got = m.crc32_desc(_dev(buf, cuda), torch.tensor(offs, dtype=torch.int64, device=cuda),
+                       torch.tensor(lens, dtype=torch.int32, device=cuda),
+                       fastcrc=fast).cpu().numpy().view(np.uint32)
+    assert np.array_equal(got, want)
+    # the fixed entry with fastcrc (every chunk longer than fastcrc)
+    if fast:
+        n, L = 100, 16384
+        host = gen.xorshift_array(n * L, seed=89)
+        got = m.crc32_fixed(_dev(host, cuda), n, L, fastcrc=fast).cpu().numpy().view(np.uint32)
+        want = gen.oracle_crc32_batch(host, np.arange(n, dtype=np.uint64) * L, [L] * n, fast)
+        assert np.array_equal(got, want)
+
+
+@pytest.mark.gpu
+def test_gpu_crc_full_size(cuda):
+    import torch
+    n, L = 1 << 20, 16384
+    d = torch.empty(n * L, dtype=torch.uint8, device=cuda)
+    m.fill_synthetic(d, seed=0xCC)
+    got = m.crc32_fixed(d, n, L)
+    idx = np.unique(np.concatenate([[0, n - 1], np.random.default_rng(3).integers(0, n, 4096)]))
+    rows = d.view(n, L)[torch.from_numpy(idx).to(cuda)].cpu().numpy()
+    want = gen.oracle_crc32_batch(rows.reshape(-1), np.arange(idx.size, dtype=np.uint64) * L,
+                                  [L] * idx.size)
+    assert np.array_equal(got[torch.from_numpy(idx).to(cuda)].cpu().numpy().view(np.uint32), want)
+    del d
+    torch.cuda.empty_cache()
