@@ -82,7 +82,7 @@ def lib():
 
 
 # Every symbol include/*.h declares (checked by tests/test_abi.py).
-EXPORTS = ["MD5Init", "MD5Update", "MD5Final", "md5hip_abi_version", "md5hip_variant_name",
+EXPORTS = ["MD5Init", "MD5Update", "MD5Final", "nc_MD5Init", "nc_MD5Update", "nc_MD5Final", "md5hip_abi_version", "md5hip_variant_name",
            "md5hip_resolve_variant",
            "md5hip_digest_fixed", "md5hip_digest_fixed_variant", "md5hip_digest_desc",
            "md5hip_plan_order", "md5hip_fill_synthetic", "md5hip_batcher_create",
