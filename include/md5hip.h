@@ -113,9 +113,15 @@ int md5hip_fill_synthetic(void *d_dst, uint64_t nbytes, uint64_t seed, void *str
  */
 typedef struct md5hip_batcher md5hip_batcher;
 
+/* What a batcher computes per chunk (default MD5, 16 bytes).  CRC32 gives
+ * netcache's own 4-byte block checksum, with the fastcrc head^tail window
+ * (0 = whole block), i.e. exactly what blk_make_crc returns. */
+enum md5hip_digest_kind { MD5HIP_DIGEST_MD5 = 0, MD5HIP_DIGEST_CRC32 = 1 };
+
 int md5hip_batcher_create(int device, uint64_t slice_bytes, uint32_t nslots,
                           md5hip_batcher **out);
 void md5hip_batcher_destroy(md5hip_batcher *b);
+int md5hip_batcher_set_digest(md5hip_batcher *b, int kind, uint32_t fastcrc);
 
 /* digests[i] = MD5(ptrs[i], lens[i]); any host memory.  -E2BIG if one chunk
  * exceeds slice_bytes. */
@@ -135,6 +141,15 @@ struct md5hip_iov {
  * into the pinned staging slice; -E2BIG if one chunk exceeds slice_bytes. */
 int md5_batch_submit_iov(md5hip_batcher *b, const struct md5hip_iov *segs,
                          const uint64_t *seg_first, uint64_t n, unsigned char *digests);
+
+/* Batched verify (cache read / write verify sites, blk_io.c:665-704,
+ * bc_mgr.c:1464-1492): ok[i] = (digest of chunk i == expected[i]), expected
+ * holding 16 (MD5) or 4 (CRC32) bytes per chunk.  Returns the number of
+ * mismatches (>= 0) or -errno; the caller keeps its per-block EAGAIN /
+ * inode-reset policy (blk_io.c:693-703). */
+int md5hip_batch_verify_iov(md5hip_batcher *b, const struct md5hip_iov *segs,
+                            const uint64_t *seg_first, uint64_t n, const void *expected,
+                            unsigned char *ok);
 
 /* digests[i] = MD5(h_base + i*stride, len) from one contiguous host buffer
  * (pinned for full PCIe rate), copied slice by slice with no host gather. */

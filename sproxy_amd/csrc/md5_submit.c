@@ -31,11 +31,15 @@ struct slot {
     unsigned char *h_dig, *d_dig;     /* 16 * maxn */
     unsigned char *user_dig;          /* where this slot's digests go (NULL = idle) */
     uint64_t ndig;
+    uint32_t dsz;
     int busy;
 };
 
 struct md5hip_batcher {
     int device;
+    int kind;          /* MD5HIP_DIGEST_MD5 or MD5HIP_DIGEST_CRC32 */
+    uint32_t fastcrc;  /* CRC-32 head^tail window (blk_io.c:408-424), 0 = whole block */
+    uint32_t dsz;      /* digest bytes per chunk: 16 or 4 */
     uint32_t nslots;
     uint64_t cap;      /* staging bytes per slot */
     uint64_t maxn;     /* chunks per slot */
@@ -48,7 +52,7 @@ static int slot_retire(struct slot *sl)
 {
     if (!sl->busy) return 0;
     if (hipEventSynchronize(sl->done) != hipSuccess) return -EIO;
-    if (sl->user_dig) memcpy(sl->user_dig, sl->h_dig, 16 * sl->ndig);
+    if (sl->user_dig) memcpy(sl->user_dig, sl->h_dig, (size_t)sl->dsz * sl->ndig);
     sl->busy = 0;
     sl->user_dig = NULL;
     return 0;
@@ -85,6 +89,8 @@ int md5hip_batcher_create(int device, uint64_t slice_bytes, uint32_t nslots, md5
     md5hip_batcher *b = calloc(1, sizeof *b);
     if (!b) return -ENOMEM;
     b->device = device;
+    b->kind = MD5HIP_DIGEST_MD5;
+    b->dsz = 16;
     b->nslots = nslots;
     b->cap = slice_bytes;
     b->maxn = slice_bytes / 64 < 4096 ? 4096 : slice_bytes / 64;
@@ -112,8 +118,32 @@ fail:
     return rc;
 }
 
+int md5hip_batcher_set_digest(md5hip_batcher *b, int kind, uint32_t fastcrc)
+{
+    if (!b) return -EINVAL;
+    if (kind == MD5HIP_DIGEST_MD5) {
+        if (fastcrc) return -EINVAL;
+        b->dsz = 16;
+    } else if (kind == MD5HIP_DIGEST_CRC32) {
+        if (fastcrc & 3u) return -EINVAL;       /* cfs_apix.c:2222-2236 */
+        b->dsz = 4;
+    } else {
+        return -EINVAL;
+    }
+    for (uint32_t k = 0; k < b->nslots; k++) {  /* never change kind under in-flight work */
+        int rc = 0;
+        struct slot *sl = &b->s[k];
+        if (sl->busy && hipEventSynchronize(sl->done) != hipSuccess) rc = -EIO;
+        if (rc) return rc;
+    }
+    b->kind = kind;
+    b->fastcrc = fastcrc;
+    return 0;
+}
+
 /* Enqueue slot `sl` holding `n` chunks, `bytes` staged bytes. */
-static int slot_launch(struct slot *sl, uint64_t n, uint64_t bytes, unsigned char *user_dig)
+static int slot_launch(const md5hip_batcher *b, struct slot *sl, uint64_t n, uint64_t bytes,
+                       unsigned char *user_dig)
 {
     int rc;
     if (md5hip_plan_order(sl->h_len, n, sl->h_ord) != 0) return -EINVAL;
@@ -122,14 +152,20 @@ static int slot_launch(struct slot *sl, uint64_t n, uint64_t bytes, unsigned cha
         hipMemcpyAsync(sl->d_len, sl->h_len, 4 * n, hipMemcpyHostToDevice, sl->stream) ||
         hipMemcpyAsync(sl->d_ord, sl->h_ord, 4 * n, hipMemcpyHostToDevice, sl->stream))
         return -EIO;
-    rc = md5hip_digest_desc(sl->d_data, sl->d_off, sl->d_len, sl->d_ord, n, sl->d_dig, sl->stream);
+    if (b->kind == MD5HIP_DIGEST_CRC32)
+        rc = crc32hip_desc(sl->d_data, sl->d_off, sl->d_len, sl->d_ord, n, b->fastcrc,
+                           (uint32_t *)sl->d_dig, sl->stream);
+    else
+        rc = md5hip_digest_desc(sl->d_data, sl->d_off, sl->d_len, sl->d_ord, n, sl->d_dig,
+                                sl->stream);
     if (rc) return rc;
-    if (hipMemcpyAsync(sl->h_dig, sl->d_dig, 16 * n, hipMemcpyDeviceToHost, sl->stream) ||
+    if (hipMemcpyAsync(sl->h_dig, sl->d_dig, (size_t)b->dsz * n, hipMemcpyDeviceToHost, sl->stream) ||
         hipEventRecord(sl->done, sl->stream))
         return -EIO;
     sl->busy = 1;
     sl->user_dig = user_dig;
     sl->ndig = n;
+    sl->dsz = b->dsz;
     return 0;
 }
 
@@ -189,7 +225,8 @@ static int submit_gather(md5hip_batcher *b, const struct chunk_src *src, uint64_
             m++;
             i++;
         }
-        if ((rc = slot_launch(sl, m, used ? used : 16, digests + 16 * first))) return rc;
+        if ((rc = slot_launch(b, sl, m, used ? used : 16, digests + (size_t)b->dsz * first)))
+            return rc;
         k = (k + 1) % b->nslots;
     }
     for (uint32_t j = 0; j < b->nslots; j++)
@@ -245,16 +282,48 @@ int md5hip_batch_host_fixed(md5hip_batcher *b, const void *h_base, uint64_t n, u
         /* straight from the caller's (ideally pinned) buffer: no host gather */
         if (hipMemcpyAsync(sl->d_data, src + i * stride, bytes, hipMemcpyHostToDevice, sl->stream))
             return -EIO;
-        if ((rc = md5hip_digest_fixed(sl->d_data, m, len, stride, sl->d_dig, sl->stream))) return rc;
-        if (hipMemcpyAsync(sl->h_dig, sl->d_dig, 16 * m, hipMemcpyDeviceToHost, sl->stream) ||
+        if (b->kind == MD5HIP_DIGEST_CRC32)
+            rc = crc32hip_fixed(sl->d_data, m, len, stride, b->fastcrc, (uint32_t *)sl->d_dig,
+                                sl->stream);
+        else
+            rc = md5hip_digest_fixed(sl->d_data, m, len, stride, sl->d_dig, sl->stream);
+        if (rc) return rc;
+        if (hipMemcpyAsync(sl->h_dig, sl->d_dig, (size_t)b->dsz * m, hipMemcpyDeviceToHost, sl->stream) ||
             hipEventRecord(sl->done, sl->stream))
             return -EIO;
         sl->busy = 1;
-        sl->user_dig = digests + 16 * i;
+        sl->user_dig = digests + (size_t)b->dsz * i;
         sl->ndig = m;
+        sl->dsz = b->dsz;
         k = (k + 1) % b->nslots;
     }
     for (uint32_t j = 0; j < b->nslots; j++)
         if ((rc = slot_retire(&b->s[j]))) return rc;
     return 0;
+}
+
+/* Batched verify for the cache-read / write-verify sites (blk_io.c:665-704,
+ * bc_mgr.c:1464-1492): ok[i] = digest(chunk i) == expected[i]; returns the
+ * number of mismatching chunks (>= 0) or -errno.  A mismatch is what
+ * dm_verify_block_crc (diskcache.c:3245-3265) reports per block; the caller
+ * applies its own EAGAIN / inode-reset policy per flagged block. */
+int md5hip_batch_verify_iov(md5hip_batcher *b, const struct md5hip_iov *segs,
+                            const uint64_t *seg_first, uint64_t n, const void *expected,
+                            unsigned char *ok)
+{
+    if (!b) return -EINVAL;
+    if (n == 0) return 0;
+    if (!expected || !ok) return -EINVAL;
+    unsigned char *got = malloc((size_t)b->dsz * n);
+    if (!got) return -ENOMEM;
+    int rc = md5_batch_submit_iov(b, segs, seg_first, n, got);
+    if (rc == 0) {
+        const unsigned char *e = (const unsigned char *)expected;
+        for (uint64_t i = 0; i < n; i++) {
+            ok[i] = memcmp(got + (size_t)b->dsz * i, e + (size_t)b->dsz * i, b->dsz) == 0;
+            rc += !ok[i];
+        }
+    }
+    free(got);
+    return rc;
 }

@@ -215,11 +215,27 @@ def resolve_variant(v=AUTO) -> int:
 class Batcher:
     """Host-memory batched submit (include/md5hip.h md5hip_batcher_*)."""
 
-    def __init__(self, device: int = 0, slice_bytes: int = 64 << 20, nslots: int = 3):
+    MD5, CRC32 = 0, 1
+
+    def __init__(self, device: int = 0, slice_bytes: int = 64 << 20, nslots: int = 3,
+                 kind: int = 0, fastcrc: int = 0):
         h = ctypes.c_void_p()
         check("md5hip_batcher_create", lib().md5hip_batcher_create(device, slice_bytes, nslots,
                                                                     ctypes.byref(h)))
         self._h = h
+        self.set_digest(kind, fastcrc)
+
+    def set_digest(self, kind: int, fastcrc: int = 0):
+        """MD5 (16 B per chunk) or netcache CRC-32 (4 B, optional fastcrc window)."""
+        check("md5hip_batcher_set_digest", lib().md5hip_batcher_set_digest(self._h, kind, fastcrc))
+        self.kind, self.dsz = kind, (16 if kind == self.MD5 else 4)
+
+    def _out(self, n):
+        return np.empty((max(n, 1), self.dsz), dtype=np.uint8)
+
+    def _ret(self, out, n):
+        out = out[:n]
+        return out if self.dsz == 16 else out.view("<u4").reshape(n)
 
     def close(self):
         if self._h:
@@ -248,14 +264,12 @@ class Batcher:
             keep.append(k)
             ptrs[i] = a
             lens[i] = memoryview(b).nbytes
-        out = np.empty((max(n, 1), 16), dtype=np.uint8)
+        out = self._out(n)
         check("md5_batch_submit", lib().md5_batch_submit(self._h, ptrs, lens.ctypes.data, n,
                                                           out.ctypes.data))
-        return out[:n]
+        return self._ret(out, n)
 
-    def submit_iov(self, chunks) -> np.ndarray:
-        """digests[i] = MD5(b"".join(chunks[i])) for a list of segment lists
-        (a netcache block = its list of pages)."""
+    def _iov(self, chunks):
         segs, first, keep = [], [0], []
         for segl in chunks:
             for sgm in segl:
@@ -267,22 +281,43 @@ class Batcher:
         for j, (a, L) in enumerate(segs):
             arr[j].base = a
             arr[j].len = L
-        fa = np.asarray(first, dtype=np.uint64)
+        return arr, np.asarray(first, dtype=np.uint64), keep
+
+    def submit_iov(self, chunks) -> np.ndarray:
+        """digests[i] = digest(b"".join(chunks[i])) for a list of segment lists
+        (a netcache block = its list of pages)."""
+        arr, fa, keep = self._iov(chunks)
         n = len(chunks)
-        out = np.empty((max(n, 1), 16), dtype=np.uint8)
+        out = self._out(n)
         check("md5_batch_submit_iov", lib().md5_batch_submit_iov(self._h, arr, fa.ctypes.data, n,
                                                                   out.ctypes.data))
-        return out[:n]
+        del keep
+        return self._ret(out, n)
+
+    def verify_iov(self, chunks, expected):
+        """(ok[i] bool array, mismatch count): digest(chunks[i]) == expected[i]."""
+        arr, fa, keep = self._iov(chunks)
+        n = len(chunks)
+        exp = np.ascontiguousarray(expected)
+        if exp.nbytes != n * self.dsz:
+            raise ValueError("expected must hold one digest per chunk")
+        ok = np.empty(max(n, 1), dtype=np.uint8)
+        rc = lib().md5hip_batch_verify_iov(self._h, arr, fa.ctypes.data, n, exp.ctypes.data,
+                                            ok.ctypes.data)
+        if rc < 0:
+            check("md5hip_batch_verify_iov", rc)
+        del keep
+        return ok[:n].astype(bool), rc
 
     def host_fixed(self, arr: np.ndarray, n: int, length: int, stride: int = None) -> np.ndarray:
         stride = length if stride is None else stride
         a = np.ascontiguousarray(arr).view(np.uint8).reshape(-1)
         if n and (n - 1) * stride + length > a.size:
             raise ValueError("batch extends past the end of the buffer")
-        out = np.empty((max(n, 1), 16), dtype=np.uint8)
+        out = self._out(n)
         check("md5hip_batch_host_fixed",
               lib().md5hip_batch_host_fixed(self._h, a.ctypes.data, n, length, stride, out.ctypes.data))
-        return out[:n]
+        return self._ret(out, n)
 
 
 __all__ = ["MD5Context", "MD5Init", "MD5Update", "MD5Final", "MD5_DIGEST_SIZE", "MD5HipError",

@@ -198,3 +198,36 @@ def test_batcher_submit_iov_pages(cuda):
     offs = np.cumsum([0] + [len(j) for j in joined[:-1]])
     want = gen.oracle_digests(np.frombuffer(blob + b"\0", dtype=np.uint8), offs, [len(j) for j in joined])
     assert np.array_equal(got, want)
+
+
+def test_batcher_crc32_and_verify(cuda):
+    """The block-checksum call site end to end: a batcher in netcache CRC-32
+    mode (fastcrc window) and the batched verify with a corrupted block."""
+    rng = np.random.default_rng(77)
+    page = 16384
+    blocks, joined = [], []
+    for b in range(30):
+        pages = [gen.xorshift_bytes(page, seed=500 + 10 * b + p) for p in range(int(rng.integers(1, 5)))]
+        pages[-1] = pages[-1][:int(rng.integers(1, page + 1))]
+        blocks.append(pages)
+        joined.append(b"".join(pages))
+    blob = b"".join(joined)
+    offs = np.cumsum([0] + [len(j) for j in joined[:-1]])
+    lens = [len(j) for j in joined]
+    arena = np.frombuffer(blob + b"\0", dtype=np.uint8)
+    for fast in (0, 128):
+        with m.Batcher(device=0, slice_bytes=1 << 20, nslots=2, kind=m.Batcher.CRC32, fastcrc=fast) as bt:
+            got = bt.submit_iov(blocks)
+            assert np.array_equal(got, gen.oracle_crc32_batch(arena, offs, lens, fast))
+            ok, bad = bt.verify_iov(blocks, got)
+            assert bad == 0 and ok.all()
+            exp = got.copy()
+            exp[7] ^= 1
+            ok, bad = bt.verify_iov(blocks, exp)
+            assert bad == 1 and not ok[7] and ok.sum() == len(blocks) - 1
+    with m.Batcher(device=0, slice_bytes=1 << 20, nslots=2) as bt:       # MD5 verify
+        dig = bt.submit_iov(blocks)
+        assert np.array_equal(dig, gen.oracle_digests(arena, offs, lens))
+        dig[3, 0] ^= 0xFF
+        ok, bad = bt.verify_iov(blocks, dig)
+        assert bad == 1 and not ok[3]
