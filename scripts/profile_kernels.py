@@ -56,7 +56,9 @@ def main():
              "load_direct4": diag(2), "load_lds64": diag(3), "load_lds128": diag(4),
              "stream_read": diag(5), "xpose1": prod("xpose1"), "xpose2": prod("xpose2"),
              "xpose1nt": prod("xpose1nt"), "xpose2nt": prod("xpose2nt"), "lds128nt": prod("lds128nt"),
-             "load_xpose1": diag(6), "load_xpose2": diag(7), "crc32": crc()}
+             "load_xpose1": diag(6), "load_xpose2": diag(7), "crc32": crc(),
+             "cp0": diag(20), "cp_sc0": diag(21), "cp_nt": diag(22), "cp_sc0nt": diag(23),
+             "cp_sc1": diag(24), "cp_sc1nt": diag(25), "cp_sc0sc1nt": diag(26)}
     if a.only:
         cases = {k: v for k, v in cases.items() if k in a.only.split(",")}
     times = {k: [] for k in cases}

@@ -9,6 +9,7 @@
 //   kind 6,7  load only for the xpose1 / xpose2 loaders
 //   kind 12   compute only with the latency-form step (md5_core.h kLat)
 //   kind 13,14 single-chain latency: few lanes, long chunks (kLat off / on)
+//   kind 20-26 xpose1 with buffer-load aux 0, 1, 2, 3, 16, 18, 19 (cache policy A/B)
 //   kind 100+K VALU issue-rate probes (instruction K of diag_valu_rate)
 //
 // C ABI: int md5diag_run(int kind, const void *base, uint64_t n, uint32_t len,
@@ -55,6 +56,16 @@ diag_xpose2_load(const uint8_t* __restrict__ base, uint64_t n, uint32_t len, uin
                  uint4* __restrict__ out) {
   __shared__ __attribute__((aligned(16))) uint8_t img[4 * 8192];
   fixed_xpose_body<2, FoldHasher>(base, n, len, stride, out, img);
+}
+
+// Cache-policy A/B for the product loader (xpose1): aux bits of the buffer
+// loads (gfx950 CPol: sc0 = 1, nt = 2, sc1 = 16).
+template <int CP>
+__global__ void __launch_bounds__(256)
+diag_xpose1_cp(const uint8_t* __restrict__ base, uint64_t n, uint32_t len, uint64_t stride,
+               uint4* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) uint8_t img[4 * 8192];
+  fixed_xpose_body<1, Md5Hasher<false>, CP>(base, n, len, stride, out, img);
 }
 
 // Compute only: lane L hashes `nblocks` blocks whose words it re-reads from its
@@ -187,6 +198,13 @@ extern "C" int md5diag_run(int kind, const void* base, uint64_t n, uint32_t len,
     case 12:
       hipLaunchKernelGGL(diag_compute<true>, dim3(grid), dim3(256), 0, s, n, len >> 6, o);
       break;
+    case 20: hipLaunchKernelGGL(diag_xpose1_cp<0>, dim3(grid), dim3(256), 0, s, b, n, len, stride, o); break;
+    case 21: hipLaunchKernelGGL(diag_xpose1_cp<1>, dim3(grid), dim3(256), 0, s, b, n, len, stride, o); break;
+    case 22: hipLaunchKernelGGL(diag_xpose1_cp<2>, dim3(grid), dim3(256), 0, s, b, n, len, stride, o); break;
+    case 23: hipLaunchKernelGGL(diag_xpose1_cp<3>, dim3(grid), dim3(256), 0, s, b, n, len, stride, o); break;
+    case 24: hipLaunchKernelGGL(diag_xpose1_cp<16>, dim3(grid), dim3(256), 0, s, b, n, len, stride, o); break;
+    case 25: hipLaunchKernelGGL(diag_xpose1_cp<18>, dim3(grid), dim3(256), 0, s, b, n, len, stride, o); break;
+    case 26: hipLaunchKernelGGL(diag_xpose1_cp<19>, dim3(grid), dim3(256), 0, s, b, n, len, stride, o); break;
     case 13: case 14: {
       // single-chain latency: n lanes (one wave per CU at n = 16384), each
       // hashing `len` bytes; 64-thread workgroups so every CU gets one wave
