@@ -156,6 +156,38 @@ int md5hip_batch_verify_iov(md5hip_batcher *b, const struct md5hip_iov *segs,
 int md5hip_batch_host_fixed(md5hip_batcher *b, const void *h_base, uint64_t n, uint32_t len,
                             uint64_t stride, unsigned char *digests);
 
+/*
+ * Multi-GPU host pool.  Chunks are independent, so a batch
+ * shards with no collective: the pool owns one batcher per listed device
+ * (a device may be listed twice) and cuts every call into contiguous chunk
+ * ranges, one per device, balanced by bytes; a host thread per device drives
+ * its range and writes the digests straight into its slice of `digests`.
+ * Same results and errors as the batcher entries; calls are synchronous and
+ * serialized by an internal lock, so one pool may be shared by threads.
+ */
+typedef struct md5hip_pool md5hip_pool;
+
+int md5hip_pool_create(const int *devices, uint32_t ndev, uint64_t slice_bytes, uint32_t nslots,
+                       md5hip_pool **out);
+void md5hip_pool_destroy(md5hip_pool *p);
+int md5hip_pool_ndev(const md5hip_pool *p);
+int md5hip_pool_set_digest(md5hip_pool *p, int kind, uint32_t fastcrc);
+int md5hip_pool_submit(md5hip_pool *p, const void *const *ptrs, const uint32_t *lens, uint64_t n,
+                       unsigned char *digests);
+int md5hip_pool_submit_iov(md5hip_pool *p, const struct md5hip_iov *segs,
+                           const uint64_t *seg_first, uint64_t n, unsigned char *digests);
+int md5hip_pool_verify_iov(md5hip_pool *p, const struct md5hip_iov *segs,
+                           const uint64_t *seg_first, uint64_t n, const void *expected,
+                           unsigned char *ok);
+int md5hip_pool_host_fixed(md5hip_pool *p, const void *h_base, uint64_t n, uint32_t len,
+                           uint64_t stride, unsigned char *digests);
+
+/* The pool's split, exposed for callers and tests (host only, synchronous):
+ * first[0..nparts] such that part g is chunks [first[g], first[g+1]).
+ * lens == NULL: equal counts, first[g] = g*n/nparts.  Otherwise contiguous
+ * ranges of near-equal weight, weight(chunk) = len + 64. */
+int md5hip_pool_plan(const uint32_t *lens, uint64_t n, uint32_t nparts, uint64_t *first);
+
 #ifdef __cplusplus
 }
 #endif

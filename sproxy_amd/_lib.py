@@ -74,6 +74,15 @@ def lib():
         "md5hip_batcher_set_digest": (i, [vp, i, u32]),
         "md5hip_batch_verify_iov": (i, [vp, vp, vp, u64, vp, vp]),
         "md5hip_batch_host_fixed": (i, [vp, vp, u64, u32, u64, vp]),
+        "md5hip_pool_create": (i, [vp, u32, u64, u32, ctypes.POINTER(vp)]),
+        "md5hip_pool_destroy": (None, [vp]),
+        "md5hip_pool_ndev": (i, [vp]),
+        "md5hip_pool_set_digest": (i, [vp, i, u32]),
+        "md5hip_pool_submit": (i, [vp, vp, vp, u64, vp]),
+        "md5hip_pool_submit_iov": (i, [vp, vp, vp, u64, vp]),
+        "md5hip_pool_verify_iov": (i, [vp, vp, vp, u64, vp, vp]),
+        "md5hip_pool_host_fixed": (i, [vp, vp, u64, u32, u64, vp]),
+        "md5hip_pool_plan": (i, [vp, u64, u32, vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -91,7 +100,10 @@ EXPORTS = ["MD5Init", "MD5Update", "MD5Final", "nc_MD5Init", "nc_MD5Update", "nc
            "crc32hip_fixed", "crc32hip_desc",
            "md5hip_batcher_destroy", "md5_batch_submit", "md5_batch_submit_iov",
            "md5hip_batcher_set_digest", "md5hip_batch_verify_iov",
-           "md5hip_batch_host_fixed"]
+           "md5hip_batch_host_fixed", "md5hip_pool_create", "md5hip_pool_destroy",
+           "md5hip_pool_ndev", "md5hip_pool_set_digest", "md5hip_pool_submit",
+           "md5hip_pool_submit_iov", "md5hip_pool_verify_iov", "md5hip_pool_host_fixed",
+           "md5hip_pool_plan"]
 
 
 def check(fn, rc):

@@ -216,6 +216,9 @@ class Batcher:
     """Host-memory batched submit (include/md5hip.h md5hip_batcher_*)."""
 
     MD5, CRC32 = 0, 1
+    _fn = dict(set_digest="md5hip_batcher_set_digest", destroy="md5hip_batcher_destroy",
+               submit="md5_batch_submit", submit_iov="md5_batch_submit_iov",
+               verify_iov="md5hip_batch_verify_iov", host_fixed="md5hip_batch_host_fixed")
 
     def __init__(self, device: int = 0, slice_bytes: int = 64 << 20, nslots: int = 3,
                  kind: int = 0, fastcrc: int = 0):
@@ -225,9 +228,13 @@ class Batcher:
         self._h = h
         self.set_digest(kind, fastcrc)
 
+    def _call(self, op, *args):
+        name = self._fn[op]
+        return name, getattr(lib(), name)(self._h, *args)
+
     def set_digest(self, kind: int, fastcrc: int = 0):
         """MD5 (16 B per chunk) or netcache CRC-32 (4 B, optional fastcrc window)."""
-        check("md5hip_batcher_set_digest", lib().md5hip_batcher_set_digest(self._h, kind, fastcrc))
+        check(*self._call("set_digest", kind, fastcrc))
         self.kind, self.dsz = kind, (16 if kind == self.MD5 else 4)
 
     def _out(self, n):
@@ -238,8 +245,8 @@ class Batcher:
         return out if self.dsz == 16 else out.view("<u4").reshape(n)
 
     def close(self):
-        if self._h:
-            lib().md5hip_batcher_destroy(self._h)
+        if getattr(self, "_h", None):
+            getattr(lib(), self._fn["destroy"])(self._h)
             self._h = None
 
     def __enter__(self):
@@ -265,8 +272,7 @@ class Batcher:
             ptrs[i] = a
             lens[i] = memoryview(b).nbytes
         out = self._out(n)
-        check("md5_batch_submit", lib().md5_batch_submit(self._h, ptrs, lens.ctypes.data, n,
-                                                          out.ctypes.data))
+        check(*self._call("submit", ptrs, lens.ctypes.data, n, out.ctypes.data))
         return self._ret(out, n)
 
     def _iov(self, chunks):
@@ -289,8 +295,7 @@ class Batcher:
         arr, fa, keep = self._iov(chunks)
         n = len(chunks)
         out = self._out(n)
-        check("md5_batch_submit_iov", lib().md5_batch_submit_iov(self._h, arr, fa.ctypes.data, n,
-                                                                  out.ctypes.data))
+        check(*self._call("submit_iov", arr, fa.ctypes.data, n, out.ctypes.data))
         del keep
         return self._ret(out, n)
 
@@ -302,10 +307,9 @@ class Batcher:
         if exp.nbytes != n * self.dsz:
             raise ValueError("expected must hold one digest per chunk")
         ok = np.empty(max(n, 1), dtype=np.uint8)
-        rc = lib().md5hip_batch_verify_iov(self._h, arr, fa.ctypes.data, n, exp.ctypes.data,
-                                            ok.ctypes.data)
+        name, rc = self._call("verify_iov", arr, fa.ctypes.data, n, exp.ctypes.data, ok.ctypes.data)
         if rc < 0:
-            check("md5hip_batch_verify_iov", rc)
+            check(name, rc)
         del keep
         return ok[:n].astype(bool), rc
 
@@ -315,11 +319,47 @@ class Batcher:
         if n and (n - 1) * stride + length > a.size:
             raise ValueError("batch extends past the end of the buffer")
         out = self._out(n)
-        check("md5hip_batch_host_fixed",
-              lib().md5hip_batch_host_fixed(self._h, a.ctypes.data, n, length, stride, out.ctypes.data))
+        check(*self._call("host_fixed", a.ctypes.data, n, length, stride, out.ctypes.data))
         return self._ret(out, n)
+
+
+class Pool(Batcher):
+    """Multi-GPU host pool (include/md5hip.h md5hip_pool_*): one batcher and
+    host thread per listed device, contiguous byte-balanced chunk ranges, no
+    collective.  Same methods and results as Batcher."""
+
+    _fn = dict(set_digest="md5hip_pool_set_digest", destroy="md5hip_pool_destroy",
+               submit="md5hip_pool_submit", submit_iov="md5hip_pool_submit_iov",
+               verify_iov="md5hip_pool_verify_iov", host_fixed="md5hip_pool_host_fixed")
+
+    def __init__(self, devices=(0,), slice_bytes: int = 64 << 20, nslots: int = 3,
+                 kind: int = 0, fastcrc: int = 0):
+        devs = (ctypes.c_int * max(len(devices), 1))(*devices)
+        h = ctypes.c_void_p()
+        check("md5hip_pool_create", lib().md5hip_pool_create(devs, len(devices), slice_bytes,
+                                                              nslots, ctypes.byref(h)))
+        self._h = h
+        self.set_digest(kind, fastcrc)
+
+    @property
+    def ndev(self) -> int:
+        return lib().md5hip_pool_ndev(self._h)
+
+
+def pool_plan(lens, nparts: int) -> np.ndarray:
+    """md5hip_pool_plan: first[0..nparts] of the pool's contiguous split
+    (lens None: equal counts over `lens`=n given as an int)."""
+    first = np.empty(nparts + 1, dtype=np.uint64)
+    if isinstance(lens, int):
+        check("md5hip_pool_plan", lib().md5hip_pool_plan(None, lens, nparts, first.ctypes.data))
+    else:
+        L = np.ascontiguousarray(lens, dtype=np.uint32)
+        check("md5hip_pool_plan", lib().md5hip_pool_plan(L.ctypes.data if L.size else None, L.size,
+                                                          nparts, first.ctypes.data))
+    return first
 
 
 __all__ = ["MD5Context", "MD5Init", "MD5Update", "MD5Final", "MD5_DIGEST_SIZE", "MD5HipError",
            "md5", "digest_fixed", "digest_desc", "crc32_fixed", "crc32_desc", "plan_order", "fill_synthetic", "Batcher",
+           "Pool", "pool_plan",
            "variant_name", "resolve_variant", "VARIANTS"]

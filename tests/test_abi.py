@@ -144,3 +144,30 @@ def test_device_api_rejects_host_tensors():
     import torch
     with pytest.raises(ValueError):
         m.digest_fixed(torch.zeros((4, 64), dtype=torch.uint8))
+
+
+def test_pool_plan_partitions_by_bytes():
+    """md5hip_pool_plan (host logic of the multi-GPU pool, §8e): contiguous,
+    covering, equal counts for fixed batches, near-equal weight for mixed."""
+    for n in (0, 1, 7, 1000, 1 << 20):
+        for G in (1, 2, 3, 8):
+            f = m.pool_plan(n, G)
+            assert list(f) == [n * g // G for g in range(G + 1)]
+    rng = np.random.default_rng(5)
+    for trial in range(20):
+        n = int(rng.integers(0, 3000))
+        lens = gen.mixed_lengths(n, seed=trial, max_len=1 << 20) if n else []
+        w = np.asarray(lens, dtype=np.int64) + 64
+        for G in (1, 2, 4, 8):
+            f = m.pool_plan(lens, G).astype(np.int64)
+            assert f[0] == 0 and f[-1] == n and np.all(np.diff(f) >= 0)
+            parts = [w[f[g]:f[g + 1]].sum() for g in range(G)]
+            slack = w.max() if n else 0
+            assert max(parts) <= w.sum() / G + slack
+    # one huge chunk among small ones: it lands alone-ish, nothing is lost
+    f = m.pool_plan([16] * 10 + [1 << 30] + [16] * 10, 4)
+    assert f[0] == 0 and f[-1] == 21
+    L, EINVAL = _lib.lib(), -errno.EINVAL
+    assert L.md5hip_pool_plan(None, 5, 0, (ctypes.c_uint64 * 2)()) == EINVAL
+    h = ctypes.c_void_p()
+    assert L.md5hip_pool_create(None, 0, 0, 0, ctypes.byref(h)) == EINVAL

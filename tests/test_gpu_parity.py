@@ -231,3 +231,35 @@ def test_batcher_crc32_and_verify(cuda):
         dig[3, 0] ^= 0xFF
         ok, bad = bt.verify_iov(blocks, dig)
         assert bad == 1 and not ok[3]
+
+
+@pytest.mark.gpu
+def test_pool_matches_oracle(cuda):
+    """Multi-GPU host pool (§8e) on the one device of the box, listed 1-3
+    times: each entry is a separate batcher driven by its own host thread, so
+    the split, per-thread device binding and digest placement are exercised."""
+    lens = gen.mixed_lengths(700, seed=91, max_len=1 << 18) + [0, 1, 64, 16384]
+    blob = gen.xorshift_bytes(sum(lens) + 1, seed=92)
+    bufs, cur = [], 0
+    for L in lens:
+        bufs.append(blob[cur:cur + L])
+        cur += L
+    arena = np.frombuffer(blob, dtype=np.uint8)
+    offs = np.cumsum([0] + lens[:-1])
+    want = gen.oracle_digests(arena, offs, lens)
+    n, L = 3000, 16384
+    host = gen.xorshift_array(n * L, seed=93)
+    want_fixed = gen.oracle_digests_fixed(host, n, L)
+    pages = [[bufs[i][:7000], bufs[i][7000:]] for i in range(len(bufs))]
+    for devs in ((0,), (0, 0), (0, 0, 0)):
+        with m.Pool(devs, slice_bytes=2 << 20, nslots=2) as p:
+            assert p.ndev == len(devs)
+            assert np.array_equal(p.submit(bufs), want)
+            assert np.array_equal(p.submit_iov(pages), want)
+            assert np.array_equal(p.host_fixed(host, n, L), want_fixed)
+            bad = want.copy()
+            bad[[5, 600]] ^= 1
+            ok, nbad = p.verify_iov(pages, bad)
+            assert nbad == 2 and not ok[5] and not ok[600]
+            p.set_digest(m.Pool.CRC32, 64)
+            assert np.array_equal(p.submit(bufs), gen.oracle_crc32_batch(arena, offs, lens, 64))
