@@ -122,6 +122,7 @@ int md5hip_batcher_create(int device, uint64_t slice_bytes, uint32_t nslots,
                           md5hip_batcher **out);
 void md5hip_batcher_destroy(md5hip_batcher *b);
 int md5hip_batcher_set_digest(md5hip_batcher *b, int kind, uint32_t fastcrc);
+int md5hip_batcher_get_digest(const md5hip_batcher *b, int *kind, uint32_t *fastcrc);
 
 /* digests[i] = MD5(ptrs[i], lens[i]); any host memory.  -E2BIG if one chunk
  * exceeds slice_bytes. */

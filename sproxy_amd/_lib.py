@@ -83,6 +83,17 @@ def lib():
         "md5hip_pool_verify_iov": (i, [vp, vp, vp, u64, vp, vp]),
         "md5hip_pool_host_fixed": (i, [vp, vp, u64, u32, u64, vp]),
         "md5hip_pool_plan": (i, [vp, u64, u32, vp]),
+        "md5hip_batcher_get_digest": (i, [vp, vp, vp]),
+        "nc_canned_digest_size": (u64, [u32, u32]),
+        "nc_digest_update": (i, [vp, u64, u32, u64, u64, vp]),
+        "nc_digest_verify": (i, [vp, u64, u32, u64, vp]),
+        "nc_digest_scatter": (i, [vp, u64, u32, u64, vp, u64, vp]),
+        "nc_digest_compare": (i, [vp, u64, u32, vp, u64, vp, vp]),
+        "nc_crc32": (u32, [vp, u64]),
+        "nc_header_crc": (u32, [vp]),
+        "nc_header_seal": (i, [vp]),
+        "nc_header_verify": (i, [vp]),
+        "md5hip_batch_verify_headers": (i, [vp, vp, u64, vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -103,7 +114,10 @@ EXPORTS = ["MD5Init", "MD5Update", "MD5Final", "nc_MD5Init", "nc_MD5Update", "nc
            "md5hip_batch_host_fixed", "md5hip_pool_create", "md5hip_pool_destroy",
            "md5hip_pool_ndev", "md5hip_pool_set_digest", "md5hip_pool_submit",
            "md5hip_pool_submit_iov", "md5hip_pool_verify_iov", "md5hip_pool_host_fixed",
-           "md5hip_pool_plan"]
+           "md5hip_pool_plan", "md5hip_batcher_get_digest", "nc_canned_digest_size",
+           "nc_digest_update", "nc_digest_verify", "nc_digest_scatter", "nc_digest_compare",
+           "nc_crc32", "nc_header_crc", "nc_header_seal", "nc_header_verify",
+           "md5hip_batch_verify_headers"]
 
 
 def check(fn, rc):

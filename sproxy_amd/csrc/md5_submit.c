@@ -141,6 +141,14 @@ int md5hip_batcher_set_digest(md5hip_batcher *b, int kind, uint32_t fastcrc)
     return 0;
 }
 
+int md5hip_batcher_get_digest(const md5hip_batcher *b, int *kind, uint32_t *fastcrc)
+{
+    if (!b || !kind || !fastcrc) return -EINVAL;
+    *kind = b->kind;
+    *fastcrc = b->fastcrc;
+    return 0;
+}
+
 /* Enqueue slot `sl` holding `n` chunks, `bytes` staged bytes. */
 static int slot_launch(const md5hip_batcher *b, struct slot *sl, uint64_t n, uint64_t bytes,
                        unsigned char *user_dig)

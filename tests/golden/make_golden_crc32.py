@@ -72,6 +72,20 @@ def main():
             e["crc"] = ["%08x" % c for c in crcs]
         batches.append(e)
     out["batches"] = batches
+    # on-disk header CRC (diskcache.c:1391-1393 write, :3660-3690 verify): CRC-32 over
+    # header_size bytes with disk_header_size (4..8), flag (12..16), crc (16..20) as zero
+    hdrs = []
+    for k, hs in enumerate([20, 21, 27, 100, 1000, 4096, 70001]):
+        body = gen.xorshift_bytes(hs, seed=0x4EAD + k)
+        dhs, flag = (hs // 3, 0x10000000) if k % 2 else (0, 0)
+        zeroed = struct.pack("<IiiII", 0x30334253, 0, hs, 0, 0) + body[20:]
+        crc = ref([(zeroed, 0)])[0][0]
+        assert crc == zlib.crc32(zeroed)
+        hdrs.append({"header_size": hs, "body_seed": 0x4EAD + k, "disk_header_size": dhs,
+                     "flag": flag, "crc": "%08x" % crc})
+    out["headers"] = {"magic": "%08x" % 0x30334253, "cases": hdrs,
+                      "layout": "<I magic, i disk_header_size, i header_size, I flag, I crc, then "
+                                "xorshift_bytes(header_size, body_seed)[20:]"}
     path = os.path.join(HERE, "crc32_golden.json")
     with open(path, "w") as f:
         json.dump(out, f, indent=0)

@@ -20,7 +20,7 @@ INC = os.path.join(gen.REPO, "include")
 
 def declared_functions():
     names = set()
-    for h in ("md5.h", "md5hip.h", "nc_md5.h"):
+    for h in ("md5.h", "md5hip.h", "nc_md5.h", "nc_digest.h"):
         text = open(os.path.join(INC, h)).read()
         text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
         for mm in re.finditer(r"^\s*(?:const\s+)?[\w\s\*]+?\b(\w+)\s*\(", text, flags=re.M):
