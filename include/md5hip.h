@@ -87,6 +87,16 @@ int md5hip_digest_desc(const void *d_base, const uint64_t *d_offsets, const uint
  */
 int crc32hip_fixed(const void *d_base, uint64_t n, uint32_t len, uint64_t stride,
                    uint32_t fastcrc, uint32_t *d_crcs, void *stream);
+/* CRC-32 kernel variants for crc32hip_fixed_variant (A-B benches). */
+enum crc32hip_variant {
+    CRC32HIP_AUTO = 0,      /* library's choice (env CRC32HIP_VARIANT overrides) */
+    CRC32HIP_SHARED8 = 1,   /* slicing-by-8, one shared 8 KiB LDS table set, xpose loads */
+    CRC32HIP_LANE32 = 2,    /* slicing-by-4, 32 lane-private table copies (128 KiB LDS) */
+    CRC32HIP_LANE16 = 3,    /* slicing-by-4, 16 table copies (64 KiB LDS) */
+    CRC32HIP_NUM_VARIANTS = 4
+};
+int crc32hip_fixed_variant(const void *d_base, uint64_t n, uint32_t len, uint64_t stride,
+                           uint32_t fastcrc, uint32_t *d_crcs, void *stream, int variant);
 int crc32hip_desc(const void *d_base, const uint64_t *d_offsets, const uint32_t *d_lens,
                   const uint32_t *d_order, uint64_t n, uint32_t fastcrc, uint32_t *d_crcs,
                   void *stream);

@@ -42,8 +42,8 @@ def main():
 
     crc_out = torch.empty(n, dtype=torch.int32, device="cuda")
 
-    def crc():
-        return lambda: m.crc32_fixed(data, n, L, out=crc_out)
+    def crc(v="auto"):
+        return lambda: m.crc32_fixed(data, n, L, out=crc_out, variant=v)
 
     def diag(kind):
         def f():
@@ -57,6 +57,7 @@ def main():
              "stream_read": diag(5), "xpose1": prod("xpose1"), "xpose2": prod("xpose2"),
              "xpose1nt": prod("xpose1nt"), "xpose2nt": prod("xpose2nt"), "lds128nt": prod("lds128nt"),
              "load_xpose1": diag(6), "load_xpose2": diag(7), "crc32": crc(),
+             "crc_shared8": crc("shared8"), "crc_lane32": crc("lane32"), "crc_lane16": crc("lane16"),
              "cp0": diag(20), "cp_sc0": diag(21), "cp_nt": diag(22), "cp_sc0nt": diag(23),
              "cp_sc1": diag(24), "cp_sc1nt": diag(25), "cp_sc0sc1nt": diag(26)}
     if a.only:

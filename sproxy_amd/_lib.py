@@ -66,6 +66,7 @@ def lib():
         "md5hip_plan_order": (i, [vp, u64, vp]),
         "crc32hip_fixed": (i, [vp, u64, u32, u64, u32, vp, vp]),
         "crc32hip_desc": (i, [vp, vp, vp, vp, u64, u32, vp, vp]),
+        "crc32hip_fixed_variant": (i, [vp, u64, u32, u64, u32, vp, vp, i]),
         "md5hip_fill_synthetic": (i, [vp, u64, u64, vp]),
         "md5hip_batcher_create": (i, [i, u64, u32, ctypes.POINTER(vp)]),
         "md5hip_batcher_destroy": (None, [vp]),
@@ -108,7 +109,7 @@ EXPORTS = ["MD5Init", "MD5Update", "MD5Final", "nc_MD5Init", "nc_MD5Update", "nc
            "md5hip_resolve_variant",
            "md5hip_digest_fixed", "md5hip_digest_fixed_variant", "md5hip_digest_desc",
            "md5hip_plan_order", "md5hip_fill_synthetic", "md5hip_batcher_create",
-           "crc32hip_fixed", "crc32hip_desc",
+           "crc32hip_fixed", "crc32hip_desc", "crc32hip_fixed_variant",
            "md5hip_batcher_destroy", "md5_batch_submit", "md5_batch_submit_iov",
            "md5hip_batcher_set_digest", "md5hip_batch_verify_iov",
            "md5hip_batch_host_fixed", "md5hip_pool_create", "md5hip_pool_destroy",

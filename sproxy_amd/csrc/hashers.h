@@ -186,4 +186,80 @@ struct Crc32Hasher {
   }
 };
 
+// ---------------------------------------------------------------------------
+// CRC-32, slicing-by-4 over LANE-PRIVATE table copies.  Every table entry is
+// stored K times, copy c in bank c (LDS word e*K + c), and lane l reads copy
+// l % K, so a ds_read_b32 lane group (32 lanes, bank = dword mod 32,
+// MI355X_MICROARCH §LDS) hits at most 32/K lanes per bank whatever bytes
+// the lanes look up: conflict-free for K = 32 (2 LDS cycles per wave
+// lookup), where the shared 8 KiB tables of Crc32Hasher average ~3.5-way.
+// Same polynomial and byte order as crc32.c:186-240 (4 bytes per step).
+// LDS: 4 tables x 256 entries x K copies x 4 B = K KiB * 4 (128 KiB at K=32).
+// Address bits (K=32): lane copy 2..6, entry 7..14, table 15..16 -- disjoint,
+// so an address is one OR/shift; table 1/3 come from the ds_read offset.
+// ---------------------------------------------------------------------------
+template <int K>
+struct Crc32LaneHasher {
+  static_assert(K == 16 || K == 32, "K copies: 16 or 32");
+  using State = Crc32State;
+  using Out = uint32_t;
+  static constexpr int kLdsBytes = 4 * 256 * K * 4;
+  static constexpr uint32_t kEntryShift = K == 32 ? 7 : 6;     // log2(K * 4)
+  static constexpr uint32_t kTableBytes = 256u * K * 4u;
+  const uint8_t* lds;
+  uint32_t lane4;                      // (lane % K) * 4
+  __device__ __forceinline__ void setup(uint8_t* l) {
+    uint32_t* t = reinterpret_cast<uint32_t*>(l);
+    const uint32_t* src = &kCrcTables.t[0][0];
+    for (uint32_t k = threadIdx.x; k < 4u * 256u * K; k += blockDim.x)
+      t[k] = src[k / K];               // table s entry e copy c at ((s*256 + e)*K + c)
+    __syncthreads();
+    lds = l;
+    lane4 = (threadIdx.x % K) * 4u;
+  }
+  __device__ __forceinline__ uint32_t look(uint32_t table, uint32_t byte) const {
+    return *reinterpret_cast<const uint32_t*>(lds + table * kTableBytes +
+                                              ((byte << kEntryShift) | lane4));
+  }
+  __device__ __forceinline__ uint32_t step4(uint32_t c, uint32_t w) const {
+    c ^= w;
+    return look(0, c >> 24) ^ look(1, (c >> 16) & 0xFFu) ^ look(2, (c >> 8) & 0xFFu) ^
+           look(3, c & 0xFFu);
+  }
+  __device__ __forceinline__ State init() { return State{0xFFFFFFFFu}; }
+  __device__ __forceinline__ void block(State& st, const uint4 (&w)[4]) {
+    uint32_t c = st.c;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      c = step4(c, w[k].x);
+      c = step4(c, w[k].y);
+      c = step4(c, w[k].z);
+      c = step4(c, w[k].w);
+    }
+    st.c = c;
+  }
+  __device__ __forceinline__ void finish(State& st, const uint8_t* tail, uint32_t r, uint64_t) {
+    uint32_t c = st.c;
+    if (r) {
+      uint32_t w[16];
+      load_tail(tail, r, w);
+#pragma unroll
+      for (int j = 0; j < 16; ++j)
+        if ((uint32_t)(4 * j + 4) <= r) c = step4(c, w[j]);
+      const uint32_t done = r & ~3u;
+      uint32_t wd = w[0];
+#pragma unroll
+      for (int j = 1; j < 16; ++j)
+        if ((uint32_t)j == (done >> 2)) wd = w[j];
+#pragma unroll
+      for (int b = 0; b < 3; ++b)      // the last 1..3 bytes, one at a time
+        if (done + (uint32_t)b < r) c = look(0, (c ^ (wd >> (8 * b))) & 0xFFu) ^ (c >> 8);
+    }
+    st.c = ~c;
+  }
+  __device__ __forceinline__ void store(Out* out, uint64_t idx, const State& st) {
+    out[idx] = st.c;
+  }
+};
+
 }  // namespace md5hip

@@ -437,6 +437,38 @@ crc32_fixed_xpose(const uint8_t* __restrict__ base, uint64_t n, uint32_t len, ui
   fixed_xpose_body<1, Crc32Hasher, 2>(base, n, len, stride, out, img, tabs);
 }
 
+// Lane-private tables (Crc32LaneHasher): one workgroup of kLaneBlock threads
+// per CU (the tables fill most of the LDS), lane-direct dwordx4 loads with a
+// D-deep ring, grid-stride over chunk groups so each workgroup fills its
+// tables once.
+template <int K, int D>
+__device__ __forceinline__ void crc32_fixed_lane_body(const uint8_t* __restrict__ base, uint64_t n,
+                                                      uint32_t len, uint64_t stride,
+                                                      uint32_t* __restrict__ out, uint8_t* tabs) {
+  Crc32LaneHasher<K> h;
+  h.setup(tabs);
+  const uint64_t step = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += step) {
+    Crc32State st = h.init();
+    lane_range<Crc32LaneHasher<K>, D>(h, st, base + i * stride, len);
+    out[i] = st.c;
+  }
+}
+
+__global__ void __launch_bounds__(1024)
+crc32_fixed_lane32(const uint8_t* __restrict__ base, uint64_t n, uint32_t len, uint64_t stride,
+                   uint32_t* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) uint8_t tabs[Crc32LaneHasher<32>::kLdsBytes];
+  crc32_fixed_lane_body<32, 4>(base, n, len, stride, out, tabs);
+}
+
+__global__ void __launch_bounds__(1024)
+crc32_fixed_lane16(const uint8_t* __restrict__ base, uint64_t n, uint32_t len, uint64_t stride,
+                   uint32_t* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) uint8_t tabs[Crc32LaneHasher<16>::kLdsBytes];
+  crc32_fixed_lane_body<16, 4>(base, n, len, stride, out, tabs);
+}
+
 // fastcrc (blk_io.c:408-424): len <= f -> crc(all), else crc(first f bytes)
 // ^ crc(last f bytes).  kImplicit: chunk i at base + i*stride, length flen.
 template <bool kImplicit>

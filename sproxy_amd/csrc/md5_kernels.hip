@@ -60,6 +60,43 @@ int default_variant() {
   return v;
 }
 
+// Compute units of the current device (grid sizing of one-workgroup-per-CU
+// kernels).
+int cu_count() {
+  int dev = 0, cus = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+      cus <= 0)
+    return 256;
+  return cus;
+}
+
+int default_crc_variant() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("CRC32HIP_VARIANT");
+    int x = e ? atoi(e) : 0;
+    v = (x > 0 && x < CRC32HIP_NUM_VARIANTS) ? x : CRC32HIP_LANE32;
+  }
+  return v;
+}
+
+// Lane-private-table kernels: kLaneBlock threads, `per_cu` workgroups per CU
+// resident (LDS-limited), grid-stride over the batch.
+constexpr int kLaneBlock = 1024;
+
+template <int K>
+int launch_crc_lane(const uint8_t* base, uint64_t n, uint32_t len, uint64_t stride, uint32_t* out,
+                    hipStream_t s) {
+  const int per_cu = K == 32 ? 1 : 2;
+  const uint64_t need = (n + kLaneBlock - 1) / kLaneBlock;
+  const uint64_t cap = (uint64_t)cu_count() * per_cu;
+  const uint64_t grid = need < cap ? need : cap;
+  hipLaunchKernelGGL(K == 32 ? crc32_fixed_lane32 : crc32_fixed_lane16, dim3((uint32_t)grid),
+                     dim3(kLaneBlock), 0, s, base, n, len, stride, out);
+  return launched();
+}
+
 template <int BB, bool NT = false>
 int launch_lds(const uint8_t* base, uint64_t n, uint32_t len, uint64_t stride, uint4* out,
                hipStream_t s) {
@@ -177,12 +214,14 @@ int md5hip_digest_fixed(const void* d_base, uint64_t n, uint32_t len, uint64_t s
   return md5hip_digest_fixed_variant(d_base, n, len, stride, d_digests, stream, MD5HIP_AUTO);
 }
 
-int crc32hip_fixed(const void* d_base, uint64_t n, uint32_t len, uint64_t stride,
-                   uint32_t fastcrc, uint32_t* d_crcs, void* stream) {
+int crc32hip_fixed_variant(const void* d_base, uint64_t n, uint32_t len, uint64_t stride,
+                           uint32_t fastcrc, uint32_t* d_crcs, void* stream, int variant) {
   if (n == 0) return 0;
   if (!d_base || !d_crcs || len > stride || (fastcrc & 3u)) return -EINVAL;
   if (((uintptr_t)d_crcs & 3u) != 0) return -EINVAL;
+  if (variant < 0 || variant >= CRC32HIP_NUM_VARIANTS) return -EINVAL;
   if (int e = device_ok()) return e;
+  if (variant == CRC32HIP_AUTO) variant = default_crc_variant();
   hipStream_t s = (hipStream_t)stream;
   const uint8_t* base = (const uint8_t*)d_base;
   if (fastcrc && len > fastcrc) {
@@ -193,7 +232,10 @@ int crc32hip_fixed(const void* d_base, uint64_t n, uint32_t len, uint64_t stride
                        fastcrc, d_crcs);
     return launched();
   }
-  if (((uintptr_t)base & 15u) == 0 && (stride & 15u) == 0 && stride < (1ull << 31) / 64) {
+  const bool aligned = ((uintptr_t)base & 15u) == 0 && (stride & 15u) == 0;
+  if (aligned && variant == CRC32HIP_LANE32) return launch_crc_lane<32>(base, n, len, stride, d_crcs, s);
+  if (aligned && variant == CRC32HIP_LANE16) return launch_crc_lane<16>(base, n, len, stride, d_crcs, s);
+  if (aligned && stride < (1ull << 31) / 64) {
     const uint64_t g = (n + kBlock - 1) / kBlock;
     if (g > 0x7fffffffull) return -EINVAL;
     hipLaunchKernelGGL(crc32_fixed_xpose, dim3((uint32_t)g), dim3(kBlock), 0, s, base, n, len,
@@ -206,6 +248,11 @@ int crc32hip_fixed(const void* d_base, uint64_t n, uint32_t len, uint64_t stride
                      (const uint64_t*)nullptr, (const uint32_t*)nullptr,
                      (const uint32_t*)nullptr, n, stride, len, d_crcs);
   return launched();
+}
+
+int crc32hip_fixed(const void* d_base, uint64_t n, uint32_t len, uint64_t stride,
+                   uint32_t fastcrc, uint32_t* d_crcs, void* stream) {
+  return crc32hip_fixed_variant(d_base, n, len, stride, fastcrc, d_crcs, stream, CRC32HIP_AUTO);
 }
 
 int crc32hip_desc(const void* d_base, const uint64_t* d_offsets, const uint32_t* d_lens,

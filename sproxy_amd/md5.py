@@ -152,8 +152,11 @@ def digest_desc(base, offsets, lens, order=None, out=None, stream=None):
     return out
 
 
+CRC_VARIANTS = {"auto": 0, "shared8": 1, "lane32": 2, "lane16": 3}   # enum crc32hip_variant
+
+
 def crc32_fixed(data, n: int = None, length: int = None, stride: int = None, fastcrc: int = 0,
-                out=None, stream=None):
+                out=None, stream=None, variant=0):
     """crcs[i] = netcache block CRC-32 of chunk i (blk_make_crc semantics,
     blk_io.c:354-430; fastcrc > 0 -> head ^ tail).  uint32 [n] on device."""
     _need_cuda(data, "data")
@@ -166,8 +169,11 @@ def crc32_fixed(data, n: int = None, length: int = None, stride: int = None, fas
         raise ValueError("batch extends past the end of `data`")
     if out is None:
         out = torch.empty(n, dtype=torch.int32, device=data.device)
-    check("crc32hip_fixed", lib().crc32hip_fixed(data.data_ptr(), n, length, stride, fastcrc,
-                                                 out.data_ptr(), _stream(stream)))
+    if isinstance(variant, str):
+        variant = CRC_VARIANTS[variant]
+    check("crc32hip_fixed_variant",
+          lib().crc32hip_fixed_variant(data.data_ptr(), n, length, stride, fastcrc, out.data_ptr(),
+                                       _stream(stream), variant))
     return out
 
 
@@ -361,5 +367,5 @@ def pool_plan(lens, nparts: int) -> np.ndarray:
 
 __all__ = ["MD5Context", "MD5Init", "MD5Update", "MD5Final", "MD5_DIGEST_SIZE", "MD5HipError",
            "md5", "digest_fixed", "digest_desc", "crc32_fixed", "crc32_desc", "plan_order", "fill_synthetic", "Batcher",
-           "Pool", "pool_plan",
+           "Pool", "pool_plan", "CRC_VARIANTS",
            "variant_name", "resolve_variant", "VARIANTS"]

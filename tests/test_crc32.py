@@ -66,19 +66,24 @@ def _dev(a, cuda):
     return torch.from_numpy(np.ascontiguousarray(a)).to(cuda)
 
 
+CRC_VARIANTS = list(m.CRC_VARIANTS)
+
+
 @pytest.mark.gpu
-def test_gpu_crc_batches(cuda):
+@pytest.mark.parametrize("variant", CRC_VARIANTS)
+def test_gpu_crc_batches(cuda, variant):
     for b in GOLD["batches"]:
         n, L = b["n"], b["len"]
         host = gen.xorshift_array(n * L)
-        got = m.crc32_fixed(_dev(host, cuda), n, L).cpu().numpy().view(np.uint32)
+        got = m.crc32_fixed(_dev(host, cuda), n, L, variant=variant).cpu().numpy().view(np.uint32)
         assert "%08x" % gen.fold(b"".join(struct.pack("<I", int(c)) for c in got)) == b["fold"], (n, L)
         if "crc" in b:
             assert ["%08x" % c for c in got] == b["crc"]
 
 
 @pytest.mark.gpu
-def test_gpu_crc_edges_fixed_and_unaligned(cuda):
+@pytest.mark.parametrize("variant", CRC_VARIANTS)
+def test_gpu_crc_edges_fixed_and_unaligned(cuda, variant):
     big = np.frombuffer(gen.mul_pattern(1 << 20), dtype=np.uint8)
     for L, want in zip(GOLD["edge"]["lengths"], GOLD["edge"]["crc"]):
         if L > (1 << 17):
@@ -88,7 +93,7 @@ def test_gpu_crc_edges_fixed_and_unaligned(cuda):
             host = np.zeros(n * stride + 16, dtype=np.uint8)
             for i in range(n):
                 host[i * stride:i * stride + L] = big[:L]
-            got = m.crc32_fixed(_dev(host, cuda), n, L, stride).cpu().numpy().view(np.uint32)
+            got = m.crc32_fixed(_dev(host, cuda), n, L, stride, variant=variant).cpu().numpy().view(np.uint32)
             assert all("%08x" % c == want for c in got), (L, stride)
 
 
@@ -114,12 +119,27 @@ def test_gpu_crc_desc_fastcrc(cuda, fast):
 
 
 @pytest.mark.gpu
+def test_gpu_crc_variants_grid_stride(cuda):
+    """More chunks than one grid of the lane-table kernels covers (grid-stride
+    loop), ragged n, every variant equal to the oracle."""
+    n, L = 300000, 1040
+    host = gen.xorshift_array(n * L, seed=515)
+    want = gen.oracle_crc32_batch(host, np.arange(n, dtype=np.uint64) * L, [L] * n)
+    d = _dev(host, cuda)
+    for v in CRC_VARIANTS:
+        got = m.crc32_fixed(d, n, L, variant=v).cpu().numpy().view(np.uint32)
+        assert np.array_equal(got, want), v
+
+
+@pytest.mark.gpu
 def test_gpu_crc_full_size(cuda):
     import torch
     n, L = 1 << 20, 16384
     d = torch.empty(n * L, dtype=torch.uint8, device=cuda)
     m.fill_synthetic(d, seed=0xCC)
     got = m.crc32_fixed(d, n, L)
+    for v in CRC_VARIANTS[1:]:
+        assert torch.equal(m.crc32_fixed(d, n, L, variant=v), got), v
     idx = np.unique(np.concatenate([[0, n - 1], np.random.default_rng(3).integers(0, n, 4096)]))
     rows = d.view(n, L)[torch.from_numpy(idx).to(cuda)].cpu().numpy()
     want = gen.oracle_crc32_batch(rows.reshape(-1), np.arange(idx.size, dtype=np.uint64) * L,
