@@ -62,8 +62,12 @@ def main():
     out = torch.empty((lens.size, 16), dtype=torch.uint8, device="cuda")
     st = torch.cuda.current_stream().cuda_stream
     ref = None
-    for kind, name in [(0, "r1"), (1, "lat_prio_D2"), (3, "D8"), (16, "r1_t64"),
-                       (17, "lat_prio_D2_t64"), (18, "D4_t64"), (19, "D8_t64"), (20, "D8_noprio_t64")]:
+    cases = [(0, "r1"), (1, "lat_prio_D2"), (3, "D8"), (16, "r1_t64"),
+             (17, "lat_prio_D2_t64"), (18, "D4_t64"), (19, "D8_t64"), (20, "D8_noprio_t64"),
+             (22, "D8_pair_t64")]
+    if "--pair" in sys.argv:
+        cases = [(19, "D8_t64"), (22, "D8_pair_t64"), (19, "D8_t64_again"), (22, "D8_pair_t64_again")]
+    for kind, name in cases:
         f = lambda: D.md5diag_desc(kind, data.data_ptr(), d_off.data_ptr(), d_len.data_ptr(),  # noqa
                                    order.data_ptr(), lens.size, out.data_ptr(), st)
         ms = timeit(f, reps=2, rounds=3)
@@ -71,6 +75,9 @@ def main():
             ref = out.clone()
         assert torch.equal(out, ref), name
         res["c3_" + name] = {"ms": round(ms, 3), "GBps": round(lens.sum() / ms / 1e6, 1)}
+    if "--pair" in sys.argv:
+        print(json.dumps(res))
+        return
     del data
     torch.cuda.empty_cache()
     # uniform small chunks through the descriptor kernel (occupancy check)

@@ -10,6 +10,9 @@
 //   kind 12   compute only with the latency-form step (md5_core.h kLat)
 //   kind 13,14 single-chain latency: few lanes, long chunks (kLat off / on)
 //   kind 20-26 xpose1 with buffer-load aux 0, 1, 2, 3, 16, 18, 19 (cache policy A/B)
+//   kind 8,9  load only, direct2 / direct4 with paired (whole-line) ring refill
+//   kind 10,11 MD5 direct2 / direct4 with paired refill
+//   kind 27   CRC-32 lane32 with the unpaired ring (out = u32 per chunk)
 //   kind 100+K VALU issue-rate probes (instruction K of diag_valu_rate)
 //
 // C ABI: int md5diag_run(int kind, const void *base, uint64_t n, uint32_t len,
@@ -22,6 +25,20 @@ namespace md5hip {
 
 template __global__ void md5_fixed_direct<2, FoldHasher>(const uint8_t*, uint64_t, uint32_t, uint64_t, uint4*);
 template __global__ void md5_fixed_direct<4, FoldHasher>(const uint8_t*, uint64_t, uint32_t, uint64_t, uint4*);
+template __global__ void md5_fixed_direct<2, FoldHasher, true>(const uint8_t*, uint64_t, uint32_t, uint64_t, uint4*);
+template __global__ void md5_fixed_direct<4, FoldHasher, true>(const uint8_t*, uint64_t, uint32_t, uint64_t, uint4*);
+template __global__ void md5_fixed_direct<2, Md5Hasher<false>, true>(const uint8_t*, uint64_t, uint32_t, uint64_t, uint4*);
+template __global__ void md5_fixed_direct<4, Md5Hasher<false>, true>(const uint8_t*, uint64_t, uint32_t, uint64_t, uint4*);
+template __global__ void md5_desc<false, true, true, 8, true>(const uint8_t*, const uint64_t*, const uint32_t*,
+                                                              const uint32_t*, uint64_t, uint64_t, uint32_t, uint4*);
+
+// CRC-32 lane-private tables with the unpaired ring (A/B of the paired default)
+__global__ void __launch_bounds__(1024)
+diag_crc_lane32_unpaired(const uint8_t* __restrict__ base, uint64_t n, uint32_t len, uint64_t stride,
+                         uint32_t* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) uint8_t tabs[Crc32LaneHasher<32>::kLdsBytes];
+  crc32_fixed_lane_body<32, 4, false>(base, n, len, stride, out, tabs);
+}
 #define DESC_INST(L, P, D)                                                                  \
   template __global__ void md5_desc<false, L, P, D>(const uint8_t*, const uint64_t*,       \
                                                     const uint32_t*, const uint32_t*, uint64_t, \
@@ -219,6 +236,27 @@ extern "C" int md5diag_run(int kind, const void* base, uint64_t n, uint32_t len,
     case 2:
       hipLaunchKernelGGL((md5_fixed_direct<4, FoldHasher>), dim3(grid), dim3(256), 0, s, b, n, len, stride, o);
       break;
+    case 8:
+      hipLaunchKernelGGL((md5_fixed_direct<2, FoldHasher, true>), dim3(grid), dim3(256), 0, s, b, n, len, stride, o);
+      break;
+    case 9:
+      hipLaunchKernelGGL((md5_fixed_direct<4, FoldHasher, true>), dim3(grid), dim3(256), 0, s, b, n, len, stride, o);
+      break;
+    case 10:
+      hipLaunchKernelGGL((md5_fixed_direct<2, Md5Hasher<false>, true>), dim3(grid), dim3(256), 0, s, b, n, len, stride, o);
+      break;
+    case 11:
+      hipLaunchKernelGGL((md5_fixed_direct<4, Md5Hasher<false>, true>), dim3(grid), dim3(256), 0, s, b, n, len, stride, o);
+      break;
+    case 27: {
+      int dev = 0, cus = 256;
+      (void)hipGetDevice(&dev);
+      (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+      const uint64_t need = (n + 1023) / 1024;
+      const uint32_t g = (uint32_t)(need < (uint64_t)cus ? need : (uint64_t)cus);
+      hipLaunchKernelGGL(diag_crc_lane32_unpaired, dim3(g), dim3(1024), 0, s, b, n, len, stride, (uint32_t*)out);
+      break;
+    }
     case 3: {
       const size_t lds = 4 * 2 * 64 * 64;
       hipLaunchKernelGGL(diag_lds64_load, dim3(grid), dim3(256), lds, s, b, n, len, stride, o);
@@ -262,7 +300,8 @@ extern "C" int md5diag_run(int kind, const void* base, uint64_t n, uint32_t len,
 }
 
 // Descriptor-kernel A/B (C3): 0 = (no kLat, no prio, D=2: round-1 kernel),
-// 1 = (kLat, prio, D=2), 2 = D=4, 3 = D=8, 4 = D=8 without prio, 5 = D=12;
+// 1 = (kLat, prio, D=2), 2 = D=4, 3 = D=8, 4 = D=8 without prio, 5 = D=12,
+// 6 = D=8 with paired (whole-line) refill;
 // +16: the same with 64-thread workgroups.
 extern "C" int md5diag_desc(int kind, const void* base, const uint64_t* offs, const uint32_t* lens,
                             const uint32_t* order, uint64_t n, void* out, void* stream) {
@@ -279,6 +318,7 @@ extern "C" int md5diag_desc(int kind, const void* base, const uint64_t* offs, co
     case 3: L(false, true, true, 8); break;
     case 4: L(false, true, false, 8); break;
     case 5: L(false, true, true, 12); break;
+    case 6: L(false, true, true, 8, true); break;
     default: return -EINVAL;
   }
 #undef L

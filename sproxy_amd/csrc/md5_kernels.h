@@ -42,10 +42,33 @@ __device__ __forceinline__ void load_block(uint4 (&r)[4], const uint4* p) {
 // Fixed-length, lane-direct loads.  base/stride 16-B aligned, len <= stride.
 // ---------------------------------------------------------------------------
 // (hashers without LDS state only: Md5Hasher, FoldHasher)
-template <int D, class H = Md5Hasher<false>>
+// Ring refill.  kPair: slots are refilled two at a time (blocks 2k, 2k+1 --
+// one whole 128-B line when the chunk is 128-B aligned), so a lane never
+// leaves half a line in the cache for a later instruction: with ~16 waves x
+// 64 lanes per CU the half-consumed lines of all lanes add up to the size of
+// an XCD's L2, and unpaired refills re-fetch the evicted halves.
+template <class H, int D, bool kPair>
+__device__ __forceinline__ void ring_steps(H& h, typename H::State& st, uint4 (&R)[D][4],
+                                           const uint4* p, uint32_t blk, uint32_t lastb) {
+#pragma unroll
+  for (int j = 0; j < D; ++j) {
+    h.block(st, R[j]);
+    if constexpr (kPair) {
+      if (j & 1) {
+        load_block(R[j - 1], p + 4 * min(blk + j - 1 + D, lastb));
+        load_block(R[j], p + 4 * min(blk + j + D, lastb));
+      }
+    } else {
+      load_block(R[j], p + 4 * min(blk + j + D, lastb));
+    }
+  }
+}
+
+template <int D, class H = Md5Hasher<false>, bool kPair = false>
 __global__ void __launch_bounds__(256)
 md5_fixed_direct(const uint8_t* __restrict__ base, uint64_t n, uint32_t len, uint64_t stride,
                  typename H::Out* __restrict__ out) {
+  static_assert(!kPair || D % 2 == 0, "paired refill needs an even ring");
   H h;
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
@@ -62,13 +85,8 @@ md5_fixed_direct(const uint8_t* __restrict__ base, uint64_t n, uint32_t len, uin
 #pragma unroll
     for (int j = 0; j < D; ++j) load_block(R[j], p + 4 * min((uint32_t)j, lastb));
     uint32_t blk = 0;
-    for (; blk + D <= nfull; blk += D) {   // steady state: no conditionals, so
-#pragma unroll                              // the waits stay counted (vmcnt(4*(D-1)))
-      for (int j = 0; j < D; ++j) {
-        h.block(st, R[j]);
-        load_block(R[j], p + 4 * min(blk + j + D, lastb));
-      }
-    }
+    for (; blk + D <= nfull; blk += D)     // steady state: no conditionals, so
+      ring_steps<H, D, kPair>(h, st, R, p, blk, lastb);   // the waits stay counted
 #pragma unroll
     for (int j = 0; j < D - 1; ++j)
       if (blk + j < nfull) h.block(st, R[j]);
@@ -349,7 +367,7 @@ __device__ __forceinline__ uint32_t wave_max(uint32_t v) {
 // One lane digests [chunk, chunk + len) into st (blocks + finish): aligned
 // chunks through a D-deep dwordx4 register ring, unaligned ones through
 // dword loads + v_alignbit_b32.
-template <class H, int D>
+template <class H, int D, bool kPair = false>
 __device__ __forceinline__ void lane_range(H& h, typename H::State& st, const uint8_t* chunk,
                                            uint32_t len) {
   const uint32_t nfull = len >> 6;
@@ -361,13 +379,8 @@ __device__ __forceinline__ void lane_range(H& h, typename H::State& st, const ui
 #pragma unroll
       for (int j = 0; j < D; ++j) load_block(R[j], p + 4 * min((uint32_t)j, lastb));
       uint32_t blk = 0;
-      for (; blk + D <= nfull; blk += D) {
-#pragma unroll
-        for (int j = 0; j < D; ++j) {
-          h.block(st, R[j]);
-          load_block(R[j], p + 4 * min(blk + j + D, lastb));
-        }
-      }
+      for (; blk + D <= nfull; blk += D)
+        ring_steps<H, D, kPair>(h, st, R, p, blk, lastb);
 #pragma unroll
       for (int j = 0; j < D - 1; ++j)
         if (blk + j < nfull) h.block(st, R[j]);
@@ -391,7 +404,8 @@ __device__ __forceinline__ void lane_range(H& h, typename H::State& st, const ui
 // D: depth of the per-lane register ring (blocks in flight per lane).  Mixed
 // batches have few waves per SIMD (C3: ~1.2), so latency must be hidden by
 // prefetch depth, not by occupancy.
-template <bool kImplicit, class H = Md5Hasher<true>, bool kPrio = true, int D = 8>
+template <bool kImplicit, class H = Md5Hasher<true>, bool kPrio = true, int D = 8,
+          bool kPair = false>
 __device__ __forceinline__ void desc_body(const uint8_t* __restrict__ base,
                                           const uint64_t* __restrict__ offs,
                                           const uint32_t* __restrict__ lens,
@@ -414,16 +428,17 @@ __device__ __forceinline__ void desc_body(const uint8_t* __restrict__ base,
     else if (wmax >= 256u) __builtin_amdgcn_s_setprio(1);    // >= 16 KiB
   }
   typename H::State st = h.init();
-  lane_range<H, D>(h, st, chunk, len);
+  lane_range<H, D, kPair>(h, st, chunk, len);
   h.store(out, c, st);
 }
 
-template <bool kImplicit, bool kLat = true, bool kPrio = true, int D = 8>
+template <bool kImplicit, bool kLat = true, bool kPrio = true, int D = 8, bool kPair = false>
 __global__ void __launch_bounds__(256)
 md5_desc(const uint8_t* __restrict__ base, const uint64_t* __restrict__ offs,
          const uint32_t* __restrict__ lens, const uint32_t* __restrict__ order, uint64_t n,
          uint64_t stride, uint32_t flen, uint4* __restrict__ out) {
-  desc_body<kImplicit, Md5Hasher<kLat>, kPrio, D>(base, offs, lens, order, n, stride, flen, out);
+  desc_body<kImplicit, Md5Hasher<kLat>, kPrio, D, kPair>(base, offs, lens, order, n, stride, flen,
+                                                         out);
 }
 
 // ---------------------------------------------------------------------------
@@ -441,7 +456,7 @@ crc32_fixed_xpose(const uint8_t* __restrict__ base, uint64_t n, uint32_t len, ui
 // per CU (the tables fill most of the LDS), lane-direct dwordx4 loads with a
 // D-deep ring, grid-stride over chunk groups so each workgroup fills its
 // tables once.
-template <int K, int D>
+template <int K, int D, bool kPair = true>
 __device__ __forceinline__ void crc32_fixed_lane_body(const uint8_t* __restrict__ base, uint64_t n,
                                                       uint32_t len, uint64_t stride,
                                                       uint32_t* __restrict__ out, uint8_t* tabs) {
@@ -450,7 +465,7 @@ __device__ __forceinline__ void crc32_fixed_lane_body(const uint8_t* __restrict_
   const uint64_t step = (uint64_t)gridDim.x * blockDim.x;
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += step) {
     Crc32State st = h.init();
-    lane_range<Crc32LaneHasher<K>, D>(h, st, base + i * stride, len);
+    lane_range<Crc32LaneHasher<K>, D, kPair>(h, st, base + i * stride, len);
     out[i] = st.c;
   }
 }
