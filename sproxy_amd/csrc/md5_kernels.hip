@@ -76,7 +76,7 @@ int default_crc_variant() {
   if (v < 0) {
     const char* e = getenv("CRC32HIP_VARIANT");
     int x = e ? atoi(e) : 0;
-    v = (x > 0 && x < CRC32HIP_NUM_VARIANTS) ? x : CRC32HIP_LANE32;
+    v = (x > 0 && x < CRC32HIP_NUM_VARIANTS) ? x : CRC32HIP_SHARED8;  // measured best, DESIGN.md §5
   }
   return v;
 }
