@@ -13,6 +13,8 @@
 //   kind 8,9  load only, direct2 / direct4 with paired (whole-line) ring refill
 //   kind 10,11 MD5 direct2 / direct4 with paired refill
 //   kind 27   CRC-32 lane32 with the unpaired ring (out = u32 per chunk)
+//   kind 28-33 serial-chain latency with 64/32/16/1 active lanes (28-31), and
+//             64/32 with the latency-form step (32,33); n = waves, len = bytes
 //   kind 100+K VALU issue-rate probes (instruction K of diag_valu_rate)
 //
 // C ABI: int md5diag_run(int kind, const void *base, uint64_t n, uint32_t len,
@@ -109,6 +111,28 @@ diag_compute(uint64_t n, uint32_t nblocks, uint4* __restrict__ out) {
   }
   compress_pad_only(st, nblocks * 512u, 0u);
   if (i < n) out[i] = make_uint4(st.a, st.b, st.c, st.d);
+}
+
+// Serial-chain latency with ACT active lanes per wave (the others exit at
+// once): does a partly-masked wave64 finish a dependent MD5 chain sooner?
+// Message words live in registers (xor with the block index, off the chain).
+template <int ACT, bool kLat>
+__global__ void __launch_bounds__(64)
+diag_chain(uint32_t nblocks, uint4* __restrict__ out) {
+  if ((threadIdx.x & 63u) >= (uint32_t)ACT) return;
+  const uint32_t i = blockIdx.x * 64u + threadIdx.x;
+  uint4 w0[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+    w0[k] = make_uint4(i * 2654435761u + 4 * k, i * 40503u + 4 * k + 1, i ^ (0x9E37u * k), i + 77u * k);
+  State st = initial_state();
+  for (uint32_t b = 0; b < nblocks; ++b) {
+    uint4 w[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) w[k] = make_uint4(w0[k].x ^ b, w0[k].y ^ b, w0[k].z ^ b, w0[k].w ^ b);
+    compress_regs<kLat>(st, w);
+  }
+  out[i] = make_uint4(st.a, st.b, st.c, st.d);
 }
 
 // Ideal streaming read of n*len bytes: grid-stride, 16 B per lane, consecutive
@@ -222,6 +246,18 @@ extern "C" int md5diag_run(int kind, const void* base, uint64_t n, uint32_t len,
     case 24: hipLaunchKernelGGL(diag_xpose1_cp<16>, dim3(grid), dim3(256), 0, s, b, n, len, stride, o); break;
     case 25: hipLaunchKernelGGL(diag_xpose1_cp<18>, dim3(grid), dim3(256), 0, s, b, n, len, stride, o); break;
     case 26: hipLaunchKernelGGL(diag_xpose1_cp<19>, dim3(grid), dim3(256), 0, s, b, n, len, stride, o); break;
+    case 28: case 29: case 30: case 31: case 32: case 33: {
+      // n = workgroups (64 threads, one wave each); len = bytes per chain
+      const dim3 g1((uint32_t)n);
+      const uint32_t nb = len >> 6;
+      if (kind == 28) hipLaunchKernelGGL((diag_chain<64, false>), g1, dim3(64), 0, s, nb, o);
+      if (kind == 29) hipLaunchKernelGGL((diag_chain<32, false>), g1, dim3(64), 0, s, nb, o);
+      if (kind == 30) hipLaunchKernelGGL((diag_chain<16, false>), g1, dim3(64), 0, s, nb, o);
+      if (kind == 31) hipLaunchKernelGGL((diag_chain<1, false>), g1, dim3(64), 0, s, nb, o);
+      if (kind == 32) hipLaunchKernelGGL((diag_chain<64, true>), g1, dim3(64), 0, s, nb, o);
+      if (kind == 33) hipLaunchKernelGGL((diag_chain<32, true>), g1, dim3(64), 0, s, nb, o);
+      break;
+    }
     case 13: case 14: {
       // single-chain latency: n lanes (one wave per CU at n = 16384), each
       // hashing `len` bytes; 64-thread workgroups so every CU gets one wave
