@@ -33,6 +33,8 @@ template __global__ void md5_fixed_direct<2, Md5Hasher<false>, true>(const uint8
 template __global__ void md5_fixed_direct<4, Md5Hasher<false>, true>(const uint8_t*, uint64_t, uint32_t, uint64_t, uint4*);
 template __global__ void md5_desc<false, true, true, 8, true>(const uint8_t*, const uint64_t*, const uint32_t*,
                                                               const uint32_t*, uint64_t, uint64_t, uint32_t, uint4*);
+template __global__ void md5_desc<false, true, true, 8, false, true>(const uint8_t*, const uint64_t*, const uint32_t*,
+                                                                     const uint32_t*, uint64_t, uint64_t, uint32_t, uint4*);
 
 // CRC-32 lane-private tables with the unpaired ring (A/B of the paired default)
 __global__ void __launch_bounds__(1024)
@@ -337,7 +339,8 @@ extern "C" int md5diag_run(int kind, const void* base, uint64_t n, uint32_t len,
 
 // Descriptor-kernel A/B (C3): 0 = (no kLat, no prio, D=2: round-1 kernel),
 // 1 = (kLat, prio, D=2), 2 = D=4, 3 = D=8, 4 = D=8 without prio, 5 = D=12,
-// 6 = D=8 with paired (whole-line) refill;
+// 6 = D=8 with paired (whole-line) refill, 7 = D=8 holding the whole register
+// file (one wave per SIMD: long chains run alone);
 // +16: the same with 64-thread workgroups.
 extern "C" int md5diag_desc(int kind, const void* base, const uint64_t* offs, const uint32_t* lens,
                             const uint32_t* order, uint64_t n, void* out, void* stream) {
@@ -355,6 +358,7 @@ extern "C" int md5diag_desc(int kind, const void* base, const uint64_t* offs, co
     case 4: L(false, true, false, 8); break;
     case 5: L(false, true, true, 12); break;
     case 6: L(false, true, true, 8, true); break;
+    case 7: L(false, true, true, 8, false, true); break;
     default: return -EINVAL;
   }
 #undef L

@@ -405,7 +405,7 @@ __device__ __forceinline__ void lane_range(H& h, typename H::State& st, const ui
 // batches have few waves per SIMD (C3: ~1.2), so latency must be hidden by
 // prefetch depth, not by occupancy.
 template <bool kImplicit, class H = Md5Hasher<true>, bool kPrio = true, int D = 8,
-          bool kPair = false>
+          bool kPair = false, bool kHog = false>
 __device__ __forceinline__ void desc_body(const uint8_t* __restrict__ base,
                                           const uint64_t* __restrict__ offs,
                                           const uint32_t* __restrict__ lens,
@@ -415,6 +415,8 @@ __device__ __forceinline__ void desc_body(const uint8_t* __restrict__ base,
                                           uint8_t* hlds = nullptr) {
   H h;
   h.setup(hlds);                     // before any early exit (may barrier)
+  if constexpr (kHog)                // claim the whole register file: one wave per SIMD
+    asm volatile("" ::: "v255", "a255");
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const uint64_t c = (!kImplicit && order) ? (uint64_t)order[i] : i;
@@ -432,13 +434,14 @@ __device__ __forceinline__ void desc_body(const uint8_t* __restrict__ base,
   h.store(out, c, st);
 }
 
-template <bool kImplicit, bool kLat = true, bool kPrio = true, int D = 8, bool kPair = false>
+template <bool kImplicit, bool kLat = true, bool kPrio = true, int D = 8, bool kPair = false,
+          bool kHog = false>
 __global__ void __launch_bounds__(256)
 md5_desc(const uint8_t* __restrict__ base, const uint64_t* __restrict__ offs,
          const uint32_t* __restrict__ lens, const uint32_t* __restrict__ order, uint64_t n,
          uint64_t stride, uint32_t flen, uint4* __restrict__ out) {
-  desc_body<kImplicit, Md5Hasher<kLat>, kPrio, D, kPair>(base, offs, lens, order, n, stride, flen,
-                                                         out);
+  desc_body<kImplicit, Md5Hasher<kLat>, kPrio, D, kPair, kHog>(base, offs, lens, order, n, stride,
+                                                               flen, out);
 }
 
 // ---------------------------------------------------------------------------
