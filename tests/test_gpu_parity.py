@@ -263,3 +263,51 @@ def test_pool_matches_oracle(cuda):
             assert nbad == 2 and not ok[5] and not ok[600]
             p.set_digest(m.Pool.CRC32, 64)
             assert np.array_equal(p.submit(bufs), gen.oracle_crc32_batch(arena, offs, lens, 64))
+
+
+@pytest.mark.parametrize("variant", FIXED_VARIANTS)
+def test_fixed_ragged_counts_and_empty_chunks(cuda, variant):
+    """n not a multiple of the wave (64) or workgroup (256), n = 1, and
+    zero-length chunks (digest of the empty message, md5.c:221-265)."""
+    L = 4160                                       # 65 blocks: odd block count, no tail
+    host = gen.xorshift_array(4100 * L, seed=61)
+    d = _dev(host, cuda)
+    for n in (1, 63, 65, 255, 257, 4097):
+        got = m.digest_fixed(d, n, L, variant=variant).cpu().numpy()
+        assert np.array_equal(got, gen.oracle_digests_fixed(host, n, L)), (variant, n)
+    got = m.digest_fixed(d, 100, 0, 16, variant=variant).cpu().numpy()
+    assert all(bytes(x).hex() == "d41d8cd98f00b204e9800998ecf8427e" for x in got)
+
+
+def test_huge_stride_and_large_chunks(cuda):
+    """A stride past the 32-bit buffer-offset range of the xpose/lds loaders
+    (they fall back to the lane-direct kernel), and long chunks: 16 MiB each
+    through the fixed entry and one 64 MiB chunk among small ones through the
+    descriptor entry (MD5 and CRC-32)."""
+    L, stride, n = 16384, 40 << 20, 5              # 40 MiB > 2^31 / 64
+    host = np.zeros(n * stride, dtype=np.uint8)
+    for i in range(n):
+        host[i * stride:i * stride + L] = np.frombuffer(gen.xorshift_bytes(L, seed=70 + i), np.uint8)
+    d = _dev(host, cuda)
+    want = gen.oracle_digests(host, np.arange(n, dtype=np.uint64) * stride, [L] * n)
+    for v in FIXED_VARIANTS:
+        assert np.array_equal(m.digest_fixed(d, n, L, stride, variant=v).cpu().numpy(), want), v
+    crc_want = gen.oracle_crc32_batch(host, np.arange(n, dtype=np.uint64) * stride, [L] * n)
+    for v in m.CRC_VARIANTS:
+        got = m.crc32_fixed(d, n, L, stride, variant=v).cpu().numpy().view(np.uint32)
+        assert np.array_equal(got, crc_want), v
+    del d
+    nb, Lb = 4, 16 << 20
+    big = gen.xorshift_array(nb * Lb, seed=71)
+    db = _dev(big, cuda)
+    assert np.array_equal(m.digest_fixed(db, nb, Lb).cpu().numpy(), gen.oracle_digests_fixed(big, nb, Lb))
+    lens = [3, 64 << 20, 100, 0, 4097]
+    offs, total = gen.pack_offsets(lens, align=16)
+    arena = gen.xorshift_array(total + 64, seed=72)
+    da = _dev(arena, cuda)
+    t_off = torch.tensor(offs, dtype=torch.int64, device=cuda)
+    t_len = torch.tensor(lens, dtype=torch.int32, device=cuda)
+    got = m.digest_desc(da, t_off, t_len).cpu().numpy()
+    assert np.array_equal(got, gen.oracle_digests(arena, offs, lens))
+    got = m.crc32_desc(da, t_off, t_len).cpu().numpy().view(np.uint32)
+    assert np.array_equal(got, gen.oracle_crc32_batch(arena, offs, lens))
