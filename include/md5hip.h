@@ -162,6 +162,26 @@ int md5hip_batch_verify_iov(md5hip_batcher *b, const struct md5hip_iov *segs,
                             const uint64_t *seg_first, uint64_t n, const void *expected,
                             unsigned char *ok);
 
+/*
+ * Zero-copy input.  md5hip_host_register pins and device-maps host memory
+ * for every device (hipHostRegister, portable + mapped) -- e.g. each bulk of
+ * netcache's page heap as it is allocated (bc_mgr.c:1260-1290).  A batcher
+ * whose gather mode is DEVICE or DMA then skips the host memcpy into its
+ * staging slice for any call whose segments all lie in registered memory:
+ *   DEVICE  a gather kernel reads the segments over PCIe into HBM;
+ *   DMA     one async DMA copy per segment.
+ * Other calls (or mode HOST, the default) gather on the host as before.
+ * Ranges must not overlap (-EEXIST); unregister with the same base.
+ */
+enum md5hip_gather_mode {
+    MD5HIP_GATHER_HOST = 0,
+    MD5HIP_GATHER_DEVICE = 1,
+    MD5HIP_GATHER_DMA = 2
+};
+int md5hip_host_register(void *base, uint64_t bytes);
+int md5hip_host_unregister(void *base);
+int md5hip_batcher_set_gather(md5hip_batcher *b, int mode);
+
 /* digests[i] = MD5(h_base + i*stride, len) from one contiguous host buffer
  * (pinned for full PCIe rate), copied slice by slice with no host gather. */
 int md5hip_batch_host_fixed(md5hip_batcher *b, const void *h_base, uint64_t n, uint32_t len,
@@ -183,6 +203,7 @@ int md5hip_pool_create(const int *devices, uint32_t ndev, uint64_t slice_bytes, 
 void md5hip_pool_destroy(md5hip_pool *p);
 int md5hip_pool_ndev(const md5hip_pool *p);
 int md5hip_pool_set_digest(md5hip_pool *p, int kind, uint32_t fastcrc);
+int md5hip_pool_set_gather(md5hip_pool *p, int mode);
 int md5hip_pool_submit(md5hip_pool *p, const void *const *ptrs, const uint32_t *lens, uint64_t n,
                        unsigned char *digests);
 int md5hip_pool_submit_iov(md5hip_pool *p, const struct md5hip_iov *segs,

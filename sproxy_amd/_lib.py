@@ -85,6 +85,10 @@ def lib():
         "md5hip_pool_host_fixed": (i, [vp, vp, u64, u32, u64, vp]),
         "md5hip_pool_plan": (i, [vp, u64, u32, vp]),
         "md5hip_batcher_get_digest": (i, [vp, vp, vp]),
+        "md5hip_host_register": (i, [vp, u64]),
+        "md5hip_host_unregister": (i, [vp]),
+        "md5hip_batcher_set_gather": (i, [vp, i]),
+        "md5hip_pool_set_gather": (i, [vp, i]),
         "nc_canned_digest_size": (u64, [u32, u32]),
         "nc_digest_update": (i, [vp, u64, u32, u64, u64, vp]),
         "nc_digest_verify": (i, [vp, u64, u32, u64, vp]),
@@ -118,7 +122,8 @@ EXPORTS = ["MD5Init", "MD5Update", "MD5Final", "nc_MD5Init", "nc_MD5Update", "nc
            "md5hip_pool_plan", "md5hip_batcher_get_digest", "nc_canned_digest_size",
            "nc_digest_update", "nc_digest_verify", "nc_digest_scatter", "nc_digest_compare",
            "nc_crc32", "nc_header_crc", "nc_header_seal", "nc_header_verify",
-           "md5hip_batch_verify_headers"]
+           "md5hip_batch_verify_headers", "md5hip_host_register", "md5hip_host_unregister",
+           "md5hip_batcher_set_gather", "md5hip_pool_set_gather"]
 
 
 def check(fn, rc):

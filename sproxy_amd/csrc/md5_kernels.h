@@ -523,6 +523,37 @@ crc32_desc(const uint8_t* __restrict__ base, const uint64_t* __restrict__ offs,
 }
 
 // ---------------------------------------------------------------------------
+// Device-side gather for the batcher's zero-copy path: segment k of a slice
+// is read from registered (pinned, device-mapped) host memory over PCIe and
+// written to its packed place in the slice's HBM buffer.  One workgroup per
+// segment (grid-stride); 16-B accesses when both ends are 16-B aligned
+// (cache pages are 4 KiB aligned, md5_submit.c packs chunks 16-B aligned),
+// bytes otherwise.
+// ---------------------------------------------------------------------------
+struct GatherSeg {
+  uint64_t src, dst;
+  uint32_t len, pad;
+};
+
+__global__ void __launch_bounds__(256)
+gather_segments(const GatherSeg* __restrict__ segs, uint64_t nseg, uint8_t* __restrict__ dst) {
+  for (uint64_t k = blockIdx.x; k < nseg; k += gridDim.x) {
+    const GatherSeg g = segs[k];
+    const uint8_t* src = reinterpret_cast<const uint8_t*>(g.src);
+    uint8_t* d = dst + g.dst;
+    uint32_t head = 0;
+    if (((g.src | (uintptr_t)d) & 15u) == 0) {
+      const uint32_t n16 = g.len >> 4;
+      const uint4* s16 = reinterpret_cast<const uint4*>(src);
+      uint4* d16 = reinterpret_cast<uint4*>(d);
+      for (uint32_t j = threadIdx.x; j < n16; j += blockDim.x) d16[j] = s16[j];
+      head = n16 << 4;
+    }
+    for (uint32_t j = head + threadIdx.x; j < g.len; j += blockDim.x) d[j] = src[j];
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Synthetic data: 32-bit word i of the buffer = mix32(seed, i) (a splitmix64
 // finaliser).  tests/gen.py has the numpy mirror.
 // ---------------------------------------------------------------------------

@@ -32,6 +32,7 @@ template __global__ void crc32_fast<true>(const uint8_t*, const uint64_t*, const
 #include <string.h>
 
 #include "../../include/md5hip.h"
+#include "md5_internal.h"
 
 using namespace md5hip;
 
@@ -274,6 +275,16 @@ int crc32hip_desc(const void* d_base, const uint64_t* d_offsets, const uint32_t*
                        (const uint8_t*)d_base, d_offsets, d_lens, d_order, n, (uint64_t)0, 0u,
                        d_crcs);
   }
+  return launched();
+}
+
+int md5hip_gather_launch(const struct md5hip_seg* d_segs, uint64_t nseg, unsigned char* d_dst,
+                         void* stream) {
+  static_assert(sizeof(md5hip_seg) == sizeof(GatherSeg), "segment layout");
+  if (nseg == 0) return 0;
+  const uint64_t g = nseg < 65536 ? nseg : 65536;
+  hipLaunchKernelGGL(gather_segments, dim3((uint32_t)g), dim3(256), 0, (hipStream_t)stream,
+                     reinterpret_cast<const GatherSeg*>(d_segs), nseg, d_dst);
   return launched();
 }
 

@@ -99,6 +99,16 @@ int md5hip_pool_set_digest(md5hip_pool *p, int kind, uint32_t fastcrc)
     return rc;
 }
 
+int md5hip_pool_set_gather(md5hip_pool *p, int mode)
+{
+    if (!p) return -EINVAL;
+    pthread_mutex_lock(&p->lock);
+    int rc = 0;
+    for (uint32_t g = 0; g < p->ndev && rc == 0; g++) rc = md5hip_batcher_set_gather(p->b[g], mode);
+    pthread_mutex_unlock(&p->lock);
+    return rc;
+}
+
 /* One device's share of a call. */
 enum job_kind { JOB_PTRS, JOB_IOV, JOB_FIXED };
 struct job {

@@ -13,6 +13,7 @@
  * chunk alone exceeds the slot's staging capacity.
  */
 #include <errno.h>
+#include <pthread.h>
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
@@ -20,6 +21,92 @@
 #include <hip/hip_runtime_api.h>
 
 #include "../../include/md5hip.h"
+#include "md5_internal.h"
+
+/* ------------------------------------------------------------------------
+ * Registered host ranges (zero-copy input).  netcache allocates its cache
+ * pages in 4 KiB-aligned bulks (bc_mgr.c:1260-1290); a bulk registered here
+ * is pinned and mapped for every device, so the batcher can let the device
+ * (or the DMA engine) pull the pages directly instead of memcpy'ing them into
+ * the pinned staging slice on the host.
+ * ------------------------------------------------------------------------ */
+#define REG_MAXDEV 16
+struct reg_range {
+    uintptr_t lo, hi;
+    intptr_t delta[REG_MAXDEV];       /* device-visible address - host address */
+};
+static struct reg_range *g_reg;
+static size_t g_nreg, g_capreg;
+static pthread_rwlock_t g_reg_lock = PTHREAD_RWLOCK_INITIALIZER;
+
+/* index of the range containing [p, p+len), or -1 (caller holds the lock) */
+static long reg_find(uintptr_t p, uint64_t len)
+{
+    size_t lo = 0, hi = g_nreg;
+    while (lo < hi) {
+        const size_t mid = (lo + hi) / 2;
+        if (g_reg[mid].hi <= p) lo = mid + 1;
+        else hi = mid;
+    }
+    if (lo < g_nreg && g_reg[lo].lo <= p && p + len <= g_reg[lo].hi) return (long)lo;
+    return -1;
+}
+
+int md5hip_host_register(void *base, uint64_t bytes)
+{
+    if (!base || bytes == 0) return -EINVAL;
+    const uintptr_t lo = (uintptr_t)base, hi = lo + bytes;
+    int ndev = 0, cur = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return -ENODEV;
+    if (ndev > REG_MAXDEV) ndev = REG_MAXDEV;
+    pthread_rwlock_wrlock(&g_reg_lock);
+    int rc = 0;
+    size_t at = 0;
+    while (at < g_nreg && g_reg[at].hi <= lo) at++;
+    if (at < g_nreg && g_reg[at].lo < hi) { rc = -EEXIST; goto out; }     /* overlap */
+    if (g_nreg == g_capreg) {
+        size_t cap = g_capreg ? 2 * g_capreg : 64;
+        struct reg_range *r = realloc(g_reg, cap * sizeof *r);
+        if (!r) { rc = -ENOMEM; goto out; }
+        g_reg = r;
+        g_capreg = cap;
+    }
+    if (hipHostRegister(base, bytes, hipHostRegisterPortable | hipHostRegisterMapped) != hipSuccess) {
+        rc = -ENODEV;
+        goto out;
+    }
+    struct reg_range r = {lo, hi, {0}};
+    (void)hipGetDevice(&cur);
+    for (int d = 0; d < ndev; d++) {
+        void *dp = NULL;
+        if (hipSetDevice(d) == hipSuccess && hipHostGetDevicePointer(&dp, base, 0) == hipSuccess)
+            r.delta[d] = (intptr_t)((uintptr_t)dp - lo);
+    }
+    (void)hipSetDevice(cur);
+    memmove(&g_reg[at + 1], &g_reg[at], (g_nreg - at) * sizeof *g_reg);
+    g_reg[at] = r;
+    g_nreg++;
+out:
+    pthread_rwlock_unlock(&g_reg_lock);
+    return rc;
+}
+
+int md5hip_host_unregister(void *base)
+{
+    if (!base) return -EINVAL;
+    pthread_rwlock_wrlock(&g_reg_lock);
+    int rc = -ENOENT;
+    for (size_t k = 0; k < g_nreg; k++) {
+        if (g_reg[k].lo == (uintptr_t)base) {
+            rc = hipHostUnregister(base) == hipSuccess ? 0 : -EIO;
+            memmove(&g_reg[k], &g_reg[k + 1], (g_nreg - k - 1) * sizeof *g_reg);
+            g_nreg--;
+            break;
+        }
+    }
+    pthread_rwlock_unlock(&g_reg_lock);
+    return rc;
+}
 
 struct slot {
     hipStream_t stream;
@@ -29,6 +116,9 @@ struct slot {
     uint32_t *h_len, *d_len;
     uint32_t *h_ord, *d_ord;
     unsigned char *h_dig, *d_dig;     /* 16 * maxn */
+    struct md5hip_seg *h_seg, *d_seg; /* zero-copy gather table, `segcap` entries */
+    void **b_dst, **b_src;            /* DMA-batch gather arrays (plain host memory) */
+    size_t *b_len;
     unsigned char *user_dig;          /* where this slot's digests go (NULL = idle) */
     uint64_t ndig;
     uint32_t dsz;
@@ -43,6 +133,8 @@ struct md5hip_batcher {
     uint32_t nslots;
     uint64_t cap;      /* staging bytes per slot */
     uint64_t maxn;     /* chunks per slot */
+    uint64_t segcap;   /* gather segments per slot (zero-copy modes) */
+    int gather;        /* enum md5hip_gather_mode */
     struct slot *s;
 };
 
@@ -71,6 +163,8 @@ void md5hip_batcher_destroy(md5hip_batcher *b)
         hipHostFree(sl->h_ord); hipHostFree(sl->h_dig);
         hipFree(sl->d_data); hipFree(sl->d_off); hipFree(sl->d_len);
         hipFree(sl->d_ord); hipFree(sl->d_dig);
+        hipHostFree(sl->h_seg); hipFree(sl->d_seg);
+        free(sl->b_dst); free(sl->b_src); free(sl->b_len);
     }
     free(b->s);
     free(b);
@@ -94,6 +188,8 @@ int md5hip_batcher_create(int device, uint64_t slice_bytes, uint32_t nslots, md5
     b->nslots = nslots;
     b->cap = slice_bytes;
     b->maxn = slice_bytes / 64 < 4096 ? 4096 : slice_bytes / 64;
+    b->segcap = slice_bytes / 1024 < 4096 ? 4096 : slice_bytes / 1024;
+    b->gather = MD5HIP_GATHER_HOST;
     b->s = calloc(nslots, sizeof *b->s);
     if (!b->s) { free(b); return -ENOMEM; }
     for (uint32_t k = 0; k < nslots; k++) {
@@ -110,6 +206,12 @@ int md5hip_batcher_create(int device, uint64_t slice_bytes, uint32_t nslots, md5
         CK(hipMalloc((void **)&sl->d_len, 4 * b->maxn));
         CK(hipMalloc((void **)&sl->d_ord, 4 * b->maxn));
         CK(hipMalloc((void **)&sl->d_dig, 16 * b->maxn));
+        CK(hipHostMalloc((void **)&sl->h_seg, sizeof(struct md5hip_seg) * b->segcap, hipHostMallocDefault));
+        CK(hipMalloc((void **)&sl->d_seg, sizeof(struct md5hip_seg) * b->segcap));
+        sl->b_dst = malloc(sizeof(void *) * b->segcap);
+        sl->b_src = malloc(sizeof(void *) * b->segcap);
+        sl->b_len = malloc(sizeof(size_t) * b->segcap);
+        if (!sl->b_dst || !sl->b_src || !sl->b_len) { rc = -ENOMEM; goto fail; }
     }
     *out = b;
     return 0;
@@ -149,17 +251,41 @@ int md5hip_batcher_get_digest(const md5hip_batcher *b, int *kind, uint32_t *fast
     return 0;
 }
 
-/* Enqueue slot `sl` holding `n` chunks, `bytes` staged bytes. */
+int md5hip_batcher_set_gather(md5hip_batcher *b, int mode)
+{
+    if (!b || mode < MD5HIP_GATHER_HOST || mode > MD5HIP_GATHER_DMA) return -EINVAL;
+    b->gather = mode;
+    return 0;
+}
+
+/* Enqueue slot `sl` holding `n` chunks, `bytes` packed bytes.  nseg == 0: the
+ * bytes are in the pinned staging buffer (one H2D copy); nseg > 0: they are
+ * pulled from registered host memory by the gather table (zero-copy modes). */
 static int slot_launch(const md5hip_batcher *b, struct slot *sl, uint64_t n, uint64_t bytes,
-                       unsigned char *user_dig)
+                       uint64_t nseg, unsigned char *user_dig)
 {
     int rc;
     if (md5hip_plan_order(sl->h_len, n, sl->h_ord) != 0) return -EINVAL;
-    if (hipMemcpyAsync(sl->d_data, sl->h_data, bytes, hipMemcpyHostToDevice, sl->stream) ||
-        hipMemcpyAsync(sl->d_off, sl->h_off, 8 * n, hipMemcpyHostToDevice, sl->stream) ||
+    if (hipMemcpyAsync(sl->d_off, sl->h_off, 8 * n, hipMemcpyHostToDevice, sl->stream) ||
         hipMemcpyAsync(sl->d_len, sl->h_len, 4 * n, hipMemcpyHostToDevice, sl->stream) ||
         hipMemcpyAsync(sl->d_ord, sl->h_ord, 4 * n, hipMemcpyHostToDevice, sl->stream))
         return -EIO;
+    if (nseg == 0) {
+        if (hipMemcpyAsync(sl->d_data, sl->h_data, bytes, hipMemcpyHostToDevice, sl->stream))
+            return -EIO;
+    } else if (b->gather == MD5HIP_GATHER_DEVICE) {
+        if (hipMemcpyAsync(sl->d_seg, sl->h_seg, sizeof(struct md5hip_seg) * nseg,
+                           hipMemcpyHostToDevice, sl->stream))
+            return -EIO;
+        if ((rc = md5hip_gather_launch(sl->d_seg, nseg, sl->d_data, sl->stream))) return rc;
+    } else {
+        /* one async copy per segment (hipMemcpyBatchAsync is newer than the
+         * HIP runtime torch ships, which this library shares) */
+        for (uint64_t q = 0; q < nseg; q++)
+            if (hipMemcpyAsync(sl->b_dst[q], sl->b_src[q], sl->b_len[q], hipMemcpyHostToDevice,
+                               sl->stream) != hipSuccess)
+                return -EIO;
+    }
     if (b->kind == MD5HIP_DIGEST_CRC32)
         rc = crc32hip_desc(sl->d_data, sl->d_off, sl->d_len, sl->d_ord, n, b->fastcrc,
                            (uint32_t *)sl->d_dig, sl->stream);
@@ -194,6 +320,35 @@ static uint64_t src_len(const struct chunk_src *s, uint64_t i)
     return L;
 }
 
+static uint64_t src_nseg(const struct chunk_src *s, uint64_t i)
+{
+    return s->ptrs ? 1 : s->seg_first[i + 1] - s->seg_first[i];
+}
+
+static void src_seg(const struct chunk_src *s, uint64_t i, uint64_t k, const void **base,
+                    uint32_t *len)
+{
+    if (s->ptrs) { *base = s->ptrs[i]; *len = s->lens[i]; return; }
+    *base = s->segs[s->seg_first[i] + k].base;
+    *len = s->segs[s->seg_first[i] + k].len;
+}
+
+/* Every non-empty segment of the call in registered memory? */
+static int src_registered(const struct chunk_src *s, uint64_t n)
+{
+    int ok = 1;
+    pthread_rwlock_rdlock(&g_reg_lock);
+    for (uint64_t i = 0; i < n && ok; i++)
+        for (uint64_t k = 0; k < src_nseg(s, i) && ok; k++) {
+            const void *p;
+            uint32_t L;
+            src_seg(s, i, k, &p, &L);
+            if (L && reg_find((uintptr_t)p, L) < 0) ok = 0;
+        }
+    pthread_rwlock_unlock(&g_reg_lock);
+    return ok;
+}
+
 static void src_copy(const struct chunk_src *s, uint64_t i, unsigned char *dst)
 {
     if (s->ptrs) {
@@ -215,25 +370,53 @@ static int submit_gather(md5hip_batcher *b, const struct chunk_src *src, uint64_
         if ((L + 15) / 16 * 16 > b->cap) return -E2BIG;
     }
     if (hipSetDevice(b->device) != hipSuccess) return -ENODEV;
+    int zc = b->gather != MD5HIP_GATHER_HOST && src_registered(src, n);
+    if (zc)
+        for (uint64_t i = 0; i < n; i++)
+            if (src_nseg(src, i) > b->segcap) zc = 0;   /* a chunk too fragmented for one table */
+    const int dev = b->device < REG_MAXDEV ? b->device : 0;
     int rc = 0;
     uint32_t k = 0;
     uint64_t i = 0;
     while (i < n) {
         struct slot *sl = &b->s[k];
         if ((rc = slot_retire(sl))) return rc;
-        uint64_t used = 0, m = 0, first = i;
+        uint64_t used = 0, m = 0, first = i, nseg = 0;
+        if (zc) pthread_rwlock_rdlock(&g_reg_lock);
         while (i < n && m < b->maxn) {
             const uint64_t L = src_len(src, i);
             const uint64_t sz = (L + 15) & ~15ull;   /* 16-B aligned packing */
             if (used + sz > b->cap) break;
-            src_copy(src, i, sl->h_data + used);
+            if (zc) {
+                const uint64_t ns = src_nseg(src, i);
+                if (nseg + ns > b->segcap) break;
+                uint64_t at = used;
+                for (uint64_t q = 0; q < ns; q++) {
+                    const void *p;
+                    uint32_t len;
+                    src_seg(src, i, q, &p, &len);
+                    if (!len) continue;
+                    const long r = reg_find((uintptr_t)p, len);
+                    sl->h_seg[nseg] = (struct md5hip_seg){
+                        (uint64_t)((uintptr_t)p + g_reg[r].delta[dev]), at, len, 0};
+                    sl->b_dst[nseg] = sl->d_data + at;
+                    sl->b_src[nseg] = (void *)p;
+                    sl->b_len[nseg] = len;
+                    nseg++;
+                    at += len;
+                }
+            } else {
+                src_copy(src, i, sl->h_data + used);
+            }
             sl->h_off[m] = used;
             sl->h_len[m] = (uint32_t)L;
             used += sz;
             m++;
             i++;
         }
-        if ((rc = slot_launch(b, sl, m, used ? used : 16, digests + (size_t)b->dsz * first)))
+        if (zc) pthread_rwlock_unlock(&g_reg_lock);
+        if ((rc = slot_launch(b, sl, m, used ? used : 16, zc ? nseg : 0,
+                              digests + (size_t)b->dsz * first)))
             return rc;
         k = (k + 1) % b->nslots;
     }

@@ -222,7 +222,9 @@ class Batcher:
     """Host-memory batched submit (include/md5hip.h md5hip_batcher_*)."""
 
     MD5, CRC32 = 0, 1
-    _fn = dict(set_digest="md5hip_batcher_set_digest", destroy="md5hip_batcher_destroy",
+    GATHER_HOST, GATHER_DEVICE, GATHER_DMA = 0, 1, 2
+    _fn = dict(set_digest="md5hip_batcher_set_digest", set_gather="md5hip_batcher_set_gather",
+               destroy="md5hip_batcher_destroy",
                submit="md5_batch_submit", submit_iov="md5_batch_submit_iov",
                verify_iov="md5hip_batch_verify_iov", host_fixed="md5hip_batch_host_fixed")
 
@@ -242,6 +244,12 @@ class Batcher:
         """MD5 (16 B per chunk) or netcache CRC-32 (4 B, optional fastcrc window)."""
         check(*self._call("set_digest", kind, fastcrc))
         self.kind, self.dsz = kind, (16 if kind == self.MD5 else 4)
+
+    def set_gather(self, mode: int):
+        """HOST (memcpy into pinned staging), DEVICE (gather kernel over PCIe)
+        or DMA (batched async copies); the last two apply to calls whose
+        segments all lie in register_host()'ed memory."""
+        check(*self._call("set_gather", mode))
 
     def _out(self, n):
         return np.empty((max(n, 1), self.dsz), dtype=np.uint8)
@@ -334,7 +342,8 @@ class Pool(Batcher):
     host thread per listed device, contiguous byte-balanced chunk ranges, no
     collective.  Same methods and results as Batcher."""
 
-    _fn = dict(set_digest="md5hip_pool_set_digest", destroy="md5hip_pool_destroy",
+    _fn = dict(set_digest="md5hip_pool_set_digest", set_gather="md5hip_pool_set_gather",
+               destroy="md5hip_pool_destroy",
                submit="md5hip_pool_submit", submit_iov="md5hip_pool_submit_iov",
                verify_iov="md5hip_pool_verify_iov", host_fixed="md5hip_pool_host_fixed")
 
@@ -350,6 +359,15 @@ class Pool(Batcher):
     @property
     def ndev(self) -> int:
         return lib().md5hip_pool_ndev(self._h)
+
+
+def register_host(arr: np.ndarray):
+    """md5hip_host_register over a numpy array's buffer (pin + device-map)."""
+    check("md5hip_host_register", lib().md5hip_host_register(arr.ctypes.data, arr.nbytes))
+
+
+def unregister_host(arr: np.ndarray):
+    check("md5hip_host_unregister", lib().md5hip_host_unregister(arr.ctypes.data))
 
 
 def pool_plan(lens, nparts: int) -> np.ndarray:
@@ -368,4 +386,5 @@ def pool_plan(lens, nparts: int) -> np.ndarray:
 __all__ = ["MD5Context", "MD5Init", "MD5Update", "MD5Final", "MD5_DIGEST_SIZE", "MD5HipError",
            "md5", "digest_fixed", "digest_desc", "crc32_fixed", "crc32_desc", "plan_order", "fill_synthetic", "Batcher",
            "Pool", "pool_plan", "CRC_VARIANTS",
+           "register_host", "unregister_host",
            "variant_name", "resolve_variant", "VARIANTS"]

@@ -311,3 +311,58 @@ def test_huge_stride_and_large_chunks(cuda):
     assert np.array_equal(got, gen.oracle_digests(arena, offs, lens))
     got = m.crc32_desc(da, t_off, t_len).cpu().numpy().view(np.uint32)
     assert np.array_equal(got, gen.oracle_crc32_batch(arena, offs, lens))
+
+
+def test_zero_copy_gather_modes(cuda):
+    """Registered host memory (md5hip_host_register) pulled by the device
+    gather kernel or per-segment DMA instead of the host memcpy: same digests
+    as the oracle for page-list blocks with ragged, unaligned segment sizes,
+    empty blocks and CRC-32 mode; a call touching unregistered memory takes
+    the host gather; unregister works and double registration is refused."""
+    rng = np.random.default_rng(404)
+    heap = np.frombuffer(gen.xorshift_bytes(8 << 20, seed=405), np.uint8).copy()   # the "page heap"
+    other = np.frombuffer(gen.xorshift_bytes(1 << 20, seed=406), np.uint8).copy()  # not registered
+    page = 16384
+    blocks, joined = [], []
+    for b in range(60):
+        segs = []
+        for p in range(int(rng.integers(0, 6))):
+            start = int(rng.integers(0, heap.size // page)) * page
+            ln = page if rng.integers(0, 3) else int(rng.integers(1, page))     # ragged -> unaligned dst
+            segs.append(heap[start:start + ln])
+        blocks.append(segs)
+        joined.append(b"".join(x.tobytes() for x in segs))
+    lens = [len(j) for j in joined]
+    arena = np.frombuffer(b"".join(joined) + b"\0", np.uint8)
+    offs = np.cumsum([0] + lens[:-1])
+    want = gen.oracle_digests(arena, offs, lens)
+    want_crc = gen.oracle_crc32_batch(arena, offs, lens)
+    m.register_host(heap)
+    try:
+        with pytest.raises(m.MD5HipError):
+            m.register_host(heap[4096:8192])                 # overlaps
+        with m.Batcher(device=0, slice_bytes=1 << 20, nslots=2) as b:
+            for mode in (b.GATHER_HOST, b.GATHER_DEVICE, b.GATHER_DMA):
+                b.set_gather(mode)
+                b.set_digest(b.MD5)
+                assert np.array_equal(b.submit_iov(blocks), want), mode
+                flat = [x for segs in blocks for x in segs]
+                fj = [x.tobytes() for x in flat]
+                fa = np.frombuffer(b"".join(fj) + b"\0", np.uint8)
+                fo = np.cumsum([0] + [len(x) for x in fj[:-1]])
+                assert np.array_equal(b.submit(flat), gen.oracle_digests(fa, fo, [len(x) for x in fj]))
+                b.set_digest(b.CRC32)
+                assert np.array_equal(b.submit_iov(blocks), want_crc), mode
+            b.set_gather(b.GATHER_DEVICE)
+            b.set_digest(b.MD5)
+            mixed = blocks[:5] + [[other[:5000]]]            # one unregistered segment
+            got = b.submit_iov(mixed)
+            assert np.array_equal(got[:5], want[:5])
+            assert bytes(got[5]).hex() == bytes(gen.oracle_digests(other, [0], [5000])[0]).hex()
+        with m.Pool((0, 0), slice_bytes=1 << 20, nslots=2) as p:
+            p.set_gather(p.GATHER_DEVICE)
+            assert np.array_equal(p.submit_iov(blocks), want)
+    finally:
+        m.unregister_host(heap)
+    with pytest.raises(m.MD5HipError):
+        m.unregister_host(heap)
