@@ -59,6 +59,9 @@ def main():
             b.set_gather(mode)
             got = timed(name)
             assert np.array_equal(got, ref), name
+        if "--only-device" in sys.argv:
+            b.set_gather(b.GATHER_DEVICE)
+            got = timed("device_" + os.environ.get("MD5HIP_GATHER_UNROLL", "4"))
     finally:
         m.unregister_host(heap)
     # pinned H2D alone, for the roofline of this path

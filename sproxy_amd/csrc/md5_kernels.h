@@ -535,6 +535,8 @@ struct GatherSeg {
   uint32_t len, pad;
 };
 
+// U: 16-B loads in flight per thread before the stores (PCIe latency).
+template <int U>
 __global__ void __launch_bounds__(256)
 gather_segments(const GatherSeg* __restrict__ segs, uint64_t nseg, uint8_t* __restrict__ dst) {
   for (uint64_t k = blockIdx.x; k < nseg; k += gridDim.x) {
@@ -546,7 +548,15 @@ gather_segments(const GatherSeg* __restrict__ segs, uint64_t nseg, uint8_t* __re
       const uint32_t n16 = g.len >> 4;
       const uint4* s16 = reinterpret_cast<const uint4*>(src);
       uint4* d16 = reinterpret_cast<uint4*>(d);
-      for (uint32_t j = threadIdx.x; j < n16; j += blockDim.x) d16[j] = s16[j];
+      uint32_t j = threadIdx.x;
+      for (; j + (U - 1) * blockDim.x < n16; j += U * blockDim.x) {
+        uint4 v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) v[u] = s16[j + u * blockDim.x];
+#pragma unroll
+        for (int u = 0; u < U; ++u) d16[j + u * blockDim.x] = v[u];
+      }
+      for (; j < n16; j += blockDim.x) d16[j] = s16[j];
       head = n16 << 4;
     }
     for (uint32_t j = head + threadIdx.x; j < g.len; j += blockDim.x) d[j] = src[j];

@@ -283,7 +283,13 @@ int md5hip_gather_launch(const struct md5hip_seg* d_segs, uint64_t nseg, unsigne
   static_assert(sizeof(md5hip_seg) == sizeof(GatherSeg), "segment layout");
   if (nseg == 0) return 0;
   const uint64_t g = nseg < 65536 ? nseg : 65536;
-  hipLaunchKernelGGL(gather_segments, dim3((uint32_t)g), dim3(256), 0, (hipStream_t)stream,
+  static int unroll = -1;
+  if (unroll < 0) {
+    const char* e = getenv("MD5HIP_GATHER_UNROLL");   // A/B knob
+    unroll = e ? atoi(e) : 4;
+  }
+  auto fn = unroll == 1 ? gather_segments<1> : unroll == 2 ? gather_segments<2> : gather_segments<4>;
+  hipLaunchKernelGGL(fn, dim3((uint32_t)g), dim3(256), 0, (hipStream_t)stream,
                      reinterpret_cast<const GatherSeg*>(d_segs), nseg, d_dst);
   return launched();
 }
