@@ -25,11 +25,15 @@ def main():
     rng = np.random.default_rng(7)
     npages = heap_bytes // page
     nblocks = npages // per_block
-    perm = rng.permutation(npages)
+    # default: pages scattered at random over the heap; --contiguous: each
+    # block's pages adjacent (one netcache bulk per block, bc_mgr.c:1269)
+    perm = np.arange(npages) if "--contiguous" in sys.argv else rng.permutation(npages)
     blocks = [[heap[int(p) * page:(int(p) + 1) * page] for p in perm[b * per_block:(b + 1) * per_block]]
               for b in range(nblocks)]
     total = nblocks * per_block * page
-    res = {"blocks": nblocks, "pages_per_block": per_block, "bytes": total}
+    res = {"blocks": nblocks, "pages_per_block": per_block, "bytes": total,
+           "layout": "contiguous" if "--contiguous" in sys.argv else "scattered",
+           "coarse": os.environ.get("MD5HIP_REGISTER_COARSE", "0")}
     b = m.Batcher(device=0, slice_bytes=64 << 20, nslots=3)
     arr, fa, keep = b._iov(blocks)                     # build the segment list once
     out = np.empty((nblocks, 16), np.uint8)

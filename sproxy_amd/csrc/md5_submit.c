@@ -71,7 +71,10 @@ int md5hip_host_register(void *base, uint64_t bytes)
         g_reg = r;
         g_capreg = cap;
     }
-    if (hipHostRegister(base, bytes, hipHostRegisterPortable | hipHostRegisterMapped) != hipSuccess) {
+    unsigned flags = hipHostRegisterPortable | hipHostRegisterMapped;
+    const char *coarse = getenv("MD5HIP_REGISTER_COARSE");      /* A/B knob, DESIGN.md §5 */
+    if (coarse && atoi(coarse)) flags |= hipExtHostRegisterCoarseGrained;
+    if (hipHostRegister(base, bytes, flags) != hipSuccess) {
         rc = -ENODEV;
         goto out;
     }
@@ -375,6 +378,10 @@ static int submit_gather(md5hip_batcher *b, const struct chunk_src *src, uint64_
         for (uint64_t i = 0; i < n; i++)
             if (src_nseg(src, i) > b->segcap) zc = 0;   /* a chunk too fragmented for one table */
     const int dev = b->device < REG_MAXDEV ? b->device : 0;
+    /* contiguous segments are merged up to this size: the gather kernel gives
+     * each segment one workgroup (keep >= ~1000 of them per slice), a DMA copy
+     * pays a fixed cost per call (merge as far as possible) */
+    const uint64_t merge_cap = b->gather == MD5HIP_GATHER_DMA ? (1ull << 30) : (64u << 10);
     int rc = 0;
     uint32_t k = 0;
     uint64_t i = 0;
@@ -397,12 +404,19 @@ static int submit_gather(md5hip_batcher *b, const struct chunk_src *src, uint64_
                     src_seg(src, i, q, &p, &len);
                     if (!len) continue;
                     const long r = reg_find((uintptr_t)p, len);
-                    sl->h_seg[nseg] = (struct md5hip_seg){
-                        (uint64_t)((uintptr_t)p + g_reg[r].delta[dev]), at, len, 0};
-                    sl->b_dst[nseg] = sl->d_data + at;
-                    sl->b_src[nseg] = (void *)p;
-                    sl->b_len[nseg] = len;
-                    nseg++;
+                    const uint64_t dsrc = (uint64_t)((uintptr_t)p + g_reg[r].delta[dev]);
+                    struct md5hip_seg *prev = nseg ? &sl->h_seg[nseg - 1] : NULL;
+                    if (prev && prev->src + prev->len == dsrc && prev->dst + prev->len == at &&
+                        (uint64_t)prev->len + len <= merge_cap) {
+                        prev->len += len;       /* contiguous in both: one longer copy */
+                        sl->b_len[nseg - 1] += len;
+                    } else {
+                        sl->h_seg[nseg] = (struct md5hip_seg){dsrc, at, len, 0};
+                        sl->b_dst[nseg] = sl->d_data + at;
+                        sl->b_src[nseg] = (void *)p;
+                        sl->b_len[nseg] = len;
+                        nseg++;
+                    }
                     at += len;
                 }
             } else {
