@@ -166,17 +166,20 @@ int md5hip_batch_verify_iov(md5hip_batcher *b, const struct md5hip_iov *segs,
  * Zero-copy input.  md5hip_host_register pins and device-maps host memory
  * for every device (hipHostRegister, portable + mapped) -- e.g. each bulk of
  * netcache's page heap as it is allocated (bc_mgr.c:1260-1290).  A batcher
- * whose gather mode is DEVICE or DMA then skips the host memcpy into its
- * staging slice for any call whose segments all lie in registered memory:
+ * whose gather mode is not HOST then skips the host memcpy into its staging
+ * slice for any call whose segments all lie in registered memory:
  *   DEVICE  a gather kernel reads the segments over PCIe into HBM;
- *   DMA     one async DMA copy per segment.
- * Other calls (or mode HOST, the default) gather on the host as before.
+ *   DMA     one async DMA copy per run of contiguous segments;
+ *   AUTO    (default) per slice, DMA when the runs average >= 256 KiB,
+ *           else DEVICE.
+ * Other calls (or mode HOST) gather on the host into the pinned slice.
  * Ranges must not overlap (-EEXIST); unregister with the same base.
  */
 enum md5hip_gather_mode {
     MD5HIP_GATHER_HOST = 0,
     MD5HIP_GATHER_DEVICE = 1,
-    MD5HIP_GATHER_DMA = 2
+    MD5HIP_GATHER_DMA = 2,
+    MD5HIP_GATHER_AUTO = 3
 };
 int md5hip_host_register(void *base, uint64_t bytes);
 int md5hip_host_unregister(void *base);

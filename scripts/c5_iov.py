@@ -59,7 +59,7 @@ def main():
     m.register_host(heap)
     try:
         timed("host_reg")
-        for mode, name in ((b.GATHER_DEVICE, "device"), (b.GATHER_DMA, "dma")):
+        for mode, name in ((b.GATHER_DEVICE, "device"), (b.GATHER_DMA, "dma"), (b.GATHER_AUTO, "auto")):
             b.set_gather(mode)
             got = timed(name)
             assert np.array_equal(got, ref), name

@@ -71,9 +71,12 @@ int md5hip_host_register(void *base, uint64_t bytes)
         g_reg = r;
         g_capreg = cap;
     }
+    /* coarse-grained: the batcher reads a range only between the caller's
+     * writes (calls are synchronous), and DMA from coarse-grained pages runs
+     * 44 vs 34 GB/s; MD5HIP_REGISTER_COARSE=0 turns it off */
     unsigned flags = hipHostRegisterPortable | hipHostRegisterMapped;
-    const char *coarse = getenv("MD5HIP_REGISTER_COARSE");      /* A/B knob, DESIGN.md §5 */
-    if (coarse && atoi(coarse)) flags |= hipExtHostRegisterCoarseGrained;
+    const char *coarse = getenv("MD5HIP_REGISTER_COARSE");
+    if (!coarse || atoi(coarse)) flags |= hipExtHostRegisterCoarseGrained;
     if (hipHostRegister(base, bytes, flags) != hipSuccess) {
         rc = -ENODEV;
         goto out;
@@ -192,7 +195,7 @@ int md5hip_batcher_create(int device, uint64_t slice_bytes, uint32_t nslots, md5
     b->cap = slice_bytes;
     b->maxn = slice_bytes / 64 < 4096 ? 4096 : slice_bytes / 64;
     b->segcap = slice_bytes / 1024 < 4096 ? 4096 : slice_bytes / 1024;
-    b->gather = MD5HIP_GATHER_HOST;
+    b->gather = MD5HIP_GATHER_AUTO;
     b->s = calloc(nslots, sizeof *b->s);
     if (!b->s) { free(b); return -ENOMEM; }
     for (uint32_t k = 0; k < nslots; k++) {
@@ -256,7 +259,7 @@ int md5hip_batcher_get_digest(const md5hip_batcher *b, int *kind, uint32_t *fast
 
 int md5hip_batcher_set_gather(md5hip_batcher *b, int mode)
 {
-    if (!b || mode < MD5HIP_GATHER_HOST || mode > MD5HIP_GATHER_DMA) return -EINVAL;
+    if (!b || mode < MD5HIP_GATHER_HOST || mode > MD5HIP_GATHER_AUTO) return -EINVAL;
     b->gather = mode;
     return 0;
 }
@@ -265,7 +268,7 @@ int md5hip_batcher_set_gather(md5hip_batcher *b, int mode)
  * bytes are in the pinned staging buffer (one H2D copy); nseg > 0: they are
  * pulled from registered host memory by the gather table (zero-copy modes). */
 static int slot_launch(const md5hip_batcher *b, struct slot *sl, uint64_t n, uint64_t bytes,
-                       uint64_t nseg, unsigned char *user_dig)
+                       uint64_t nseg, uint64_t ndma, unsigned char *user_dig)
 {
     int rc;
     if (md5hip_plan_order(sl->h_len, n, sl->h_ord) != 0) return -EINVAL;
@@ -273,10 +276,15 @@ static int slot_launch(const md5hip_batcher *b, struct slot *sl, uint64_t n, uin
         hipMemcpyAsync(sl->d_len, sl->h_len, 4 * n, hipMemcpyHostToDevice, sl->stream) ||
         hipMemcpyAsync(sl->d_ord, sl->h_ord, 4 * n, hipMemcpyHostToDevice, sl->stream))
         return -EIO;
+    int mode = b->gather;
+    if (mode == MD5HIP_GATHER_AUTO)
+        /* measured: per-copy DMA beats the PCIe-reading gather
+         * kernel (~32 GB/s) once copies average more than ~192 KiB */
+        mode = ndma * (256u << 10) <= bytes ? MD5HIP_GATHER_DMA : MD5HIP_GATHER_DEVICE;
     if (nseg == 0) {
         if (hipMemcpyAsync(sl->d_data, sl->h_data, bytes, hipMemcpyHostToDevice, sl->stream))
             return -EIO;
-    } else if (b->gather == MD5HIP_GATHER_DEVICE) {
+    } else if (mode == MD5HIP_GATHER_DEVICE) {
         if (hipMemcpyAsync(sl->d_seg, sl->h_seg, sizeof(struct md5hip_seg) * nseg,
                            hipMemcpyHostToDevice, sl->stream))
             return -EIO;
@@ -284,7 +292,7 @@ static int slot_launch(const md5hip_batcher *b, struct slot *sl, uint64_t n, uin
     } else {
         /* one async copy per segment (hipMemcpyBatchAsync is newer than the
          * HIP runtime torch ships, which this library shares) */
-        for (uint64_t q = 0; q < nseg; q++)
+        for (uint64_t q = 0; q < ndma; q++)
             if (hipMemcpyAsync(sl->b_dst[q], sl->b_src[q], sl->b_len[q], hipMemcpyHostToDevice,
                                sl->stream) != hipSuccess)
                 return -EIO;
@@ -378,17 +386,13 @@ static int submit_gather(md5hip_batcher *b, const struct chunk_src *src, uint64_
         for (uint64_t i = 0; i < n; i++)
             if (src_nseg(src, i) > b->segcap) zc = 0;   /* a chunk too fragmented for one table */
     const int dev = b->device < REG_MAXDEV ? b->device : 0;
-    /* contiguous segments are merged up to this size: the gather kernel gives
-     * each segment one workgroup (keep >= ~1000 of them per slice), a DMA copy
-     * pays a fixed cost per call (merge as far as possible) */
-    const uint64_t merge_cap = b->gather == MD5HIP_GATHER_DMA ? (1ull << 30) : (64u << 10);
     int rc = 0;
     uint32_t k = 0;
     uint64_t i = 0;
     while (i < n) {
         struct slot *sl = &b->s[k];
         if ((rc = slot_retire(sl))) return rc;
-        uint64_t used = 0, m = 0, first = i, nseg = 0;
+        uint64_t used = 0, m = 0, first = i, nseg = 0, ndma = 0;
         if (zc) pthread_rwlock_rdlock(&g_reg_lock);
         while (i < n && m < b->maxn) {
             const uint64_t L = src_len(src, i);
@@ -405,17 +409,25 @@ static int submit_gather(md5hip_batcher *b, const struct chunk_src *src, uint64_
                     if (!len) continue;
                     const long r = reg_find((uintptr_t)p, len);
                     const uint64_t dsrc = (uint64_t)((uintptr_t)p + g_reg[r].delta[dev]);
+                    /* device table: contiguous pieces merged up to 64 KiB, so
+                     * a slice keeps >= ~1000 workgroups of gather work */
                     struct md5hip_seg *prev = nseg ? &sl->h_seg[nseg - 1] : NULL;
                     if (prev && prev->src + prev->len == dsrc && prev->dst + prev->len == at &&
-                        (uint64_t)prev->len + len <= merge_cap) {
-                        prev->len += len;       /* contiguous in both: one longer copy */
-                        sl->b_len[nseg - 1] += len;
+                        (uint64_t)prev->len + len <= (64u << 10)) {
+                        prev->len += len;
                     } else {
-                        sl->h_seg[nseg] = (struct md5hip_seg){dsrc, at, len, 0};
-                        sl->b_dst[nseg] = sl->d_data + at;
-                        sl->b_src[nseg] = (void *)p;
-                        sl->b_len[nseg] = len;
-                        nseg++;
+                        sl->h_seg[nseg++] = (struct md5hip_seg){dsrc, at, len, 0};
+                    }
+                    /* DMA list: merged without limit (a copy has a fixed cost) */
+                    if (ndma && (const unsigned char *)sl->b_src[ndma - 1] + sl->b_len[ndma - 1] ==
+                                    (const unsigned char *)p &&
+                        sl->b_dst[ndma - 1] == sl->d_data + at - sl->b_len[ndma - 1]) {
+                        sl->b_len[ndma - 1] += len;
+                    } else {
+                        sl->b_dst[ndma] = sl->d_data + at;
+                        sl->b_src[ndma] = (void *)p;
+                        sl->b_len[ndma] = len;
+                        ndma++;
                     }
                     at += len;
                 }
@@ -429,7 +441,7 @@ static int submit_gather(md5hip_batcher *b, const struct chunk_src *src, uint64_
             i++;
         }
         if (zc) pthread_rwlock_unlock(&g_reg_lock);
-        if ((rc = slot_launch(b, sl, m, used ? used : 16, zc ? nseg : 0,
+        if ((rc = slot_launch(b, sl, m, used ? used : 16, zc ? nseg : 0, ndma,
                               digests + (size_t)b->dsz * first)))
             return rc;
         k = (k + 1) % b->nslots;

@@ -222,7 +222,7 @@ class Batcher:
     """Host-memory batched submit (include/md5hip.h md5hip_batcher_*)."""
 
     MD5, CRC32 = 0, 1
-    GATHER_HOST, GATHER_DEVICE, GATHER_DMA = 0, 1, 2
+    GATHER_HOST, GATHER_DEVICE, GATHER_DMA, GATHER_AUTO = 0, 1, 2, 3
     _fn = dict(set_digest="md5hip_batcher_set_digest", set_gather="md5hip_batcher_set_gather",
                destroy="md5hip_batcher_destroy",
                submit="md5_batch_submit", submit_iov="md5_batch_submit_iov",

@@ -342,7 +342,7 @@ def test_zero_copy_gather_modes(cuda):
         with pytest.raises(m.MD5HipError):
             m.register_host(heap[4096:8192])                 # overlaps
         with m.Batcher(device=0, slice_bytes=1 << 20, nslots=2) as b:
-            for mode in (b.GATHER_HOST, b.GATHER_DEVICE, b.GATHER_DMA):
+            for mode in (b.GATHER_HOST, b.GATHER_DEVICE, b.GATHER_DMA, b.GATHER_AUTO):
                 b.set_gather(mode)
                 b.set_digest(b.MD5)
                 assert np.array_equal(b.submit_iov(blocks), want), mode
