@@ -20,7 +20,15 @@ from sproxy_amd import md5 as m  # noqa: E402
 def main():
     page, per_block = 16384, 16
     heap_bytes = 2 << 30
-    heap = np.empty(heap_bytes, np.uint8)
+    if "--huge" in sys.argv:
+        # 2 MiB transparent huge pages behind the heap (fewer IOMMU/GPUVM
+        # translations for the device and the DMA engine)
+        import mmap
+        mm = mmap.mmap(-1, heap_bytes, flags=mmap.MAP_PRIVATE | mmap.MAP_ANONYMOUS)
+        mm.madvise(mmap.MADV_HUGEPAGE)
+        heap = np.frombuffer(mm, np.uint8)
+    else:
+        heap = np.empty(heap_bytes, np.uint8)
     heap[::4096] = 1                                   # touch every page
     rng = np.random.default_rng(7)
     npages = heap_bytes // page
@@ -33,7 +41,8 @@ def main():
     total = nblocks * per_block * page
     res = {"blocks": nblocks, "pages_per_block": per_block, "bytes": total,
            "layout": "contiguous" if "--contiguous" in sys.argv else "scattered",
-           "coarse": os.environ.get("MD5HIP_REGISTER_COARSE", "0")}
+           "coarse": os.environ.get("MD5HIP_REGISTER_COARSE", "default(1)"),
+           "huge_pages": "--huge" in sys.argv}
     b = m.Batcher(device=0, slice_bytes=64 << 20, nslots=3)
     arr, fa, keep = b._iov(blocks)                     # build the segment list once
     out = np.empty((nblocks, 16), np.uint8)
