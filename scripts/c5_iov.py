@@ -17,8 +17,13 @@ sys.path.insert(0, REPO)
 from sproxy_amd import md5 as m  # noqa: E402
 
 
+def _arg(name, default):
+    return int(sys.argv[sys.argv.index(name) + 1]) if name in sys.argv else default
+
+
 def main():
-    page, per_block = 16384, 16
+    page, per_block = 16384, _arg("--pages", 16)
+    slots, slice_mib = _arg("--slots", 3), _arg("--slice-mib", 64)
     heap_bytes = 2 << 30
     if "--huge" in sys.argv:
         # 2 MiB transparent huge pages behind the heap (fewer IOMMU/GPUVM
@@ -43,7 +48,8 @@ def main():
            "layout": "contiguous" if "--contiguous" in sys.argv else "scattered",
            "coarse": os.environ.get("MD5HIP_REGISTER_COARSE", "default(1)"),
            "huge_pages": "--huge" in sys.argv}
-    b = m.Batcher(device=0, slice_bytes=64 << 20, nslots=3)
+    b = m.Batcher(device=0, slice_bytes=slice_mib << 20, nslots=slots)
+    res.update(slots=slots, slice_mib=slice_mib)
     arr, fa, keep = b._iov(blocks)                     # build the segment list once
     out = np.empty((nblocks, 16), np.uint8)
     lib = m.lib()
