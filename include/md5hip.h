@@ -118,6 +118,9 @@ int md5hip_fill_synthetic(void *d_dst, uint64_t nbytes, uint64_t seed, void *str
  * A batcher owns `nslots` pipeline slots (HIP stream + pinned staging of
  * `slice_bytes` + device buffers); slices of the batch flow
  * host gather -> H2D -> kernel -> D2H with slot k+1 overlapping slot k.
+ * slice_bytes = 0 / nslots = 0 select the defaults, 128 MiB x 4: MD5 is one
+ * serial chain per chunk, so the bytes in flight must cover the PCIe rate
+ * times one chunk's hashing time.
  * Calls are synchronous: they return once every digest is in `digests`.
  * A batcher is not thread-safe; use one per submitting thread.
  */

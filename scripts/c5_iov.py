@@ -23,7 +23,7 @@ def _arg(name, default):
 
 def main():
     page, per_block = 16384, _arg("--pages", 16)
-    slots, slice_mib = _arg("--slots", 3), _arg("--slice-mib", 64)
+    slots, slice_mib = _arg("--slots", 0), _arg("--slice-mib", 0)     # 0 = library defaults
     heap_bytes = 2 << 30
     if "--huge" in sys.argv:
         # 2 MiB transparent huge pages behind the heap (fewer IOMMU/GPUVM

@@ -181,9 +181,13 @@ int md5hip_batcher_create(int device, uint64_t slice_bytes, uint32_t nslots, md5
     int rc = 0;
     if (!out) return -EINVAL;
     *out = NULL;
-    if (nslots == 0) nslots = 3;
+    /* defaults sized for MD5's serial chains: a slice of B-byte chunks keeps
+     * slice/B lanes busy for B/110 MB/s (one chain), so the bytes in flight
+     * must cover PCIe rate x chain time -- 4 x 128 MiB reaches the H2D rate
+     * for 256 KiB blocks where 3 x 64 MiB stalls at ~34 GB/s */
+    if (nslots == 0) nslots = 4;
     if (nslots > 16) return -EINVAL;
-    if (slice_bytes == 0) slice_bytes = 64ull << 20;
+    if (slice_bytes == 0) slice_bytes = 128ull << 20;
     slice_bytes = (slice_bytes + 4095) & ~4095ull;
     if (hipSetDevice(device) != hipSuccess) return -ENODEV;
     md5hip_batcher *b = calloc(1, sizeof *b);
@@ -194,6 +198,7 @@ int md5hip_batcher_create(int device, uint64_t slice_bytes, uint32_t nslots, md5
     b->nslots = nslots;
     b->cap = slice_bytes;
     b->maxn = slice_bytes / 64 < 4096 ? 4096 : slice_bytes / 64;
+    if (b->maxn > (1u << 20)) b->maxn = 1u << 20;      /* descriptors: 32 B per chunk */
     b->segcap = slice_bytes / 1024 < 4096 ? 4096 : slice_bytes / 1024;
     b->gather = MD5HIP_GATHER_AUTO;
     b->s = calloc(nslots, sizeof *b->s);

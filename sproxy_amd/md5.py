@@ -228,8 +228,9 @@ class Batcher:
                submit="md5_batch_submit", submit_iov="md5_batch_submit_iov",
                verify_iov="md5hip_batch_verify_iov", host_fixed="md5hip_batch_host_fixed")
 
-    def __init__(self, device: int = 0, slice_bytes: int = 64 << 20, nslots: int = 3,
+    def __init__(self, device: int = 0, slice_bytes: int = 0, nslots: int = 0,
                  kind: int = 0, fastcrc: int = 0):
+        """slice_bytes / nslots 0 = the library defaults (128 MiB x 4)."""
         h = ctypes.c_void_p()
         check("md5hip_batcher_create", lib().md5hip_batcher_create(device, slice_bytes, nslots,
                                                                     ctypes.byref(h)))
@@ -347,7 +348,7 @@ class Pool(Batcher):
                submit="md5hip_pool_submit", submit_iov="md5hip_pool_submit_iov",
                verify_iov="md5hip_pool_verify_iov", host_fixed="md5hip_pool_host_fixed")
 
-    def __init__(self, devices=(0,), slice_bytes: int = 64 << 20, nslots: int = 3,
+    def __init__(self, devices=(0,), slice_bytes: int = 0, nslots: int = 0,
                  kind: int = 0, fastcrc: int = 0):
         devs = (ctypes.c_int * max(len(devices), 1))(*devices)
         h = ctypes.c_void_p()
