@@ -58,7 +58,8 @@ def main():
              "xpose1nt": prod("xpose1nt"), "xpose2nt": prod("xpose2nt"), "lds128nt": prod("lds128nt"),
              "load_xpose1": diag(6), "load_xpose2": diag(7), "crc32": crc(),
              "load_direct2p": diag(8), "load_direct4p": diag(9), "direct2p": diag(10), "direct4p": diag(11),
-             "crc_lane32u": diag(27), "crc_shared8": crc("shared8"), "crc_lane32": crc("lane32"), "crc_lane16": crc("lane16"),
+             "crc_lane32u": diag(27),
+             "occ20": diag(34), "occ16": diag(35), "occ12": diag(36), "occ8": diag(37), "crc_shared8": crc("shared8"), "crc_lane32": crc("lane32"), "crc_lane16": crc("lane16"),
              "cp0": diag(20), "cp_sc0": diag(21), "cp_nt": diag(22), "cp_sc0nt": diag(23),
              "cp_sc1": diag(24), "cp_sc1nt": diag(25), "cp_sc0sc1nt": diag(26)}
     if a.only:

@@ -13,6 +13,7 @@
 //   kind 8,9  load only, direct2 / direct4 with paired (whole-line) ring refill
 //   kind 10,11 MD5 direct2 / direct4 with paired refill
 //   kind 27   CRC-32 lane32 with the unpaired ring (out = u32 per chunk)
+//   kind 34-37 product xpose1nt at 20 / 16 / 12 / 8 waves per CU (LDS-capped)
 //   kind 28-33 serial-chain latency with 64/32/16/1 active lanes (28-31), and
 //             64/32 with the latency-form step (32,33); n = waves, len = bytes
 //   kind 100+K VALU issue-rate probes (instruction K of diag_valu_rate)
@@ -248,6 +249,18 @@ extern "C" int md5diag_run(int kind, const void* base, uint64_t n, uint32_t len,
     case 24: hipLaunchKernelGGL(diag_xpose1_cp<16>, dim3(grid), dim3(256), 0, s, b, n, len, stride, o); break;
     case 25: hipLaunchKernelGGL(diag_xpose1_cp<18>, dim3(grid), dim3(256), 0, s, b, n, len, stride, o); break;
     case 26: hipLaunchKernelGGL(diag_xpose1_cp<19>, dim3(grid), dim3(256), 0, s, b, n, len, stride, o); break;
+    case 34: case 35: case 36: case 37: {
+      // occupancy A/B of the product xpose1nt kernel: extra dynamic LDS per
+      // workgroup caps workgroups per CU (static image 32 KiB of 160 KiB):
+      // 34: +0 (5 WG = 20 waves), 35: +8 KiB (4 WG = 16 waves, 64 waves per
+      // CU = 4 whole generations), 36: +22 KiB (3 WG = 12 waves), 37: +48 KiB (2 WG)
+      const size_t extra = kind == 34 ? 0 : kind == 35 ? 8192 : kind == 36 ? 22528 : 49152;
+      if (extra > 32768)
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(md5_fixed_xpose1nt),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)extra);
+      hipLaunchKernelGGL(md5_fixed_xpose1nt, dim3(grid), dim3(256), extra, s, b, n, len, stride, o);
+      break;
+    }
     case 28: case 29: case 30: case 31: case 32: case 33: {
       // n = workgroups (64 threads, one wave each); len = bytes per chain
       const dim3 g1((uint32_t)n);
