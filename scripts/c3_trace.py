@@ -33,7 +33,7 @@ nw = (lens.size + 63) // 64
 rec = torch.zeros(4 * nw, dtype=torch.int64, device="cuda")
 st = torch.cuda.current_stream().cuda_stream
 res = {}
-for tpb in (256, 64):
+for tpb in (64,):
     for _ in range(2):
         assert D.md5diag_desc_trace(tpb, data.data_ptr(), d_off.data_ptr(), d_len.data_ptr(),
                                     order.data_ptr(), lens.size, out.data_ptr(), rec.data_ptr(), st) == 0

@@ -386,7 +386,7 @@ diag_desc_trace(const uint8_t* __restrict__ base, const uint64_t* __restrict__ o
                 const uint32_t* __restrict__ lens, const uint32_t* __restrict__ order, uint64_t n,
                 uint4* __restrict__ out, uint64_t* __restrict__ rec) {
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-  desc_body<false, Md5Hasher<true>, true, 2>(base, offs, lens, order, n, 0, 0u, out);
+  desc_body<false, Md5Hasher<true>, true, 8>(base, offs, lens, order, n, 0, 0u, out);   // product config
   const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
   if ((threadIdx.x & 63u) == 0) {
     uint32_t hw, xcc;
