@@ -66,3 +66,20 @@ for tpb in (64,):
                         "long_waves_per_simd_max": max(per_simd.values()),
                         "by_len": summary}
 print(json.dumps(res))
+
+# slow long waves: who shared their CU / SIMD, and when
+long_w = [w for w in range(nw) if wave_len[w] >= (1 << 20)]
+durs = sorted(dur[w] for w in long_w)
+detail = {"long_dur_us_quantiles": [round(float(np.quantile(durs, q)), 1) for q in (0, .1, .5, .9, .95, 1)]}
+slow = sorted(long_w, key=lambda w: -dur[w])[:6]
+fast = sorted(long_w, key=lambda w: dur[w])[:3]
+def neighbours(w):
+    same_cu = [v for v in range(nw) if v != w and key[v] == key[w]]
+    same_simd = [v for v in same_cu if simd[v] == simd[w]]
+    busy = lambda vs: round(float(sum(dur[v] for v in vs)) / 1000.0, 2)   # ms of co-resident wave time
+    return {"xcc": key[w][0], "se": key[w][1], "cu": key[w][3], "simd": int(simd[w]),
+            "dur_us": round(float(dur[w]), 1), "cu_waves": len(same_cu), "cu_busy_ms": busy(same_cu),
+            "simd_waves": len(same_simd), "simd_busy_ms": busy(same_simd)}
+detail["slowest"] = [neighbours(w) for w in slow]
+detail["fastest"] = [neighbours(w) for w in fast]
+print(json.dumps(detail))
