@@ -6,7 +6,7 @@ A "step" = one pass of the batched-MD5 kernel over the rank's whole batch
 (default 1,048,576 x 16 KiB = 16 GiB, BASELINE config C2), inputs already in
 HBM (filled on the device by md5hip_fill_synthetic, per-rank seed).
 
-    python bench.py [--gpus N --steps K --warmup W] [--config c2|c3|c5]
+    python bench.py [--gpus N --steps K --warmup W] [--config c2|c3|c5|crc]
 
 N > 1: one process per GPU (torch.distributed.run); each rank hashes its own
 shard of independent chunks (weak scaling, no data-path collective); barrier +
@@ -80,7 +80,7 @@ def cpu_model():
     return platform.processor() or "unknown"
 
 
-def cpu_baseline(reps=5):
+def cpu_baseline(reps=10):
     """Host md5.c on the C1 sample: 65,536 x 16 KiB xorshift64,
     Init/Update/Final per chunk, 1 thread, median of `reps`."""
     ref = os.path.join(REPO, "oracle", "_ref", "md5_cpu_bench")
@@ -96,6 +96,24 @@ def cpu_baseline(reps=5):
                        f"median of {reps}, 1 thread of {cpu_model()} ({os.cpu_count()} logical CPUs); "
                        f"fold {r['fold']} (expect 53a0a616)"),
             "fold_ok": r["fold"] == "53a0a616"}
+
+
+def cpu_baseline_crc(reps=7):
+    """Host netcache crc32_8bytes (crc32.c, compiled in place) per chunk on the
+    C1 sample, 1 thread, median of `reps` (fold ad5b15d5 = reference == port)."""
+    ref = os.path.join(REPO, "oracle", "_ref", "crc32_cpu_bench")
+    port = os.path.join(REPO, "oracle", "_build", "crc32_cpu_bench_port")
+    exe, kind = (ref, "reference") if os.path.exists(ref) else (port, "port")
+    if not os.path.exists(exe):
+        return None
+    out = subprocess.run([exe, "65536", "16384", str(reps), "1"], capture_output=True, text=True,
+                         timeout=600, check=True).stdout
+    r = json.loads(out.strip().splitlines()[-1])
+    return {"value": round(r["gib_s"], 4), "unit": "GiB/s", "cores": 1, "kind": kind,
+            "sample": (f"C1 shape: 65,536 x 16 KiB xorshift64 (1 GiB), crc32_8bytes per chunk "
+                       f"(blk_make_crc, fastcrc 0), median of {reps}, 1 thread of {cpu_model()}; "
+                       f"fold {r['fold']} (expect ad5b15d5)"),
+            "fold_ok": r["fold"] == "ad5b15d5"}
 
 
 def load_traffic(path, variant):
@@ -148,6 +166,32 @@ def run_c2(a, rank, world):
                      "alg_bytes_per_launch": int(alg_bytes)},
     }
     return res
+
+
+def run_crc(a, rank, world):
+    """§8f row 2: netcache's own block checksum (CRC-32, crc32.c) over the C2
+    shape, device-resident; the same step/timing rules as C2."""
+    L, n = a.len, a.chunks
+    data = torch.empty(n * L, dtype=torch.uint8, device="cuda")
+    m.fill_synthetic(data, seed=0x5EED0000 + rank)
+    out = torch.empty(n, dtype=torch.int32, device="cuda")
+    fn = lambda: m.crc32_fixed(data, n, L, out=out)  # noqa: E731
+    wall, dev_ms = timed_steps(fn, a.steps, a.warmup, world)
+    wall_max = max_over_ranks(wall, world, "cuda")
+    dev_ms_max = max_over_ranks(dev_ms, world, "cuda")
+    value = float(n) * L * world * a.steps / wall_max / GIB
+    alg_bytes = float(n) * (L + 4)
+    achieved = alg_bytes / (dev_ms_max * 1e-3) / 1e9
+    return {"metric": "device-resident CRC-32 (netcache blk_make_crc) GiB/s on batched 16 KiB chunks",
+            "value": round(value, 2), "unit": "GiB/s", "n_gpus": world, "steps": a.steps,
+            "warmup": a.warmup, "ms_per_step": round(wall_max / a.steps * 1e3, 4),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32",
+            "data": "synthetic (device-generated splitmix words, per-rank seed)",
+            "config": {"workload": f"{n} x {L} B chunks per GPU, device-resident, fastcrc 0",
+                       "chunks_per_gpu": n, "chunk_bytes": L, "kernel_variant": "crc32 auto"},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                         "avg_launch_ms": round(dev_ms_max, 4), "alg_bytes_per_launch": int(alg_bytes)}}
 
 
 def run_c3(a, rank, world):
@@ -243,7 +287,7 @@ def main():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=3)
-    p.add_argument("--config", default="c2", choices=["c2", "c3", "c5"])
+    p.add_argument("--config", default="c2", choices=["c2", "c3", "c5", "crc"])
     p.add_argument("--chunks", type=int, default=1 << 20, help="chunks per GPU (C2, weak scaling)")
     p.add_argument("--total-chunks", type=int, default=0,
                    help="one global batch split across ranks (C4: 16777216 on 8 GPUs)")
@@ -256,9 +300,11 @@ def main():
     p.add_argument("--c5-slice", type=int, default=64 << 20)
     a = p.parse_args()
     rank, world, _ = dist_setup(a.gpus)
-    res = {"c2": run_c2, "c3": run_c3, "c5": run_c5}[a.config](a, rank, world)
+    res = {"c2": run_c2, "c3": run_c3, "c5": run_c5, "crc": run_crc}[a.config](a, rank, world)
     if rank == 0 and world == 1 and a.config == "c2" and not a.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline()
+    if rank == 0 and world == 1 and a.config == "crc" and not a.no_cpu_baseline:
+        res["cpu_baseline"] = cpu_baseline_crc()
     if rank == 0:
         print(json.dumps(res), flush=True)
     if world > 1:

@@ -14,6 +14,12 @@
  *   _build/md5_cpu_bench_port against oracle/md5_oracle.c ("port")
  * Only bench.py's cpu_baseline leg and the tests run these binaries.
  *
+ * With -DCRC_MODE the same harness times netcache's block CRC-32 instead
+ * (crc32_8bytes per chunk, crc32.c:186-240, as blk_make_crc calls it with
+ * fastcrc = 0), 4-byte results, fold over those:
+ *   _ref/crc32_cpu_bench        reference crc32.c compiled in place
+ *   _build/crc32_cpu_bench_port oracle/crc32_oracle.c
+ *
  * usage: md5_cpu_bench N LEN REPS THREADS   -> one JSON line on stdout
  */
 #define _GNU_SOURCE
@@ -24,7 +30,17 @@
 #include <string.h>
 #include <time.h>
 
+#ifdef CRC_MODE
+#include <stddef.h>
 #ifdef USE_PORT
+uint32_t oracle_crc32(const void *, uint64_t);
+#define CRC_FN(p, n) oracle_crc32((p), (n))
+#else
+uint32_t crc32_8bytes(const void *data, size_t length);   /* reference crc32.c */
+#define CRC_FN(p, n) crc32_8bytes((p), (n))
+#endif
+#define DSZ 4
+#elif defined(USE_PORT)
 struct oracle_md5_ctx { uint32_t s[4]; uint32_t b[2]; unsigned char in[64]; };
 void oracle_md5_init(struct oracle_md5_ctx *);
 void oracle_md5_update(struct oracle_md5_ctx *, const void *, unsigned);
@@ -33,8 +49,10 @@ void oracle_md5_final(unsigned char d[16], struct oracle_md5_ctx *);
 #define H_INIT oracle_md5_init
 #define H_UPDATE oracle_md5_update
 #define H_FINAL oracle_md5_final
+#define DSZ 16
 #else
 #include "md5.h"   /* /root/reference/md5.h via -I */
+#define DSZ 16
 #define CTX struct MD5Context
 #define H_INIT MD5Init
 #define H_UPDATE MD5Update
@@ -47,10 +65,15 @@ static void *run_range(void *arg)
 {
     struct job *j = (struct job *)arg;
     for (uint64_t i = j->lo; i < j->hi; i++) {
+#ifdef CRC_MODE
+        const uint32_t c = CRC_FN(j->data + i * (uint64_t)j->len, j->len);
+        memcpy(j->dig + 4 * i, &c, 4);
+#else
         CTX c;
         H_INIT(&c);
         H_UPDATE(&c, j->data + i * (uint64_t)j->len, j->len);
         H_FINAL(j->dig + 16 * i, &c);
+#endif
     }
     return NULL;
 }
@@ -78,7 +101,7 @@ int main(int argc, char **argv)
     if (threads < 1) threads = 1;
     uint64_t bytes = n * (uint64_t)len;
     unsigned char *data = malloc(bytes + 8);
-    unsigned char *dig = malloc(16 * n);
+    unsigned char *dig = malloc(DSZ * n);
     if (!data || !dig) { fprintf(stderr, "oom\n"); return 1; }
     uint64_t s = 0x9E3779B97F4A7C15ull;
     for (uint64_t off = 0; off < bytes; off += 8) {
@@ -101,7 +124,7 @@ int main(int argc, char **argv)
         t[r] = now_s() - t0;
     }
     uint32_t fold = 0;
-    for (uint64_t i = 0; i < 16 * n; i++) fold = fold * 31u + dig[i];
+    for (uint64_t i = 0; i < DSZ * n; i++) fold = fold * 31u + dig[i];
     qsort(t, reps, sizeof(double), cmp_d);
     double med = t[reps / 2];
     printf("{\"n\": %llu, \"len\": %u, \"reps\": %d, \"threads\": %d, "
