@@ -30,6 +30,9 @@ def main():
     p.add_argument("--chunks", type=int, default=1 << 20)
     p.add_argument("--len", type=int, default=16384)
     p.add_argument("--only", default="")
+    p.add_argument("--no-rotate", action="store_true",
+                   help="keep one case order every round (default: rotate it, so no case always "
+                        "follows the same predecessor's clock state)")
     a = p.parse_args()
     n, L = a.chunks, a.len
     data = torch.empty(n * L, dtype=torch.uint8, device="cuda")
@@ -59,6 +62,9 @@ def main():
              "load_xpose1": diag(6), "load_xpose2": diag(7), "crc32": crc(),
              "load_direct2p": diag(8), "load_direct4p": diag(9), "direct2p": diag(10), "direct4p": diag(11),
              "crc_lane32u": diag(27),
+             "x64nt": diag(38), "x64": diag(39), "d64nt": diag(44), "d64": diag(45),
+             "x2pairnt": diag(46), "x2pair": diag(47),
+             "comp32": diag(40), "comp24": diag(41), "comp20": diag(42), "comp16": diag(43),
              "occ20": diag(34), "occ16": diag(35), "occ12": diag(36), "occ8": diag(37), "crc_shared8": crc("shared8"), "crc_lane32": crc("lane32"), "crc_lane16": crc("lane16"),
              "cp0": diag(20), "cp_sc0": diag(21), "cp_nt": diag(22), "cp_sc0nt": diag(23),
              "cp_sc1": diag(24), "cp_sc1nt": diag(25), "cp_sc0sc1nt": diag(26)}
@@ -68,8 +74,11 @@ def main():
     for f in cases.values():
         f()
     torch.cuda.synchronize()
-    for _ in range(a.rounds):
-        for k, f in cases.items():
+    names = list(cases)
+    for rnd in range(a.rounds):
+        order = names if a.no_rotate else names[rnd % len(names):] + names[:rnd % len(names)]
+        for k in order:
+            f = cases[k]
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(stream)
             for _ in range(a.reps):

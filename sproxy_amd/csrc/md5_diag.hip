@@ -14,6 +14,12 @@
 //   kind 10,11 MD5 direct2 / direct4 with paired refill
 //   kind 27   CRC-32 lane32 with the unpaired ring (out = u32 per chunk)
 //   kind 34-37 product xpose1nt at 20 / 16 / 12 / 8 waves per CU (LDS-capped)
+//   kind 38,39 64-B stages through VGPRs at 8 waves/SIMD (nt / default policy)
+//   kind 44,45 64-B stages by LDS-DMA, single 4 KiB image (nt / default)
+//   kind 40-43 compute only at 32 / 24 / 20 / 16 waves per CU
+//   kind 46,47 xpose2 with paired 256-B refill (nt / default)
+//   kind 48,49 xpose1nt / compute only with per-wave clock stamps after the digests
+//   kind 50   load only (xpose1nt loader, xor fold) with clock stamps
 //   kind 28-33 serial-chain latency with 64/32/16/1 active lanes (28-31), and
 //             64/32 with the latency-form step (32,33); n = waves, len = bytes
 //   kind 100+K VALU issue-rate probes (instruction K of diag_valu_rate)
@@ -93,8 +99,7 @@ diag_xpose1_cp(const uint8_t* __restrict__ base, uint64_t n, uint32_t len, uint6
 // Compute only: lane L hashes `nblocks` blocks whose words it re-reads from its
 // own 64-B LDS row every block (ds_read_b128 x4, like lds64), then the pad block.
 template <bool kLat>
-__global__ void __launch_bounds__(256)
-diag_compute(uint64_t n, uint32_t nblocks, uint4* __restrict__ out) {
+__device__ __forceinline__ void diag_compute_body(uint64_t n, uint32_t nblocks, uint4* __restrict__ out) {
   __shared__ __attribute__((aligned(16))) uint8_t rows[256 * 64];
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   uint32_t* my = reinterpret_cast<uint32_t*>(rows + threadIdx.x * 64);
@@ -114,6 +119,27 @@ diag_compute(uint64_t n, uint32_t nblocks, uint4* __restrict__ out) {
   }
   compress_pad_only(st, nblocks * 512u, 0u);
   if (i < n) out[i] = make_uint4(st.a, st.b, st.c, st.d);
+}
+
+template <bool kLat>
+__global__ void __launch_bounds__(256)
+diag_compute(uint64_t n, uint32_t nblocks, uint4* __restrict__ out) {
+  diag_compute_body<kLat>(n, nblocks, out);
+}
+
+__global__ void __launch_bounds__(256)
+diag_compute_clk(uint64_t n, uint32_t nblocks, uint4* __restrict__ out) {
+  const uint64_t t0 = __builtin_amdgcn_s_memtime();
+  const uint64_t r0 = __builtin_amdgcn_s_memrealtime();
+  diag_compute_body<false>(n, nblocks, out);
+  const uint64_t t1 = __builtin_amdgcn_s_memtime();
+  const uint64_t r1 = __builtin_amdgcn_s_memrealtime();
+  if ((threadIdx.x & 63u) == 0) {
+    uint64_t* clk = reinterpret_cast<uint64_t*>(out + n);
+    const uint64_t w = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    clk[2 * w] = t1 - t0;
+    clk[2 * w + 1] = r1 - r0;
+  }
 }
 
 // Serial-chain latency with ACT active lanes per wave (the others exit at
@@ -136,6 +162,45 @@ diag_chain(uint32_t nblocks, uint4* __restrict__ out) {
     compress_regs<kLat>(st, w);
   }
   out[i] = make_uint4(st.a, st.b, st.c, st.d);
+}
+
+// 64-B-stage candidates at 8 waves per SIMD (md5_kernels.h fixed_x64_body).
+template <int CP, bool kDma>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8)))
+diag_x64(const uint8_t* __restrict__ base, uint64_t n, uint32_t len, uint64_t stride,
+         uint4* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) uint8_t img[4 * 4096];
+  fixed_x64_body<CP, kDma>(base, n, len, stride, out, img);
+}
+
+// xpose2 with paired (256-B per chunk) refill.
+template <int CP>
+__global__ void __launch_bounds__(256)
+diag_xpose2_pair(const uint8_t* __restrict__ base, uint64_t n, uint32_t len, uint64_t stride,
+                 uint4* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) uint8_t img[4 * 8192];
+  fixed_xpose_body<2, Md5Hasher<false>, CP, true>(base, n, len, stride, out, img);
+}
+
+// In-kernel clock (MI355X_MICROARCH 'DVFS give-back' item 6): per wave,
+// (s_memtime delta, s_memrealtime delta) around the product body (kind 48) or
+// the compute-only body (kind 49), written after the n digests.
+template <class H>
+__global__ void __launch_bounds__(256)
+diag_xpose1nt_clk(const uint8_t* __restrict__ base, uint64_t n, uint32_t len, uint64_t stride,
+                  uint4* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) uint8_t img[4 * 8192];
+  const uint64_t t0 = __builtin_amdgcn_s_memtime();
+  const uint64_t r0 = __builtin_amdgcn_s_memrealtime();
+  fixed_xpose_body<1, H, 2>(base, n, len, stride, out, img);
+  const uint64_t t1 = __builtin_amdgcn_s_memtime();
+  const uint64_t r1 = __builtin_amdgcn_s_memrealtime();
+  if ((threadIdx.x & 63u) == 0) {
+    uint64_t* clk = reinterpret_cast<uint64_t*>(out + n);
+    const uint64_t w = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    clk[2 * w] = t1 - t0;
+    clk[2 * w + 1] = r1 - r0;
+  }
 }
 
 // Ideal streaming read of n*len bytes: grid-stride, 16 B per lane, consecutive
@@ -259,6 +324,22 @@ extern "C" int md5diag_run(int kind, const void* base, uint64_t n, uint32_t len,
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(md5_fixed_xpose1nt),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)extra);
       hipLaunchKernelGGL(md5_fixed_xpose1nt, dim3(grid), dim3(256), extra, s, b, n, len, stride, o);
+      break;
+    }
+    case 38: hipLaunchKernelGGL((diag_x64<2, false>), dim3(grid), dim3(256), 0, s, b, n, len, stride, o); break;
+    case 39: hipLaunchKernelGGL((diag_x64<0, false>), dim3(grid), dim3(256), 0, s, b, n, len, stride, o); break;
+    case 44: hipLaunchKernelGGL((diag_x64<2, true>), dim3(grid), dim3(256), 0, s, b, n, len, stride, o); break;
+    case 45: hipLaunchKernelGGL((diag_x64<0, true>), dim3(grid), dim3(256), 0, s, b, n, len, stride, o); break;
+    case 46: hipLaunchKernelGGL(diag_xpose2_pair<2>, dim3(grid), dim3(256), 0, s, b, n, len, stride, o); break;
+    case 47: hipLaunchKernelGGL(diag_xpose2_pair<0>, dim3(grid), dim3(256), 0, s, b, n, len, stride, o); break;
+    case 50: hipLaunchKernelGGL(diag_xpose1nt_clk<FoldHasher>, dim3(grid), dim3(256), 0, s, b, n, len, stride, o); break;
+    case 48: hipLaunchKernelGGL(diag_xpose1nt_clk<Md5Hasher<false>>, dim3(grid), dim3(256), 0, s, b, n, len, stride, o); break;
+    case 49: hipLaunchKernelGGL(diag_compute_clk, dim3(grid), dim3(256), 0, s, n, len >> 6, o); break;
+    case 40: case 41: case 42: case 43: {
+      // compute-only occupancy sweep: static 16 KiB per workgroup plus extra
+      // dynamic LDS caps workgroups per CU at 8 / 6 / 5 / 4 (32/24/20/16 waves)
+      const size_t extra = kind == 40 ? 0 : kind == 41 ? 10240 : kind == 42 ? 16384 : 24576;
+      hipLaunchKernelGGL(diag_compute<false>, dim3(grid), dim3(256), extra, s, n, len >> 6, o);
       break;
     }
     case 28: case 29: case 30: case 31: case 32: case 33: {
