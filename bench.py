@@ -36,15 +36,29 @@ METRIC = "device-resident MD5 GiB/s on batched 16 KiB chunks at 1/2/4/8 MI355X"
 GIB = float(1 << 30)
 
 
-def dist_setup(ngpus):
+COLL_DEVICE = "cuda"             # where the control-plane scalars live (cpu under gloo)
+
+
+def dist_setup(ngpus, backend="nccl"):
+    """One process per GPU.  The only collectives are a barrier and one scalar
+    MAX, so `--dist-backend gloo` (CPU) is equivalent; it lets N ranks share
+    one GPU for a rehearsal of the N > 1 path on a one-GPU box."""
+    global COLL_DEVICE
     rank, world, local = env_rank()
     if world != ngpus and world > 1:
         raise SystemExit(f"--gpus {ngpus} but WORLD_SIZE={world}")
-    torch.cuda.set_device(local)
+    ndev = torch.cuda.device_count()
+    if backend == "nccl" and world > 1 and local >= ndev:
+        raise SystemExit(f"LOCAL_RANK {local} but only {ndev} GPUs visible")
+    torch.cuda.set_device(local % ndev)
     if world > 1:
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
+            COLL_DEVICE = "cpu"
     return rank, world, local
 
 
@@ -140,8 +154,8 @@ def run_c2(a, rank, world):
     variant = m.VARIANTS[a.variant]
     fn = lambda: m.digest_fixed(data, n, L, out=out, variant=variant)  # noqa: E731
     wall, dev_ms = timed_steps(fn, a.steps, a.warmup, world)
-    wall_max = max_over_ranks(wall, world, "cuda")
-    dev_ms_max = max_over_ranks(dev_ms, world, "cuda")
+    wall_max = max_over_ranks(wall, world, COLL_DEVICE)
+    dev_ms_max = max_over_ranks(dev_ms, world, COLL_DEVICE)
     n_all = a.total_chunks if a.total_chunks else n * world
     total_bytes = float(n_all) * L * a.steps
     value = total_bytes / wall_max / GIB
@@ -177,8 +191,8 @@ def run_crc(a, rank, world):
     out = torch.empty(n, dtype=torch.int32, device="cuda")
     fn = lambda: m.crc32_fixed(data, n, L, out=out)  # noqa: E731
     wall, dev_ms = timed_steps(fn, a.steps, a.warmup, world)
-    wall_max = max_over_ranks(wall, world, "cuda")
-    dev_ms_max = max_over_ranks(dev_ms, world, "cuda")
+    wall_max = max_over_ranks(wall, world, COLL_DEVICE)
+    dev_ms_max = max_over_ranks(dev_ms, world, COLL_DEVICE)
     value = float(n) * L * world * a.steps / wall_max / GIB
     alg_bytes = float(n) * (L + 4)
     achieved = alg_bytes / (dev_ms_max * 1e-3) / 1e9
@@ -223,7 +237,7 @@ def run_c3(a, rank, world):
     out = torch.empty((lens.size, 16), dtype=torch.uint8, device="cuda")
     fn = lambda: m.digest_desc(data, d_off, d_len, d_ord, out=out)  # noqa: E731
     wall, dev_ms = timed_steps(fn, a.steps, a.warmup, world)
-    wall_max = max_over_ranks(wall, world, "cuda")
+    wall_max = max_over_ranks(wall, world, COLL_DEVICE)
     payload = float(lens.sum())
     value = payload * world * a.steps / wall_max / GIB
     # the longest chunk bounds the step: a 1 MiB chunk is 16,385 dependent
@@ -294,12 +308,14 @@ def main():
     p.add_argument("--len", type=int, default=16384)
     p.add_argument("--variant", default="auto", choices=sorted(m.VARIANTS))
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                   help="control-plane backend for N > 1 (barrier + scalar MAX only)")
     p.add_argument("--traffic", default=os.path.join(REPO, "profiles", "traffic.json"))
     p.add_argument("--c3-bytes", type=int, default=16 << 30)
     p.add_argument("--c5-chunks", type=int, default=1 << 18)
     p.add_argument("--c5-slice", type=int, default=64 << 20)
     a = p.parse_args()
-    rank, world, _ = dist_setup(a.gpus)
+    rank, world, _ = dist_setup(a.gpus, a.dist_backend)
     res = {"c2": run_c2, "c3": run_c3, "c5": run_c5, "crc": run_crc}[a.config](a, rank, world)
     if rank == 0 and world == 1 and a.config == "c2" and not a.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline()

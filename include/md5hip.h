@@ -93,7 +93,9 @@ enum crc32hip_variant {
     CRC32HIP_SHARED8 = 1,   /* slicing-by-8, one shared 8 KiB LDS table set, xpose loads */
     CRC32HIP_LANE32 = 2,    /* slicing-by-4, 32 lane-private table copies (128 KiB LDS) */
     CRC32HIP_LANE16 = 3,    /* slicing-by-4, 16 table copies (64 KiB LDS) */
-    CRC32HIP_NUM_VARIANTS = 4
+    CRC32HIP_XLANE16 = 4,   /* slicing-by-4, 16 table copies + whole-line xpose loads */
+    CRC32HIP_XPERM16 = 5,   /* as XLANE16, copies laid out for one-v_perm addressing */
+    CRC32HIP_NUM_VARIANTS = 6
 };
 int crc32hip_fixed_variant(const void *d_base, uint64_t n, uint32_t len, uint64_t stride,
                            uint32_t fastcrc, uint32_t *d_crcs, void *stream, int variant);

@@ -140,12 +140,18 @@ struct Crc32Hasher {
     tab = t;
   }
   __device__ __forceinline__ State init() { return State{0xFFFFFFFFu}; }
+  // The 8 lookups fold through three 3-input XORs (v_bitop3_b32 0x96) and one
+  // v_xor: 4 VALU instead of the 7 two-input XORs hipcc emits for a ^ chain.
   __device__ __forceinline__ uint32_t step8(uint32_t c, uint32_t one, uint32_t two) const {
     one ^= c;
-    return tab[0 * 256 + (two >> 24)] ^ tab[1 * 256 + ((two >> 16) & 0xFFu)] ^
-           tab[2 * 256 + ((two >> 8) & 0xFFu)] ^ tab[3 * 256 + (two & 0xFFu)] ^
-           tab[4 * 256 + (one >> 24)] ^ tab[5 * 256 + ((one >> 16) & 0xFFu)] ^
-           tab[6 * 256 + ((one >> 8) & 0xFFu)] ^ tab[7 * 256 + (one & 0xFFu)];
+    const uint32_t x = xor3(tab[0 * 256 + (two >> 24)], tab[1 * 256 + ((two >> 16) & 0xFFu)],
+                            tab[2 * 256 + ((two >> 8) & 0xFFu)]);
+    const uint32_t y = xor3(tab[3 * 256 + (two & 0xFFu)], tab[4 * 256 + (one >> 24)],
+                            tab[5 * 256 + ((one >> 16) & 0xFFu)]);
+    return xor3(x, tab[6 * 256 + ((one >> 8) & 0xFFu)], tab[7 * 256 + (one & 0xFFu)]) ^ y;
+  }
+  static __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
   }
   __device__ __forceinline__ void block(State& st, const uint4 (&w)[4]) {
     uint32_t c = st.c;
@@ -254,6 +260,79 @@ struct Crc32LaneHasher {
 #pragma unroll
       for (int b = 0; b < 3; ++b)      // the last 1..3 bytes, one at a time
         if (done + (uint32_t)b < r) c = look(0, (c ^ (wd >> (8 * b))) & 0xFFu) ^ (c >> 8);
+    }
+    st.c = ~c;
+  }
+  __device__ __forceinline__ void store(Out* out, uint64_t idx, const State& st) {
+    out[idx] = st.c;
+  }
+};
+
+// Slicing-by-4 over 16 lane copies laid out so ONE v_perm_b32 forms each
+// lookup address: entry e of table t, copy c at word e*64 + t*16 + c, i.e.
+// byte address (e << 8) | (t << 6) | (c << 2).  v_perm_b32 drops the index
+// byte into bits 8..15 next to the lane's (c << 2) byte, and t << 6 rides in
+// the ds_read_b32 immediate offset -- 1 VALU per lookup instead of a byte
+// extract plus a shift-or.  The price: ds_read_b32 banks on word mod 32 =
+// (t & 1) * 16 + c, so lanes l and l + 16 of a 32-lane group (same copy)
+// always share a bank: a fixed 2-way conflict, where the interleaved layout of
+// Crc32LaneHasher<16> is 1.5-way on average.  64 KiB of LDS either way.
+struct Crc32PermHasher {
+  using State = Crc32State;
+  using Out = uint32_t;
+  static constexpr int kLdsBytes = 256 * 64 * 4;
+  const uint8_t* lds;
+  uint32_t lane4;                      // (lane % 16) * 4 in byte 0
+  __device__ __forceinline__ void setup(uint8_t* l) {
+    uint32_t* t = reinterpret_cast<uint32_t*>(l);
+    for (uint32_t k = threadIdx.x; k < 256u * 64u; k += blockDim.x)
+      t[k] = kCrcTables.t[(k >> 4) & 3u][k >> 6];
+    __syncthreads();
+    lds = l;
+    lane4 = (threadIdx.x & 15u) * 4u;
+  }
+  // table t, index = byte j of x
+  template <int T, int J>
+  __device__ __forceinline__ uint32_t look(uint32_t x) const {
+    // selector bytes: 0 -> lane4 byte 0, 4 + J -> x byte J, 0x0C -> zero
+    const uint32_t addr = __builtin_amdgcn_perm(x, lane4, 0x0C0C0000u | ((4u + J) << 8));
+    return *reinterpret_cast<const uint32_t*>(lds + addr + T * 64);
+  }
+  static __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+  }
+  __device__ __forceinline__ uint32_t step4(uint32_t c, uint32_t w) const {
+    c ^= w;
+    return xor3(look<0, 3>(c), look<1, 2>(c), look<2, 1>(c)) ^ look<3, 0>(c);
+  }
+  __device__ __forceinline__ State init() { return State{0xFFFFFFFFu}; }
+  __device__ __forceinline__ void block(State& st, const uint4 (&w)[4]) {
+    uint32_t c = st.c;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      c = step4(c, w[k].x);
+      c = step4(c, w[k].y);
+      c = step4(c, w[k].z);
+      c = step4(c, w[k].w);
+    }
+    st.c = c;
+  }
+  __device__ __forceinline__ void finish(State& st, const uint8_t* tail, uint32_t r, uint64_t) {
+    uint32_t c = st.c;
+    if (r) {
+      uint32_t w[16];
+      load_tail(tail, r, w);
+#pragma unroll
+      for (int j = 0; j < 16; ++j)
+        if ((uint32_t)(4 * j + 4) <= r) c = step4(c, w[j]);
+      const uint32_t done = r & ~3u;
+      uint32_t wd = w[0];
+#pragma unroll
+      for (int j = 1; j < 16; ++j)
+        if ((uint32_t)j == (done >> 2)) wd = w[j];
+#pragma unroll
+      for (int b = 0; b < 3; ++b)      // the last 1..3 bytes, one at a time (crc32.c:236-238)
+        if (done + (uint32_t)b < r) c = look<0, 0>(c ^ (wd >> (8 * b))) ^ (c >> 8);
     }
     st.c = ~c;
   }

@@ -20,6 +20,7 @@
 //   kind 46,47 xpose2 with paired 256-B refill (nt / default)
 //   kind 48,49 xpose1nt / compute only with per-wave clock stamps after the digests
 //   kind 50   load only (xpose1nt loader, xor fold) with clock stamps
+//   kind 51   CRC-32 product body (crc32_fixed_xpose) with clock stamps
 //   kind 28-33 serial-chain latency with 64/32/16/1 active lanes (28-31), and
 //             64/32 with the latency-form step (32,33); n = waves, len = bytes
 //   kind 100+K VALU issue-rate probes (instruction K of diag_valu_rate)
@@ -203,6 +204,25 @@ diag_xpose1nt_clk(const uint8_t* __restrict__ base, uint64_t n, uint32_t len, ui
   }
 }
 
+// CRC-32 product body (crc32_fixed_xpose) with clock stamps after n*16 bytes.
+__global__ void __launch_bounds__(256)
+diag_crc_clk(const uint8_t* __restrict__ base, uint64_t n, uint32_t len, uint64_t stride,
+             uint4* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) uint8_t img[4 * 8192];
+  __shared__ __attribute__((aligned(16))) uint8_t tabs[Crc32Hasher::kLdsBytes];
+  const uint64_t t0 = __builtin_amdgcn_s_memtime();
+  const uint64_t r0 = __builtin_amdgcn_s_memrealtime();
+  fixed_xpose_body<1, Crc32Hasher, 2>(base, n, len, stride, reinterpret_cast<uint32_t*>(out), img, tabs);
+  const uint64_t t1 = __builtin_amdgcn_s_memtime();
+  const uint64_t r1 = __builtin_amdgcn_s_memrealtime();
+  if ((threadIdx.x & 63u) == 0) {
+    uint64_t* clk = reinterpret_cast<uint64_t*>(out + n);
+    const uint64_t w = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    clk[2 * w] = t1 - t0;
+    clk[2 * w + 1] = r1 - r0;
+  }
+}
+
 // Ideal streaming read of n*len bytes: grid-stride, 16 B per lane, consecutive
 // lanes consecutive addresses; xor-fold per lane.
 __global__ void __launch_bounds__(256)
@@ -332,6 +352,7 @@ extern "C" int md5diag_run(int kind, const void* base, uint64_t n, uint32_t len,
     case 45: hipLaunchKernelGGL((diag_x64<0, true>), dim3(grid), dim3(256), 0, s, b, n, len, stride, o); break;
     case 46: hipLaunchKernelGGL(diag_xpose2_pair<2>, dim3(grid), dim3(256), 0, s, b, n, len, stride, o); break;
     case 47: hipLaunchKernelGGL(diag_xpose2_pair<0>, dim3(grid), dim3(256), 0, s, b, n, len, stride, o); break;
+    case 51: hipLaunchKernelGGL(diag_crc_clk, dim3(grid), dim3(256), 0, s, b, n, len, stride, o); break;
     case 50: hipLaunchKernelGGL(diag_xpose1nt_clk<FoldHasher>, dim3(grid), dim3(256), 0, s, b, n, len, stride, o); break;
     case 48: hipLaunchKernelGGL(diag_xpose1nt_clk<Md5Hasher<false>>, dim3(grid), dim3(256), 0, s, b, n, len, stride, o); break;
     case 49: hipLaunchKernelGGL(diag_compute_clk, dim3(grid), dim3(256), 0, s, n, len >> 6, o); break;

@@ -38,6 +38,18 @@ __device__ __forceinline__ void load_block(uint4 (&r)[4], const uint4* p) {
   for (int k = 0; k < 4; ++k) r[k] = ld16(p + k);
 }
 
+// A buffer descriptor the compiler can prove wave-uniform: both address
+// halves go through readfirstlane.  Without that proof hipcc wraps every
+// buffer_load in a waterfall loop (4 v_readfirstlane + 2 v_cmp + exec juggling
+// per load; it did so in crc32_fixed_xpose, whose table setup precedes it).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc(const uint8_t* p) {
+  const uint64_t a = (uint64_t)(uintptr_t)p;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+  void* u = (void*)(uintptr_t)(((uint64_t)hi << 32) | lo);
+  return __builtin_amdgcn_make_buffer_rsrc(u, (short)0, 0x7FFFFFFF, 0x00020000);
+}
+
 // ---------------------------------------------------------------------------
 // Fixed-length, lane-direct loads.  base/stride 16-B aligned, len <= stride.
 // ---------------------------------------------------------------------------
@@ -219,8 +231,7 @@ __device__ __forceinline__ void fixed_xpose_body(const uint8_t* __restrict__ bas
   if (wave_first >= n) return;
   const uint64_t left = n - wave_first;
   const uint32_t rows = left < 64 ? (uint32_t)left : 64u;
-  const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<uint8_t*>(base + wave_first * stride), (short)0, 0x7FFFFFFF, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsrc = uniform_rsrc(base + wave_first * stride);
   uint32_t voff[8];
 #pragma unroll
   for (int r = 0; r < 8; ++r) {
@@ -322,8 +333,7 @@ __device__ __forceinline__ void fixed_x64_body(const uint8_t* __restrict__ base,
   const uint64_t left = n - wave_first;
   const uint32_t rows = left < 64 ? (uint32_t)left : 64u;
   const uint8_t* wbase = base + wave_first * stride;
-  const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<uint8_t*>(wbase), (short)0, 0x7FFFFFFF, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsrc = uniform_rsrc(wbase);
   uint32_t voff[4];
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
@@ -598,6 +608,123 @@ crc32_fixed_lane16(const uint8_t* __restrict__ base, uint64_t n, uint32_t len, u
                    uint32_t* __restrict__ out) {
   __shared__ __attribute__((aligned(16))) uint8_t tabs[Crc32LaneHasher<16>::kLdsBytes];
   crc32_fixed_lane_body<16, 4>(base, n, len, stride, out, tabs);
+}
+
+// ---------------------------------------------------------------------------
+// CRC-32 with conflict-reduced lane tables AND whole-line loads ("xlane16").
+// ds_read_b32 banks on (addr/4) mod 32 in two 32-lane groups
+// (MI355X_MICROARCH §LDS), so random lookups into one shared table set run
+// ~3.5-way conflicted: crc32_fixed_xpose holds the top clock (2.38 GHz,
+// profiles/r01_clock_probe_crc.json) and is LDS-cycle-bound.  Here
+// Crc32LaneHasher<16> (16 interleaved copies, 64 KiB) leaves two lanes of a
+// group per bank pair (1.5-way), and the xpose loader keeps whole-line loads
+// with a HALF image -- 4 KiB per wave: rows 0-31 are written and read back by
+// lanes 0-31, then rows 32-63 by lanes 32-63 -- so 16 waves' images fit beside
+// the tables (64 + 64 KiB).  One 1024-thread workgroup per CU, grid-stride
+// over 64-chunk groups, so each CU builds its tables once.
+// ---------------------------------------------------------------------------
+template <class H, int CP>
+__device__ __forceinline__ void xpose_half_group(H& h, const uint8_t* __restrict__ base,
+                                                 uint64_t n, uint32_t len, uint64_t stride,
+                                                 uint64_t wave_first,
+                                                 typename H::Out* __restrict__ out, uint8_t* img) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint64_t left = n - wave_first;
+  const uint32_t rows = left < 64 ? (uint32_t)left : 64u;
+  const __amdgpu_buffer_rsrc_t rsrc = uniform_rsrc(base + wave_first * stride);
+  uint32_t voff[8];
+#pragma unroll
+  for (int r = 0; r < 8; ++r) {
+    const uint32_t row = (uint32_t)r * 8u + (lane >> 3);
+    const uint32_t rc = row < rows ? row : rows - 1u;
+    const uint32_t part = (lane & 7u) ^ ((row >> 1) & 7u);
+    voff[r] = rc * (uint32_t)stride + part * 16u;
+  }
+  const uint32_t g = (lane >> 1) & 7u;
+  const bool lo = lane < 32u;
+  const uint8_t* myrow = img + (lane & 31u) * 128u;
+  const uint32_t nfull = len >> 6;
+  const uint32_t nstage = nfull >> 1;
+  typename H::State st = h.init();
+
+  auto load_stage = [&](u32x4 (&R)[8], uint32_t stg) __attribute__((always_inline)) {
+#pragma unroll
+    for (int r = 0; r < 8; ++r)
+      R[r] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, (int)voff[r], (int)(stg * 128u), CP);
+  };
+  auto read_row = [&](uint4 (&w)[2][4]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const u32x4 v = *reinterpret_cast<const u32x4*>(myrow + ((q ^ g) * 16));
+      w[q >> 2][q & 3] = make_uint4(v.x, v.y, v.z, v.w);
+    }
+  };
+  auto consume = [&](u32x4 (&R)[8], uint32_t next, bool refill) __attribute__((always_inline)) {
+    uint4 w[2][4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      *reinterpret_cast<u32x4*>(img + r * 1024 + lane * 16) = R[r];
+    __builtin_amdgcn_wave_barrier();
+    if (lo) read_row(w);
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int r = 4; r < 8; ++r)
+      *reinterpret_cast<u32x4*>(img + (r - 4) * 1024 + lane * 16) = R[r];
+    __builtin_amdgcn_wave_barrier();
+    if (!lo) read_row(w);
+    __builtin_amdgcn_wave_barrier();
+    if (refill) load_stage(R, next);
+    __builtin_amdgcn_sched_barrier(0);
+    h.block(st, w[0]);
+    h.block(st, w[1]);
+  };
+
+  if (nstage) {
+    const uint32_t lasts = nstage - 1;
+    u32x4 R[8];
+    load_stage(R, 0);
+    for (uint32_t stg = 0; stg < nstage; ++stg) consume(R, min(stg + 1, lasts), stg < lasts);
+  }
+  const uint64_t i = wave_first + lane;
+  const uint64_t ci = lane < rows ? i : n - 1;
+  const uint8_t* chunk = base + ci * stride;
+  if (nfull & 1u) {
+    uint4 w[4];
+    load_block(w, reinterpret_cast<const uint4*>(chunk + ((uint64_t)(nfull - 1) << 6)));
+    h.block(st, w);
+  }
+  h.finish(st, chunk + ((uint64_t)nfull << 6), len & 63u, len);
+  if (lane < rows) h.store(out, i, st);
+}
+
+template <class H>
+__device__ __forceinline__ void crc32_xlane_body(const uint8_t* __restrict__ base, uint64_t n,
+                                                 uint32_t len, uint64_t stride,
+                                                 uint32_t* __restrict__ out, uint8_t* tabs,
+                                                 uint8_t* img) {
+  H h;
+  h.setup(tabs);
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint64_t ngroups = (n + 63) / 64;
+  for (uint64_t gi = (uint64_t)blockIdx.x * 16u + wave; gi < ngroups; gi += (uint64_t)gridDim.x * 16u)
+    xpose_half_group<H, 2>(h, base, n, len, stride, gi * 64u, out, img + wave * 4096u);
+}
+
+__global__ void __launch_bounds__(1024)
+crc32_fixed_xlane16(const uint8_t* __restrict__ base, uint64_t n, uint32_t len, uint64_t stride,
+                    uint32_t* __restrict__ out) {
+  // one array, tables first: they sit at LDS address 0, so a table's base
+  // folds into the 16-bit ds_read offset instead of costing a v_or per lookup
+  __shared__ __attribute__((aligned(16))) uint8_t lds[Crc32LaneHasher<16>::kLdsBytes + 16 * 4096];
+  crc32_xlane_body<Crc32LaneHasher<16>>(base, n, len, stride, out, lds,
+                                        lds + Crc32LaneHasher<16>::kLdsBytes);
+}
+
+__global__ void __launch_bounds__(1024)
+crc32_fixed_xperm16(const uint8_t* __restrict__ base, uint64_t n, uint32_t len, uint64_t stride,
+                    uint32_t* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds[Crc32PermHasher::kLdsBytes + 16 * 4096];
+  crc32_xlane_body<Crc32PermHasher>(base, n, len, stride, out, lds, lds + Crc32PermHasher::kLdsBytes);
 }
 
 // fastcrc (blk_io.c:408-424): len <= f -> crc(all), else crc(first f bytes)

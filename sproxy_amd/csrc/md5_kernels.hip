@@ -77,7 +77,7 @@ int default_crc_variant() {
   if (v < 0) {
     const char* e = getenv("CRC32HIP_VARIANT");
     int x = e ? atoi(e) : 0;
-    v = (x > 0 && x < CRC32HIP_NUM_VARIANTS) ? x : CRC32HIP_SHARED8;  // measured best, DESIGN.md §5
+    v = (x > 0 && x < CRC32HIP_NUM_VARIANTS) ? x : CRC32HIP_XPERM16;  // measured best, DESIGN.md §5
   }
   return v;
 }
@@ -236,6 +236,16 @@ int crc32hip_fixed_variant(const void* d_base, uint64_t n, uint32_t len, uint64_
   const bool aligned = ((uintptr_t)base & 15u) == 0 && (stride & 15u) == 0;
   if (aligned && variant == CRC32HIP_LANE32) return launch_crc_lane<32>(base, n, len, stride, d_crcs, s);
   if (aligned && variant == CRC32HIP_LANE16) return launch_crc_lane<16>(base, n, len, stride, d_crcs, s);
+  if (aligned && stride < (1ull << 31) / 64 &&
+      (variant == CRC32HIP_XLANE16 || variant == CRC32HIP_XPERM16)) {
+    // one 1024-thread workgroup per CU (128 KiB LDS), grid-stride over 64-chunk groups
+    const uint64_t need = (n + kLaneBlock - 1) / kLaneBlock;
+    const uint64_t cap = (uint64_t)cu_count();
+    hipLaunchKernelGGL(variant == CRC32HIP_XLANE16 ? crc32_fixed_xlane16 : crc32_fixed_xperm16,
+                       dim3((uint32_t)(need < cap ? need : cap)), dim3(kLaneBlock), 0, s, base,
+                       n, len, stride, d_crcs);
+    return launched();
+  }
   if (aligned && stride < (1ull << 31) / 64) {
     const uint64_t g = (n + kBlock - 1) / kBlock;
     if (g > 0x7fffffffull) return -EINVAL;
