@@ -74,6 +74,17 @@ int md5hip_digest_fixed_variant(const void *d_base, uint64_t n, uint32_t len, ui
 int md5hip_digest_desc(const void *d_base, const uint64_t *d_offsets, const uint32_t *d_lens,
                        const uint32_t *d_order, uint64_t n, unsigned char *d_digests,
                        void *stream);
+/* Descriptor-batch kernels for md5hip_digest_desc_variant (A-B benches). */
+enum md5hip_desc_variant {
+    MD5HIP_DESC_AUTO = 0,   /* library's choice (env MD5HIP_DESC_VARIANT overrides) */
+    MD5HIP_DESC_LANE = 1,   /* each lane streams its own chunk (8-block register ring) */
+    MD5HIP_DESC_XPOSE = 2,  /* whole-line loads of 8 chunks x 128 B + LDS transpose;
+                               waves with an unaligned chunk fall back to LANE */
+    MD5HIP_DESC_NUM_VARIANTS = 3
+};
+int md5hip_digest_desc_variant(const void *d_base, const uint64_t *d_offsets,
+                               const uint32_t *d_lens, const uint32_t *d_order, uint64_t n,
+                               unsigned char *d_digests, void *stream, int variant);
 
 /*
  * CRC-32 block checksums -- the checksum netcache itself computes at the

@@ -63,6 +63,7 @@ def lib():
         "md5hip_digest_fixed": (i, [vp, u64, u32, u64, vp, vp]),
         "md5hip_digest_fixed_variant": (i, [vp, u64, u32, u64, vp, vp, i]),
         "md5hip_digest_desc": (i, [vp, vp, vp, vp, u64, vp, vp]),
+        "md5hip_digest_desc_variant": (i, [vp, vp, vp, vp, u64, vp, vp, i]),
         "md5hip_plan_order": (i, [vp, u64, vp]),
         "crc32hip_fixed": (i, [vp, u64, u32, u64, u32, vp, vp]),
         "crc32hip_desc": (i, [vp, vp, vp, vp, u64, u32, vp, vp]),
@@ -112,6 +113,7 @@ def lib():
 EXPORTS = ["MD5Init", "MD5Update", "MD5Final", "nc_MD5Init", "nc_MD5Update", "nc_MD5Final", "md5hip_abi_version", "md5hip_variant_name",
            "md5hip_resolve_variant",
            "md5hip_digest_fixed", "md5hip_digest_fixed_variant", "md5hip_digest_desc",
+           "md5hip_digest_desc_variant",
            "md5hip_plan_order", "md5hip_fill_synthetic", "md5hip_batcher_create",
            "crc32hip_fixed", "crc32hip_desc", "crc32hip_fixed_variant",
            "md5hip_batcher_destroy", "md5_batch_submit", "md5_batch_submit_iov",

@@ -568,6 +568,117 @@ md5_desc(const uint8_t* __restrict__ base, const uint64_t* __restrict__ offs,
 }
 
 // ---------------------------------------------------------------------------
+// Descriptor batch with whole-line loads ("desc xpose").  A netcache batch is
+// mostly full chunk_size blocks plus each object's shorter last block
+// (blk_io.c:377); lanes are ordered longest-first (md5hip_plan_order), so a
+// wave's 64 chunks have nearly equal lengths.  The wave then loads like the
+// fixed xpose kernel -- each global_load_dwordx4 wave-instruction reads 8
+// chunks x 128 B -- from per-row 64-bit addresses (chunks lie anywhere in the
+// arena), a row's stage index clamped to its own last stage, and a lane
+// compresses a stage only while it still has one.  Rows without any 128-B
+// stage re-read the wave's longest chunk (always in bounds).  A wave with a
+// chunk start that is not 16-B aligned takes the lane-direct path (desc_body).
+// One wave per workgroup, as md5_desc: the dispatcher spreads long-chunk waves
+// one per CU, and s_setprio favours them.
+// ---------------------------------------------------------------------------
+template <int CP, class H = Md5Hasher<true>>
+__device__ __forceinline__ void desc_xpose_body(const uint8_t* __restrict__ base,
+                                                const uint64_t* __restrict__ offs,
+                                                const uint32_t* __restrict__ lens,
+                                                const uint32_t* __restrict__ order, uint64_t n,
+                                                typename H::Out* __restrict__ out, uint8_t* img) {
+  H h;
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint64_t first = ((uint64_t)blockIdx.x * blockDim.x) + (threadIdx.x & ~63u);
+  if (first >= n) return;
+  const uint64_t i = first + lane;
+  const bool live = i < n;
+  const uint64_t c = order ? (uint64_t)order[live ? i : first] : (live ? i : first);
+  const uint8_t* chunk = base + offs[c];
+  const uint32_t len = live ? lens[c] : 0u;
+  const uint32_t nfull = len >> 6;
+  const uint32_t nst = nfull >> 1;                       // this lane's 128-B stages
+  const uint32_t smax = wave_max(nst);
+  const uint32_t bmax = wave_max(nfull);
+  if (bmax >= 4096u) __builtin_amdgcn_s_setprio(3);      // as desc_body
+  else if (bmax >= 1024u) __builtin_amdgcn_s_setprio(2);
+  else if (bmax >= 256u) __builtin_amdgcn_s_setprio(1);
+  typename H::State st = h.init();
+  const bool unaligned = __ballot(live && (((uintptr_t)chunk & 15u) != 0)) != 0;
+  if (unaligned) {
+    if (live) {                      // rare: a short ring keeps VGPRs for the main path
+      lane_range<H, 2>(h, st, chunk, len);
+      h.store(out, c, st);
+    }
+    return;
+  }
+  if (smax) {
+    // the row with the most stages stands in for rows without any
+    const uint32_t mrow = __builtin_ctzll(__ballot(nst == smax));
+    const uint64_t off = offs[c];
+    const uint8_t* rptr[8];            // base + offset: stays a global pointer (no flat loads)
+    uint32_t rlast[8];
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      uint32_t row = (uint32_t)r * 8u + (lane >> 3);
+      const uint32_t rn = (uint32_t)__shfl((int)nst, (int)row, 64);
+      if (rn == 0) row = mrow;
+      const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)off, (int)row, 64);
+      const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(off >> 32), (int)row, 64);
+      const uint32_t part = (lane & 7u) ^ ((row >> 1) & 7u);      // source swizzle (xpose)
+      rptr[r] = base + ((((uint64_t)hi << 32) | lo) + part * 16u);
+      rlast[r] = (rn ? rn : smax) - 1u;
+    }
+    const uint32_t g = (lane >> 1) & 7u;
+    auto load_stage = [&](u32x4 (&R)[8], uint32_t stg) __attribute__((always_inline)) {
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        const u32x4* a = reinterpret_cast<const u32x4*>(rptr[r] + (min(stg, rlast[r]) << 7));
+        R[r] = CP ? __builtin_nontemporal_load(a) : *a;
+      }
+    };
+    u32x4 R[8];
+    load_stage(R, 0);
+    for (uint32_t stg = 0; stg < smax; ++stg) {
+#pragma unroll
+      for (int r = 0; r < 8; ++r)
+        *reinterpret_cast<u32x4*>(img + r * 1024 + lane * 16) = R[r];
+      __builtin_amdgcn_wave_barrier();
+      uint4 w[2][4];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const u32x4 v = *reinterpret_cast<const u32x4*>(img + lane * 128 + ((q ^ g) * 16));
+        w[q >> 2][q & 3] = make_uint4(v.x, v.y, v.z, v.w);
+      }
+      __builtin_amdgcn_wave_barrier();
+      load_stage(R, min(stg + 1, smax - 1));
+      __builtin_amdgcn_sched_barrier(0);
+      if (stg < nst) {
+        h.block(st, w[0]);
+        h.block(st, w[1]);
+      }
+    }
+  }
+  if (live) {
+    if (nfull & 1u) {
+      uint4 w[4];
+      load_block(w, reinterpret_cast<const uint4*>(chunk + ((uint64_t)(nfull - 1) << 6)));
+      h.block(st, w);
+    }
+    h.finish(st, chunk + ((uint64_t)nfull << 6), len & 63u, len);
+    h.store(out, c, st);
+  }
+}
+
+__global__ void __launch_bounds__(64)
+md5_desc_xpose(const uint8_t* __restrict__ base, const uint64_t* __restrict__ offs,
+               const uint32_t* __restrict__ lens, const uint32_t* __restrict__ order, uint64_t n,
+               uint4* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) uint8_t img[8192];
+  desc_xpose_body<2>(base, offs, lens, order, n, out, img);
+}
+
+// ---------------------------------------------------------------------------
 // CRC-32 batches (netcache blk_make_crc, blk_io.c:354-430), same loaders.
 // ---------------------------------------------------------------------------
 __global__ void __launch_bounds__(256)

@@ -139,13 +139,39 @@ const char* md5hip_variant_name(int v) {
   }
 }
 
+int default_desc_variant() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("MD5HIP_DESC_VARIANT");
+    int x = e ? atoi(e) : 0;
+    v = (x > 0 && x < MD5HIP_DESC_NUM_VARIANTS) ? x : MD5HIP_DESC_XPOSE;
+  }
+  return v;
+}
+
 int md5hip_digest_desc(const void* d_base, const uint64_t* d_offsets, const uint32_t* d_lens,
                        const uint32_t* d_order, uint64_t n, unsigned char* d_digests,
                        void* stream) {
+  return md5hip_digest_desc_variant(d_base, d_offsets, d_lens, d_order, n, d_digests, stream,
+                                    MD5HIP_DESC_AUTO);
+}
+
+int md5hip_digest_desc_variant(const void* d_base, const uint64_t* d_offsets,
+                               const uint32_t* d_lens, const uint32_t* d_order, uint64_t n,
+                               unsigned char* d_digests, void* stream, int variant) {
   if (n == 0) return 0;
   if (!d_base || !d_offsets || !d_lens || !d_digests) return -EINVAL;
   if (((uintptr_t)d_digests & 15u) != 0) return -EINVAL;
+  if (variant < 0 || variant >= MD5HIP_DESC_NUM_VARIANTS) return -EINVAL;
   if (int e = device_ok()) return e;
+  if (variant == MD5HIP_DESC_AUTO) variant = default_desc_variant();
+  if (variant == MD5HIP_DESC_XPOSE) {
+    const uint64_t g = (n + 63) / 64;
+    if (g > 0x7fffffffull) return -EINVAL;
+    hipLaunchKernelGGL(md5_desc_xpose, dim3((uint32_t)g), dim3(64), 0, (hipStream_t)stream,
+                       (const uint8_t*)d_base, d_offsets, d_lens, d_order, n, (uint4*)d_digests);
+    return launched();
+  }
   // One wave per workgroup: a mixed batch has few waves, and the dispatcher
   // then spreads them one per CU instead of packing 4 onto one CU where the
   // long chunks' lane-direct loads contend for the CU's address unit

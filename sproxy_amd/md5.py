@@ -129,7 +129,10 @@ def digest_fixed(data, n: int = None, length: int = None, stride: int = None, ou
     return out
 
 
-def digest_desc(base, offsets, lens, order=None, out=None, stream=None):
+DESC_VARIANTS = {"auto": 0, "lane": 1, "xpose": 2}   # enum md5hip_desc_variant
+
+
+def digest_desc(base, offsets, lens, order=None, out=None, stream=None, variant=0):
     """digest[i] = MD5(base_bytes[offsets[i] : offsets[i] + lens[i]])."""
     _need_cuda(base, "base")
     _need_cuda(offsets, "offsets")
@@ -145,10 +148,12 @@ def digest_desc(base, offsets, lens, order=None, out=None, stream=None):
             raise ValueError("order must be an int32 permutation of range(n)")
     if out is None:
         out = torch.empty((n, 16), dtype=torch.uint8, device=base.device)
-    rc = lib().md5hip_digest_desc(base.data_ptr(), offsets.data_ptr(), lens.data_ptr(),
-                                  order.data_ptr() if order is not None else None, n,
-                                  out.data_ptr(), _stream(stream))
-    check("md5hip_digest_desc", rc)
+    if isinstance(variant, str):
+        variant = DESC_VARIANTS[variant]
+    rc = lib().md5hip_digest_desc_variant(base.data_ptr(), offsets.data_ptr(), lens.data_ptr(),
+                                          order.data_ptr() if order is not None else None, n,
+                                          out.data_ptr(), _stream(stream), variant)
+    check("md5hip_digest_desc_variant", rc)
     return out
 
 
@@ -386,6 +391,6 @@ def pool_plan(lens, nparts: int) -> np.ndarray:
 
 __all__ = ["MD5Context", "MD5Init", "MD5Update", "MD5Final", "MD5_DIGEST_SIZE", "MD5HipError",
            "md5", "digest_fixed", "digest_desc", "crc32_fixed", "crc32_desc", "plan_order", "fill_synthetic", "Batcher",
-           "Pool", "pool_plan", "CRC_VARIANTS",
+           "Pool", "pool_plan", "CRC_VARIANTS", "DESC_VARIANTS",
            "register_host", "unregister_host",
            "variant_name", "resolve_variant", "VARIANTS"]

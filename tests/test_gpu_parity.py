@@ -54,7 +54,11 @@ def test_fixed_edge_lengths(golden, cuda, variant):
         assert all(bytes(x).hex() == want for x in got), (variant, L)
 
 
-def test_kat_through_desc(golden, cuda):
+DESC = [v for v in m.DESC_VARIANTS if v != "auto"]
+
+
+@pytest.mark.parametrize("dv", DESC)
+def test_kat_through_desc(golden, cuda, dv):
     """All KAT messages packed at odd offsets into one descriptor batch."""
     msgs = [bytes.fromhex(v["hex"]) for v in golden["kat"]]
     offs, cur, parts = [], 3, [b"\xAA" * 3]
@@ -65,11 +69,12 @@ def test_kat_through_desc(golden, cuda):
     buf = np.frombuffer(b"".join(parts) + b"\0" * 64, dtype=np.uint8)
     lens = [len(x) for x in msgs]
     got = m.digest_desc(_dev(buf, cuda), torch.tensor(offs, dtype=torch.int64, device=cuda),
-                        torch.tensor(lens, dtype=torch.int32, device=cuda)).cpu().numpy()
+                        torch.tensor(lens, dtype=torch.int32, device=cuda), variant=dv).cpu().numpy()
     assert [bytes(x).hex() for x in got] == [v["md5"] for v in golden["kat"]]
 
 
-def test_mixed_golden(golden, cuda):
+@pytest.mark.parametrize("dv", DESC)
+def test_mixed_golden(golden, cuda, dv):
     mx = golden["mixed"]
     lens, offs = mx["lengths"], mx["offsets"]
     total = gen.pack_offsets(lens, align=mx["align"])[1]
@@ -77,12 +82,14 @@ def test_mixed_golden(golden, cuda):
     order = m.plan_order(lens).astype(np.int32)
     for o in (None, _dev(order, cuda)):
         got = m.digest_desc(_dev(buf, cuda), torch.tensor(offs, dtype=torch.int64, device=cuda),
-                            torch.tensor(lens, dtype=torch.int32, device=cuda), o).cpu().numpy()
+                            torch.tensor(lens, dtype=torch.int32, device=cuda), o,
+                            variant=dv).cpu().numpy()
         assert [bytes(x).hex() for x in got] == mx["md5"]
 
 
+@pytest.mark.parametrize("dv", DESC)
 @pytest.mark.parametrize("align", [1, 4, 16])
-def test_desc_random_vs_oracle(cuda, align):
+def test_desc_random_vs_oracle(cuda, align, dv):
     lens = gen.mixed_lengths(700, seed=11 + align, max_len=1 << 17)
     lens += [0, 1, 55, 56, 63, 64, 65, 119, 120, 127, 128]
     offs, total = gen.pack_offsets(lens, align=align)
@@ -91,8 +98,38 @@ def test_desc_random_vs_oracle(cuda, align):
     order = m.plan_order(lens).astype(np.int32)
     got = m.digest_desc(_dev(buf, cuda), torch.tensor(offs, dtype=torch.int64, device=cuda),
                         torch.tensor(lens, dtype=torch.int32, device=cuda),
-                        _dev(order, cuda)).cpu().numpy()
+                        _dev(order, cuda), variant=dv).cpu().numpy()
     assert np.array_equal(got, want)
+
+
+@pytest.mark.parametrize("dv", DESC)
+def test_desc_netcache_blocks(cuda, dv):
+    """The netcache shape the xpose descriptor kernel is built for: mostly
+    full chunk_size blocks plus ragged last blocks, 16-B aligned, packed in an
+    arena, ordered longest-first or not at all; plus waves whose chunks are
+    all shorter than one 128-B stage, a ragged last wave, and one unaligned
+    chunk that sends its wave down the lane-direct path."""
+    rng = np.random.default_rng(4242)
+    for S in (4096, 65536):
+        n = 1000
+        lens = np.full(n, S, dtype=np.int64)
+        tail = rng.integers(0, 8, n) == 0
+        lens[tail] = rng.integers(0, S, int(tail.sum()))
+        lens[-70:] = rng.integers(0, 128, 70)          # a whole wave without any stage
+        lens = [int(x) for x in lens]
+        for align in (16, 4):
+            offs, total = gen.pack_offsets(lens, align=align)
+            if align == 4:                             # only chunk 500 unaligned
+                offs = list(gen.pack_offsets(lens, align=16)[0])
+                offs[500] += 4
+                total = offs[-1] + lens[-1] + 64
+            buf = gen.xorshift_array(total + 64, seed=S + align)
+            want = gen.oracle_digests(buf, offs, lens)
+            for order in (m.plan_order(lens).astype(np.int32), None):
+                got = m.digest_desc(_dev(buf, cuda), torch.tensor(offs, dtype=torch.int64, device=cuda),
+                                    torch.tensor(lens, dtype=torch.int32, device=cuda),
+                                    None if order is None else _dev(order, cuda), variant=dv).cpu().numpy()
+                assert np.array_equal(got, want), (S, align, order is None)
 
 
 def test_unaligned_fixed_falls_back_bit_exact(cuda):
@@ -307,8 +344,9 @@ def test_huge_stride_and_large_chunks(cuda):
     da = _dev(arena, cuda)
     t_off = torch.tensor(offs, dtype=torch.int64, device=cuda)
     t_len = torch.tensor(lens, dtype=torch.int32, device=cuda)
-    got = m.digest_desc(da, t_off, t_len).cpu().numpy()
-    assert np.array_equal(got, gen.oracle_digests(arena, offs, lens))
+    for dv in DESC:
+        got = m.digest_desc(da, t_off, t_len, variant=dv).cpu().numpy()
+        assert np.array_equal(got, gen.oracle_digests(arena, offs, lens)), dv
     got = m.crc32_desc(da, t_off, t_len).cpu().numpy().view(np.uint32)
     assert np.array_equal(got, gen.oracle_crc32_batch(arena, offs, lens))
 
