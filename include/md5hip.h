@@ -80,7 +80,9 @@ enum md5hip_desc_variant {
     MD5HIP_DESC_LANE = 1,   /* each lane streams its own chunk (8-block register ring) */
     MD5HIP_DESC_XPOSE = 2,  /* whole-line loads of 8 chunks x 128 B + LDS transpose;
                                waves with an unaligned chunk fall back to LANE */
-    MD5HIP_DESC_NUM_VARIANTS = 3
+    MD5HIP_DESC_HYBRID = 3, /* XPOSE, but the first waves (one per CU, env MD5HIP_DESC_NLONG)
+                               go lane-direct when they hold a chunk >= 256 KiB */
+    MD5HIP_DESC_NUM_VARIANTS = 4
 };
 int md5hip_digest_desc_variant(const void *d_base, const uint64_t *d_offsets,
                                const uint32_t *d_lens, const uint32_t *d_order, uint64_t n,

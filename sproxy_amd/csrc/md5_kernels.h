@@ -581,12 +581,20 @@ md5_desc(const uint8_t* __restrict__ base, const uint64_t* __restrict__ offs,
 // One wave per workgroup, as md5_desc: the dispatcher spreads long-chunk waves
 // one per CU, and s_setprio favours them.
 // ---------------------------------------------------------------------------
-template <int CP, class H = Md5Hasher<true>>
+// kLong > 0: the first `nlong` waves (one per CU; with longest-first order
+// these hold the batch's longest chunks) take the lane-direct path with an
+// 8-block register ring when their longest chunk has >= kLong blocks.  Such a
+// wave is a serial chain that runs nearly alone on its SIMD: the xpose
+// stage's LDS round trip (8 ds_write_b128 + 8 ds_read_b128 + waits per
+// 128 B) sits on its critical path, while one lane-direct wave per CU does
+// not yet crowd the address unit (4 per CU did: DESIGN.md §5, C3).
+template <int CP, class H = Md5Hasher<true>, uint32_t kLong = 0, int D = 1>
 __device__ __forceinline__ void desc_xpose_body(const uint8_t* __restrict__ base,
                                                 const uint64_t* __restrict__ offs,
                                                 const uint32_t* __restrict__ lens,
                                                 const uint32_t* __restrict__ order, uint64_t n,
-                                                typename H::Out* __restrict__ out, uint8_t* img) {
+                                                typename H::Out* __restrict__ out, uint8_t* img,
+                                                uint32_t nlong = 0) {
   H h;
   const uint32_t lane = threadIdx.x & 63u;
   const uint64_t first = ((uint64_t)blockIdx.x * blockDim.x) + (threadIdx.x & ~63u);
@@ -605,6 +613,13 @@ __device__ __forceinline__ void desc_xpose_body(const uint8_t* __restrict__ base
   else if (bmax >= 256u) __builtin_amdgcn_s_setprio(1);
   typename H::State st = h.init();
   const bool unaligned = __ballot(live && (((uintptr_t)chunk & 15u) != 0)) != 0;
+  if (kLong && bmax >= kLong && (first >> 6) < nlong) {
+    if (live) {
+      lane_range<H, 8>(h, st, chunk, len);
+      h.store(out, c, st);
+    }
+    return;
+  }
   if (unaligned) {
     if (live) {                      // rare: a short ring keeps VGPRs for the main path
       lane_range<H, 2>(h, st, chunk, len);
@@ -637,9 +652,7 @@ __device__ __forceinline__ void desc_xpose_body(const uint8_t* __restrict__ base
         R[r] = CP ? __builtin_nontemporal_load(a) : *a;
       }
     };
-    u32x4 R[8];
-    load_stage(R, 0);
-    for (uint32_t stg = 0; stg < smax; ++stg) {
+    auto consume = [&](u32x4 (&R)[8], uint32_t stg, uint32_t next) __attribute__((always_inline)) {
 #pragma unroll
       for (int r = 0; r < 8; ++r)
         *reinterpret_cast<u32x4*>(img + r * 1024 + lane * 16) = R[r];
@@ -651,13 +664,26 @@ __device__ __forceinline__ void desc_xpose_body(const uint8_t* __restrict__ base
         w[q >> 2][q & 3] = make_uint4(v.x, v.y, v.z, v.w);
       }
       __builtin_amdgcn_wave_barrier();
-      load_stage(R, min(stg + 1, smax - 1));
+      load_stage(R, next);
       __builtin_amdgcn_sched_barrier(0);
       if (stg < nst) {
         h.block(st, w[0]);
         h.block(st, w[1]);
       }
+    };
+    // D-stage register ring (2*D blocks of prefetch per lane)
+    const uint32_t lasts = smax - 1;
+    u32x4 R[D][8];
+#pragma unroll
+    for (int j = 0; j < D; ++j) load_stage(R[j], min((uint32_t)j, lasts));
+    uint32_t stg = 0;
+    for (; stg + D <= smax; stg += D) {
+#pragma unroll
+      for (int j = 0; j < D; ++j) consume(R[j], stg + j, min(stg + j + D, lasts));
     }
+#pragma unroll
+    for (int j = 0; j < D - 1; ++j)
+      if (stg + j < smax) consume(R[j], stg + j, lasts);
   }
   if (live) {
     if (nfull & 1u) {
@@ -676,6 +702,14 @@ md5_desc_xpose(const uint8_t* __restrict__ base, const uint64_t* __restrict__ of
                uint4* __restrict__ out) {
   __shared__ __attribute__((aligned(16))) uint8_t img[8192];
   desc_xpose_body<2>(base, offs, lens, order, n, out, img);
+}
+
+__global__ void __launch_bounds__(64)
+md5_desc_hybrid(const uint8_t* __restrict__ base, const uint64_t* __restrict__ offs,
+                const uint32_t* __restrict__ lens, const uint32_t* __restrict__ order, uint64_t n,
+                uint4* __restrict__ out, uint32_t nlong) {
+  __shared__ __attribute__((aligned(16))) uint8_t img[8192];
+  desc_xpose_body<2, Md5Hasher<true>, 4096>(base, offs, lens, order, n, out, img, nlong);   // >= 256 KiB
 }
 
 // ---------------------------------------------------------------------------

@@ -149,6 +149,18 @@ int default_desc_variant() {
   return v;
 }
 
+// Waves (in longest-first order) that may take the lane-direct path in the
+// HYBRID descriptor kernel: one per CU (env MD5HIP_DESC_NLONG overrides, A/B).
+uint32_t desc_nlong() {
+  static int64_t v = -1;
+  if (v < 0) {
+    const char* e = getenv("MD5HIP_DESC_NLONG");
+    v = e ? (int64_t)strtoull(e, nullptr, 10) : (int64_t)cu_count();
+    if (v > 0xffffffffll) v = 0xffffffffll;
+  }
+  return (uint32_t)v;
+}
+
 int md5hip_digest_desc(const void* d_base, const uint64_t* d_offsets, const uint32_t* d_lens,
                        const uint32_t* d_order, uint64_t n, unsigned char* d_digests,
                        void* stream) {
@@ -165,6 +177,14 @@ int md5hip_digest_desc_variant(const void* d_base, const uint64_t* d_offsets,
   if (variant < 0 || variant >= MD5HIP_DESC_NUM_VARIANTS) return -EINVAL;
   if (int e = device_ok()) return e;
   if (variant == MD5HIP_DESC_AUTO) variant = default_desc_variant();
+  if (variant == MD5HIP_DESC_HYBRID) {
+    const uint64_t g = (n + 63) / 64;
+    if (g > 0x7fffffffull) return -EINVAL;
+    hipLaunchKernelGGL(md5_desc_hybrid, dim3((uint32_t)g), dim3(64), 0, (hipStream_t)stream,
+                       (const uint8_t*)d_base, d_offsets, d_lens, d_order, n, (uint4*)d_digests,
+                       desc_nlong());
+    return launched();
+  }
   if (variant == MD5HIP_DESC_XPOSE) {
     const uint64_t g = (n + 63) / 64;
     if (g > 0x7fffffffull) return -EINVAL;
