@@ -195,6 +195,7 @@ def run_crc(a, rank, world):
     dev_ms_max = max_over_ranks(dev_ms, world, COLL_DEVICE)
     value = float(n) * L * world * a.steps / wall_max / GIB
     alg_bytes = float(n) * (L + 4)
+    vname = "crc32 " + m.crc_variant_name(0)
     achieved = alg_bytes / (dev_ms_max * 1e-3) / 1e9
     return {"metric": "device-resident CRC-32 (netcache blk_make_crc) GiB/s on batched 16 KiB chunks",
             "value": round(value, 2), "unit": "GiB/s", "n_gpus": world, "steps": a.steps,
@@ -202,9 +203,10 @@ def run_crc(a, rank, world):
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32",
             "data": "synthetic (device-generated splitmix words, per-rank seed)",
             "config": {"workload": f"{n} x {L} B chunks per GPU, device-resident, fastcrc 0",
-                       "chunks_per_gpu": n, "chunk_bytes": L, "kernel_variant": "crc32 auto"},
+                       "chunks_per_gpu": n, "chunk_bytes": L, "kernel_variant": vname},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "traffic": load_traffic(a.traffic, vname), "kernel": vname,
                          "avg_launch_ms": round(dev_ms_max, 4), "alg_bytes_per_launch": int(alg_bytes)}}
 
 

@@ -112,6 +112,8 @@ enum crc32hip_variant {
 };
 int crc32hip_fixed_variant(const void *d_base, uint64_t n, uint32_t len, uint64_t stride,
                            uint32_t fastcrc, uint32_t *d_crcs, void *stream, int variant);
+/* The variant CRC32HIP_AUTO resolves to (same for any other value). */
+int crc32hip_resolve_variant(int variant);
 int crc32hip_desc(const void *d_base, const uint64_t *d_offsets, const uint32_t *d_lens,
                   const uint32_t *d_order, uint64_t n, uint32_t fastcrc, uint32_t *d_crcs,
                   void *stream);

@@ -60,6 +60,7 @@ def lib():
         "md5hip_abi_version": (i, []),
         "md5hip_variant_name": (ctypes.c_char_p, [i]),
         "md5hip_resolve_variant": (i, [i]),
+        "crc32hip_resolve_variant": (i, [i]),
         "md5hip_digest_fixed": (i, [vp, u64, u32, u64, vp, vp]),
         "md5hip_digest_fixed_variant": (i, [vp, u64, u32, u64, vp, vp, i]),
         "md5hip_digest_desc": (i, [vp, vp, vp, vp, u64, vp, vp]),
@@ -111,7 +112,7 @@ def lib():
 
 # Every symbol include/*.h declares (checked by tests/test_abi.py).
 EXPORTS = ["MD5Init", "MD5Update", "MD5Final", "nc_MD5Init", "nc_MD5Update", "nc_MD5Final", "md5hip_abi_version", "md5hip_variant_name",
-           "md5hip_resolve_variant",
+           "md5hip_resolve_variant", "crc32hip_resolve_variant",
            "md5hip_digest_fixed", "md5hip_digest_fixed_variant", "md5hip_digest_desc",
            "md5hip_digest_desc_variant",
            "md5hip_plan_order", "md5hip_fill_synthetic", "md5hip_batcher_create",

@@ -122,6 +122,7 @@ extern "C" {
 int md5hip_abi_version(void) { return MD5HIP_ABI_VERSION; }
 
 int md5hip_resolve_variant(int v) { return v == MD5HIP_AUTO ? default_variant() : v; }
+int crc32hip_resolve_variant(int v) { return v == CRC32HIP_AUTO ? default_crc_variant() : v; }
 
 const char* md5hip_variant_name(int v) {
   switch (v) {

@@ -215,6 +215,12 @@ def variant_name(v: int) -> str:
     return lib().md5hip_variant_name(v).decode()
 
 
+def crc_variant_name(v=0) -> str:
+    """Name (CRC_VARIANTS key) of the CRC-32 kernel variant v resolves to."""
+    r = lib().crc32hip_resolve_variant(CRC_VARIANTS[v] if isinstance(v, str) else v)
+    return {k: x for x, k in CRC_VARIANTS.items()}[r]
+
+
 def resolve_variant(v=AUTO) -> int:
     """The concrete kernel variant that `v` (AUTO by default) runs."""
     if isinstance(v, str):
@@ -393,4 +399,4 @@ __all__ = ["MD5Context", "MD5Init", "MD5Update", "MD5Final", "MD5_DIGEST_SIZE", 
            "md5", "digest_fixed", "digest_desc", "crc32_fixed", "crc32_desc", "plan_order", "fill_synthetic", "Batcher",
            "Pool", "pool_plan", "CRC_VARIANTS", "DESC_VARIANTS",
            "register_host", "unregister_host",
-           "variant_name", "resolve_variant", "VARIANTS"]
+           "variant_name", "resolve_variant", "VARIANTS", "crc_variant_name"]
