@@ -132,6 +132,23 @@ def test_desc_netcache_blocks(cuda, dv):
                 assert np.array_equal(got, want), (S, align, order is None)
 
 
+@pytest.mark.parametrize("dv", DESC)
+def test_desc_long_and_short_waves(cuda, dv):
+    """Waves whose longest chunk is >= 256 KiB (HYBRID sends the first of
+    them lane-direct) beside short-chunk waves, longest-first and unordered."""
+    rng = np.random.default_rng(99)
+    lens = ([1 << 20] * 70 + [256 << 10] * 40 + [int(x) for x in rng.integers(1, 1 << 19, 30)]
+            + [int(x) for x in rng.integers(0, 8192, 200)])
+    offs, total = gen.pack_offsets(lens, align=16)
+    buf = gen.xorshift_array(total + 64, seed=991)
+    want = gen.oracle_digests(buf, offs, lens)
+    for order in (m.plan_order(lens).astype(np.int32), None):
+        got = m.digest_desc(_dev(buf, cuda), torch.tensor(offs, dtype=torch.int64, device=cuda),
+                            torch.tensor(lens, dtype=torch.int32, device=cuda),
+                            None if order is None else _dev(order, cuda), variant=dv).cpu().numpy()
+        assert np.array_equal(got, want), order is None
+
+
 def test_unaligned_fixed_falls_back_bit_exact(cuda):
     n, L = 300, 1000
     host = gen.xorshift_array(n * L + 8, seed=9)
