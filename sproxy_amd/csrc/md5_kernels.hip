@@ -51,13 +51,17 @@ int launched() {
   return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }
 
+// Environment knob read once; C++ magic statics make the first call
+// thread-safe (the pool calls the launchers from one host thread per GPU).
+int env_int(const char* name, int lo, int hi, int dflt) {
+  const char* e = getenv(name);
+  const int x = e ? atoi(e) : 0;
+  return (x >= lo && x < hi) ? x : dflt;
+}
+
 int default_variant() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("MD5HIP_VARIANT");
-    int x = e ? atoi(e) : 0;
-    v = (x > 0 && x < MD5HIP_NUM_VARIANTS) ? x : MD5HIP_XPOSE1NT;   // measured best, DESIGN.md
-  }
+  static const int v = env_int("MD5HIP_VARIANT", 1, MD5HIP_NUM_VARIANTS,
+                               MD5HIP_XPOSE1NT);   // measured best, DESIGN.md
   return v;
 }
 
@@ -73,12 +77,8 @@ int cu_count() {
 }
 
 int default_crc_variant() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("CRC32HIP_VARIANT");
-    int x = e ? atoi(e) : 0;
-    v = (x > 0 && x < CRC32HIP_NUM_VARIANTS) ? x : CRC32HIP_XPERM16;  // measured best, DESIGN.md §5
-  }
+  static const int v = env_int("CRC32HIP_VARIANT", 1, CRC32HIP_NUM_VARIANTS,
+                               CRC32HIP_XPERM16);  // measured best, DESIGN.md §5
   return v;
 }
 
@@ -103,13 +103,10 @@ int launch_lds(const uint8_t* base, uint64_t n, uint32_t len, uint64_t stride, u
                hipStream_t s) {
   const size_t lds = (size_t)(kBlock / 64) * 2 * 64 * BB;
   auto fn = BB == 64 ? md5_fixed_lds64 : NT ? md5_fixed_lds128nt : md5_fixed_lds128;
-  static bool attr = false;
-  if (!attr) {
-    if (hipFuncSetAttribute(reinterpret_cast<const void*>(fn),
-                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
-      return -ENODEV;
-    attr = true;
-  }
+  static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(fn),
+                                               hipFuncAttributeMaxDynamicSharedMemorySize,
+                                               (int)lds) == hipSuccess;
+  if (!attr) return -ENODEV;
   const uint64_t grid = (n + kBlock - 1) / kBlock;
   hipLaunchKernelGGL(fn, dim3((uint32_t)grid), dim3(kBlock), lds, s, base, n, len, stride, out);
   return launched();
@@ -141,25 +138,18 @@ const char* md5hip_variant_name(int v) {
 }
 
 int default_desc_variant() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("MD5HIP_DESC_VARIANT");
-    int x = e ? atoi(e) : 0;
-    v = (x > 0 && x < MD5HIP_DESC_NUM_VARIANTS) ? x : MD5HIP_DESC_XPOSE;
-  }
+  static const int v = env_int("MD5HIP_DESC_VARIANT", 1, MD5HIP_DESC_NUM_VARIANTS,
+                               MD5HIP_DESC_XPOSE);
   return v;
 }
 
 // Waves (in longest-first order) that may take the lane-direct path in the
 // HYBRID descriptor kernel: one per CU (env MD5HIP_DESC_NLONG overrides, A/B).
 uint32_t desc_nlong() {
-  static int64_t v = -1;
-  if (v < 0) {
-    const char* e = getenv("MD5HIP_DESC_NLONG");
-    v = e ? (int64_t)strtoull(e, nullptr, 10) : (int64_t)cu_count();
-    if (v > 0xffffffffll) v = 0xffffffffll;
-  }
-  return (uint32_t)v;
+  const char* e = getenv("MD5HIP_DESC_NLONG");
+  if (!e) return (uint32_t)cu_count();      // per call: the pool drives several devices
+  const unsigned long long v = strtoull(e, nullptr, 10);
+  return v > 0xffffffffull ? 0xffffffffu : (uint32_t)v;
 }
 
 int md5hip_digest_desc(const void* d_base, const uint64_t* d_offsets, const uint32_t* d_lens,
@@ -340,11 +330,7 @@ int md5hip_gather_launch(const struct md5hip_seg* d_segs, uint64_t nseg, unsigne
   static_assert(sizeof(md5hip_seg) == sizeof(GatherSeg), "segment layout");
   if (nseg == 0) return 0;
   const uint64_t g = nseg < 65536 ? nseg : 65536;
-  static int unroll = -1;
-  if (unroll < 0) {
-    const char* e = getenv("MD5HIP_GATHER_UNROLL");   // A/B knob
-    unroll = e ? atoi(e) : 4;
-  }
+  static const int unroll = env_int("MD5HIP_GATHER_UNROLL", 1, 5, 4);   // A/B knob
   auto fn = unroll == 1 ? gather_segments<1> : unroll == 2 ? gather_segments<2> : gather_segments<4>;
   hipLaunchKernelGGL(fn, dim3((uint32_t)g), dim3(256), 0, (hipStream_t)stream,
                      reinterpret_cast<const GatherSeg*>(d_segs), nseg, d_dst);
