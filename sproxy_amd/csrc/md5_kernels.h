@@ -588,17 +588,17 @@ md5_desc(const uint8_t* __restrict__ base, const uint64_t* __restrict__ offs,
 // stage's LDS round trip (8 ds_write_b128 + 8 ds_read_b128 + waits per
 // 128 B) sits on its critical path, while one lane-direct wave per CU does
 // not yet crowd the address unit (4 per CU did: DESIGN.md §5, C3).
-template <int CP, class H = Md5Hasher<true>, uint32_t kLong = 0, int D = 1>
-__device__ __forceinline__ void desc_xpose_body(const uint8_t* __restrict__ base,
-                                                const uint64_t* __restrict__ offs,
-                                                const uint32_t* __restrict__ lens,
-                                                const uint32_t* __restrict__ order, uint64_t n,
-                                                typename H::Out* __restrict__ out, uint8_t* img,
-                                                uint32_t nlong = 0) {
-  H h;
+// kHalf: 4 KiB half image (rows 0-31, then rows 32-63, as xpose_half_group) so
+// a hasher with large LDS tables fits beside 16 waves' images; `first` is the
+// wave's first position in `order` (< n), the hasher is set up by the caller.
+template <int CP, class H, uint32_t kLong = 0, int D = 1, bool kHalf = false>
+__device__ __forceinline__ void desc_xpose_group(H& h, const uint8_t* __restrict__ base,
+                                                 const uint64_t* __restrict__ offs,
+                                                 const uint32_t* __restrict__ lens,
+                                                 const uint32_t* __restrict__ order, uint64_t n,
+                                                 uint64_t first, typename H::Out* __restrict__ out,
+                                                 uint8_t* img, uint32_t nlong = 0) {
   const uint32_t lane = threadIdx.x & 63u;
-  const uint64_t first = ((uint64_t)blockIdx.x * blockDim.x) + (threadIdx.x & ~63u);
-  if (first >= n) return;
   const uint64_t i = first + lane;
   const bool live = i < n;
   const uint64_t c = order ? (uint64_t)order[live ? i : first] : (live ? i : first);
@@ -652,16 +652,34 @@ __device__ __forceinline__ void desc_xpose_body(const uint8_t* __restrict__ base
         R[r] = CP ? __builtin_nontemporal_load(a) : *a;
       }
     };
-    auto consume = [&](u32x4 (&R)[8], uint32_t stg, uint32_t next) __attribute__((always_inline)) {
-#pragma unroll
-      for (int r = 0; r < 8; ++r)
-        *reinterpret_cast<u32x4*>(img + r * 1024 + lane * 16) = R[r];
-      __builtin_amdgcn_wave_barrier();
-      uint4 w[2][4];
+    const uint8_t* myrow = img + (kHalf ? (lane & 31u) : lane) * 128u;
+    auto read_row = [&](uint4 (&w)[2][4]) __attribute__((always_inline)) {
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
-        const u32x4 v = *reinterpret_cast<const u32x4*>(img + lane * 128 + ((q ^ g) * 16));
+        const u32x4 v = *reinterpret_cast<const u32x4*>(myrow + ((q ^ g) * 16));
         w[q >> 2][q & 3] = make_uint4(v.x, v.y, v.z, v.w);
+      }
+    };
+    auto consume = [&](u32x4 (&R)[8], uint32_t stg, uint32_t next) __attribute__((always_inline)) {
+      uint4 w[2][4];
+      if constexpr (kHalf) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          *reinterpret_cast<u32x4*>(img + r * 1024 + lane * 16) = R[r];
+        __builtin_amdgcn_wave_barrier();
+        if (lane < 32u) read_row(w);
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int r = 4; r < 8; ++r)
+          *reinterpret_cast<u32x4*>(img + (r - 4) * 1024 + lane * 16) = R[r];
+        __builtin_amdgcn_wave_barrier();
+        if (lane >= 32u) read_row(w);
+      } else {
+#pragma unroll
+        for (int r = 0; r < 8; ++r)
+          *reinterpret_cast<u32x4*>(img + r * 1024 + lane * 16) = R[r];
+        __builtin_amdgcn_wave_barrier();
+        read_row(w);
       }
       __builtin_amdgcn_wave_barrier();
       load_stage(R, next);
@@ -694,6 +712,19 @@ __device__ __forceinline__ void desc_xpose_body(const uint8_t* __restrict__ base
     h.finish(st, chunk + ((uint64_t)nfull << 6), len & 63u, len);
     h.store(out, c, st);
   }
+}
+
+template <int CP, class H = Md5Hasher<true>, uint32_t kLong = 0, int D = 1>
+__device__ __forceinline__ void desc_xpose_body(const uint8_t* __restrict__ base,
+                                                const uint64_t* __restrict__ offs,
+                                                const uint32_t* __restrict__ lens,
+                                                const uint32_t* __restrict__ order, uint64_t n,
+                                                typename H::Out* __restrict__ out, uint8_t* img,
+                                                uint32_t nlong = 0) {
+  H h;
+  const uint64_t first = ((uint64_t)blockIdx.x * blockDim.x) + (threadIdx.x & ~63u);
+  if (first >= n) return;
+  desc_xpose_group<CP, H, kLong, D>(h, base, offs, lens, order, n, first, out, img, nlong);
 }
 
 __global__ void __launch_bounds__(64)
@@ -851,7 +882,9 @@ __device__ __forceinline__ void crc32_xlane_body(const uint8_t* __restrict__ bas
   h.setup(tabs);
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint64_t ngroups = (n + 63) / 64;
-  for (uint64_t gi = (uint64_t)blockIdx.x * 16u + wave; gi < ngroups; gi += (uint64_t)gridDim.x * 16u)
+  // wave-major over the grid: group g goes to workgroup g % grid, so a batch
+  // of fewer than 16 groups per CU still spreads over every CU
+  for (uint64_t gi = (uint64_t)wave * gridDim.x + blockIdx.x; gi < ngroups; gi += (uint64_t)gridDim.x * 16u)
     xpose_half_group<H, 2>(h, base, n, len, stride, gi * 64u, out, img + wave * 4096u);
 }
 
@@ -870,6 +903,24 @@ crc32_fixed_xperm16(const uint8_t* __restrict__ base, uint64_t n, uint32_t len, 
                     uint32_t* __restrict__ out) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[Crc32PermHasher::kLdsBytes + 16 * 4096];
   crc32_xlane_body<Crc32PermHasher>(base, n, len, stride, out, lds, lds + Crc32PermHasher::kLdsBytes);
+}
+
+// Descriptor batches (ragged netcache blocks) with the XPERM16 tables: the
+// descriptor xpose loader (desc_xpose_group) with half images, one 1024-thread
+// workgroup per CU, grid-stride over 64-chunk groups of `order`.
+__global__ void __launch_bounds__(1024)
+crc32_desc_xperm16(const uint8_t* __restrict__ base, const uint64_t* __restrict__ offs,
+                   const uint32_t* __restrict__ lens, const uint32_t* __restrict__ order,
+                   uint64_t n, uint32_t* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds[Crc32PermHasher::kLdsBytes + 16 * 4096];
+  Crc32PermHasher h;
+  h.setup(lds);
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  uint8_t* img = lds + Crc32PermHasher::kLdsBytes + wave * 4096u;
+  const uint64_t ngroups = (n + 63) / 64;
+  for (uint64_t gi = (uint64_t)wave * gridDim.x + blockIdx.x; gi < ngroups; gi += (uint64_t)gridDim.x * 16u)
+    desc_xpose_group<2, Crc32PermHasher, 0, 1, true>(h, base, offs, lens, order, n, gi * 64u, out,
+                                                     img);   // (wave-major, as above)
 }
 
 // fastcrc (blk_io.c:408-424): len <= f -> crc(all), else crc(first f bytes)

@@ -275,8 +275,9 @@ int crc32hip_fixed_variant(const void* d_base, uint64_t n, uint32_t len, uint64_
   if (aligned && variant == CRC32HIP_LANE16) return launch_crc_lane<16>(base, n, len, stride, d_crcs, s);
   if (aligned && stride < (1ull << 31) / 64 &&
       (variant == CRC32HIP_XLANE16 || variant == CRC32HIP_XPERM16)) {
-    // one 1024-thread workgroup per CU (128 KiB LDS), grid-stride over 64-chunk groups
-    const uint64_t need = (n + kLaneBlock - 1) / kLaneBlock;
+    // one 1024-thread workgroup per CU (128 KiB LDS), grid-stride over 64-chunk
+    // groups, wave-major (every CU gets work once there is a group per CU)
+    const uint64_t need = (n + 63) / 64;
     const uint64_t cap = (uint64_t)cu_count();
     hipLaunchKernelGGL(variant == CRC32HIP_XLANE16 ? crc32_fixed_xlane16 : crc32_fixed_xperm16,
                        dim3((uint32_t)(need < cap ? need : cap)), dim3(kLaneBlock), 0, s, base,
@@ -317,6 +318,13 @@ int crc32hip_desc(const void* d_base, const uint64_t* d_offsets, const uint32_t*
     hipLaunchKernelGGL(crc32_fast<false>, dim3((uint32_t)g), dim3(kDescBlock), 0, s,
                        (const uint8_t*)d_base, d_offsets, d_lens, n, (uint64_t)0, 0u, fastcrc,
                        d_crcs);
+  } else if (default_crc_variant() == CRC32HIP_XPERM16) {
+    // XPERM16 tables + descriptor xpose loads: one 1024-thread workgroup per CU
+    const uint64_t need = (n + 63) / 64;
+    const uint64_t cap = (uint64_t)cu_count();
+    hipLaunchKernelGGL(crc32_desc_xperm16, dim3((uint32_t)(need < cap ? need : cap)),
+                       dim3(kLaneBlock), 0, s, (const uint8_t*)d_base, d_offsets, d_lens, d_order,
+                       n, d_crcs);
   } else {
     hipLaunchKernelGGL(crc32_desc<false>, dim3((uint32_t)g), dim3(kDescBlock), 0, s,
                        (const uint8_t*)d_base, d_offsets, d_lens, d_order, n, (uint64_t)0, 0u,

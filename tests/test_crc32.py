@@ -147,3 +147,30 @@ def test_gpu_crc_full_size(cuda):
     assert np.array_equal(got[torch.from_numpy(idx).to(cuda)].cpu().numpy().view(np.uint32), want)
     del d
     torch.cuda.empty_cache()
+
+
+@pytest.mark.gpu
+def test_gpu_crc_desc_netcache_blocks(cuda):
+    """crc32hip_desc on the netcache shape (full blocks + ragged last blocks,
+    a wave without any 128-B stage, one unaligned chunk, > one grid of
+    64-chunk groups), ordered longest-first and unordered: the XPERM16
+    descriptor kernel and its lane-direct fallback against crc32.c."""
+    import torch
+    rng = np.random.default_rng(777)
+    for S, n in ((4096, 40000), (65536, 700)):
+        lens = np.full(n, S, dtype=np.int64)
+        tail = rng.integers(0, 8, n) == 0
+        lens[tail] = rng.integers(0, S, int(tail.sum()))
+        lens[-70:] = rng.integers(0, 128, 70)
+        lens = [int(x) for x in lens]
+        offs = list(gen.pack_offsets(lens, align=16)[0])
+        offs[n // 2] += 4                              # one unaligned chunk
+        total = offs[-1] + lens[-1] + 64
+        buf = gen.xorshift_array(total + 64, seed=S)
+        want = gen.oracle_crc32_batch(buf, offs, lens)
+        d = _dev(buf, cuda)
+        t_off = torch.tensor(offs, dtype=torch.int64, device=cuda)
+        t_len = torch.tensor(lens, dtype=torch.int32, device=cuda)
+        for order in (m.plan_order(lens).astype(np.int32), None):
+            got = m.crc32_desc(d, t_off, t_len, None if order is None else _dev(order, cuda))
+            assert np.array_equal(got.cpu().numpy().view(np.uint32), want), (S, order is None)
