@@ -21,6 +21,7 @@
 //   kind 48,49 xpose1nt / compute only with per-wave clock stamps after the digests
 //   kind 50   load only (xpose1nt loader, xor fold) with clock stamps
 //   kind 51   CRC-32 product body (crc32_fixed_xpose) with clock stamps
+//   kind 52,53 xpose1nt on a persistent grid with a work counter (5 / 4 WGs per CU)
 //   kind 28-33 serial-chain latency with 64/32/16/1 active lanes (28-31), and
 //             64/32 with the latency-form step (32,33); n = waves, len = bytes
 //   kind 100+K VALU issue-rate probes (instruction K of diag_valu_rate)
@@ -223,6 +224,14 @@ diag_crc_clk(const uint8_t* __restrict__ base, uint64_t n, uint32_t len, uint64_
   }
 }
 
+// Dynamic (work-counter) xpose1nt: persistent grid, waves take 64-chunk groups.
+__global__ void __launch_bounds__(256)
+diag_xpose1nt_dyn(const uint8_t* __restrict__ base, uint64_t n, uint32_t len, uint64_t stride,
+                  uint4* __restrict__ out, uint32_t* counter) {
+  __shared__ __attribute__((aligned(16))) uint8_t img[4 * 8192];
+  fixed_xpose_dyn_body<1, Md5Hasher<false>, 2>(base, n, len, stride, out, img, counter);
+}
+
 // Ideal streaming read of n*len bytes: grid-stride, 16 B per lane, consecutive
 // lanes consecutive addresses; xor-fold per lane.
 __global__ void __launch_bounds__(256)
@@ -352,6 +361,18 @@ extern "C" int md5diag_run(int kind, const void* base, uint64_t n, uint32_t len,
     case 45: hipLaunchKernelGGL((diag_x64<0, true>), dim3(grid), dim3(256), 0, s, b, n, len, stride, o); break;
     case 46: hipLaunchKernelGGL(diag_xpose2_pair<2>, dim3(grid), dim3(256), 0, s, b, n, len, stride, o); break;
     case 47: hipLaunchKernelGGL(diag_xpose2_pair<0>, dim3(grid), dim3(256), 0, s, b, n, len, stride, o); break;
+    case 52: case 53: {
+      // dynamic xpose1nt: 52 = 5 workgroups per CU (its occupancy), 53 = 4
+      static uint32_t* counter = nullptr;
+      if (!counter && hipMalloc((void**)&counter, 4) != hipSuccess) return -ENOMEM;
+      int dev = 0, cus = 256;
+      (void)hipGetDevice(&dev);
+      (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+      (void)hipMemsetAsync(counter, 0, 4, s);
+      const uint32_t g = (uint32_t)cus * (kind == 52 ? 5u : 4u);
+      hipLaunchKernelGGL(diag_xpose1nt_dyn, dim3(g), dim3(256), 0, s, b, n, len, stride, o, counter);
+      break;
+    }
     case 51: hipLaunchKernelGGL(diag_crc_clk, dim3(grid), dim3(256), 0, s, b, n, len, stride, o); break;
     case 50: hipLaunchKernelGGL(diag_xpose1nt_clk<FoldHasher>, dim3(grid), dim3(256), 0, s, b, n, len, stride, o); break;
     case 48: hipLaunchKernelGGL(diag_xpose1nt_clk<Md5Hasher<false>>, dim3(grid), dim3(256), 0, s, b, n, len, stride, o); break;

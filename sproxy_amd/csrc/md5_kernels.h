@@ -215,20 +215,12 @@ __device__ __forceinline__ void fixed_lds_body(const uint8_t* __restrict__ base,
 // adjacent 128-B lines are requested back to back (one DRAM row visit for
 // 256 B instead of two visits a stage apart).
 template <int D, class H = Md5Hasher<false>, int CP = 0, bool kPair = false>
-__device__ __forceinline__ void fixed_xpose_body(const uint8_t* __restrict__ base, uint64_t n,
-                                                 uint32_t len, uint64_t stride,
-                                                 typename H::Out* __restrict__ out, uint8_t* lds,
-                                                 uint8_t* hlds = nullptr) {
+__device__ __forceinline__ void fixed_xpose_group(H& h, const uint8_t* __restrict__ base,
+                                                  uint64_t n, uint32_t len, uint64_t stride,
+                                                  typename H::Out* __restrict__ out, uint8_t* img,
+                                                  uint64_t wave_first) {
   static_assert(!kPair || D % 2 == 0, "paired refill needs an even ring");
-  H h;
-  h.setup(hlds);                     // before any early exit (may barrier)
   const uint32_t lane = threadIdx.x & 63u;
-  // readfirstlane: the descriptor must be provably wave-uniform, or hipcc
-  // wraps every buffer load in a waterfall loop (cdna_hip_programming.md T20)
-  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  uint8_t* img = lds + (size_t)wave * 8192;
-  const uint64_t wave_first = ((uint64_t)blockIdx.x * blockDim.x) + wave * 64u;
-  if (wave_first >= n) return;
   const uint64_t left = n - wave_first;
   const uint32_t rows = left < 64 ? (uint32_t)left : 64u;
   const __amdgpu_buffer_rsrc_t rsrc = uniform_rsrc(base + wave_first * stride);
@@ -304,6 +296,43 @@ __device__ __forceinline__ void fixed_xpose_body(const uint8_t* __restrict__ bas
   }
   h.finish(st, chunk + ((uint64_t)nfull << 6), len & 63u, len);
   if (lane < rows) h.store(out, i, st);
+}
+
+template <int D, class H = Md5Hasher<false>, int CP = 0, bool kPair = false>
+__device__ __forceinline__ void fixed_xpose_body(const uint8_t* __restrict__ base, uint64_t n,
+                                                 uint32_t len, uint64_t stride,
+                                                 typename H::Out* __restrict__ out, uint8_t* lds,
+                                                 uint8_t* hlds = nullptr) {
+  H h;
+  h.setup(hlds);                     // before any early exit (may barrier)
+  // readfirstlane: the wave index must be provably wave-uniform, or hipcc
+  // wraps every buffer load in a waterfall loop (cdna_hip_programming.md T20)
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint64_t wave_first = ((uint64_t)blockIdx.x * blockDim.x) + wave * 64u;
+  if (wave_first >= n) return;
+  fixed_xpose_group<D, H, CP, kPair>(h, base, n, len, stride, out, lds + (size_t)wave * 8192,
+                                     wave_first);
+}
+
+// Dynamic variant: a persistent grid whose waves take 64-chunk groups from a
+// global counter (zeroed by the launcher), so XCDs that run faster under the
+// power cap take more groups instead of idling at the end.
+template <int D, class H = Md5Hasher<false>, int CP = 0>
+__device__ __forceinline__ void fixed_xpose_dyn_body(const uint8_t* __restrict__ base, uint64_t n,
+                                                     uint32_t len, uint64_t stride,
+                                                     typename H::Out* __restrict__ out,
+                                                     uint8_t* lds, uint32_t* counter) {
+  H h;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  uint8_t* img = lds + (size_t)wave * 8192;
+  const uint64_t ngroups = (n + 63) / 64;
+  for (;;) {
+    uint32_t g = 0;
+    if ((threadIdx.x & 63u) == 0) g = atomicAdd(counter, 1u);
+    g = __builtin_amdgcn_readfirstlane(g);
+    if (g >= ngroups) break;
+    fixed_xpose_group<D, H, CP>(h, base, n, len, stride, out, img, (uint64_t)g * 64u);
+  }
 }
 
 // ---------------------------------------------------------------------------
