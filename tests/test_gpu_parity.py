@@ -189,6 +189,31 @@ def test_full_size_c2(cuda):
     torch.cuda.empty_cache()
 
 
+def test_c4_shard_shape(cuda):
+    """BASELINE config 4 on one device: 16,777,216 x 16 KiB split over 8 GPUs
+    is 2,097,152 chunks (32 GiB) per rank (sproxy_amd.shard.shard_range).
+    The last rank's shard, generated with bench.py's per-rank seed, hashed by
+    the default kernel: sampled chunks against the oracle, and the digest of a
+    chunk independent of where its shard starts (hash of a sub-batch = the
+    same rows of the whole)."""
+    from sproxy_amd.shard import shard_range
+    lo, hi = shard_range(16 << 20, 7, 8)
+    n, L = hi - lo, 16384
+    assert n == 2 << 20
+    d = torch.empty(n * L, dtype=torch.uint8, device=cuda)
+    m.fill_synthetic(d, seed=0x5EED0000 + 7)
+    got = m.digest_fixed(d, n, L)
+    rng = np.random.default_rng(4)
+    idx = np.unique(np.concatenate([[0, n // 2, n - 1], rng.integers(0, n, 2048)]))
+    rows = d.view(n, L)[torch.from_numpy(idx).to(cuda)].cpu().numpy()
+    assert np.array_equal(got[torch.from_numpy(idx).to(cuda)].cpu().numpy(),
+                          gen.oracle_digests_fixed(rows, idx.size, L))
+    part = m.digest_fixed(d[(n // 2) * L:], n // 2, L)
+    assert torch.equal(part, got[n // 2:])
+    del d
+    torch.cuda.empty_cache()
+
+
 def test_fill_synthetic_matches_numpy_mirror(cuda):
     t = torch.empty(4096, dtype=torch.uint8, device=cuda)
     m.fill_synthetic(t, seed=123)
