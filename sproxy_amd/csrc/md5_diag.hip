@@ -34,6 +34,127 @@
 
 namespace md5hip {
 
+// ---- experimental loaders (measured, not shipped: DESIGN.md §4) ----
+
+// ---------------------------------------------------------------------------
+// Fixed-length, 64-B stages at full occupancy ("x64").
+// The MD5 stream issues fastest with 8 waves per SIMD (the VALU issue rate of
+// the step's instructions rises from 4 to 8 waves per SIMD), which needs
+// <= 64 VGPRs and <= 5 KiB of LDS per wave.  A stage is one 64-B block for the
+// wave's 64 chunks (4 KiB): 4 buffer_load_dwordx4 wave-instructions of
+// 16 chunks x 64 B (4 lanes per run), a 4 KiB per-wave LDS image, one stage of
+// register prefetch.  kDma: the stage goes HBM -> LDS by LDS-DMA
+// (global_load_lds_dwordx4) instead of through VGPRs; the single image is
+// re-filled only after this lane's ds_reads have returned.
+// Same source swizzle as fixed_lds_body<64>: row L's 16-B slot q holds part
+// q ^ ((L >> 2) & 3), so every ds_read_b128 lane group is conflict-free.
+// Requires 64 * stride < 2^31 (checked by the launcher).
+// ---------------------------------------------------------------------------
+template <int CP, bool kDma = false, class H = Md5Hasher<false>>
+__device__ __forceinline__ void fixed_x64_body(const uint8_t* __restrict__ base, uint64_t n,
+                                               uint32_t len, uint64_t stride,
+                                               typename H::Out* __restrict__ out, uint8_t* lds) {
+  H h;
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  uint8_t* img = lds + (size_t)wave * 4096;
+  const uint64_t wave_first = ((uint64_t)blockIdx.x * blockDim.x) + wave * 64u;
+  if (wave_first >= n) return;
+  const uint64_t left = n - wave_first;
+  const uint32_t rows = left < 64 ? (uint32_t)left : 64u;
+  const uint8_t* wbase = base + wave_first * stride;
+  const __amdgpu_buffer_rsrc_t rsrc = uniform_rsrc(wbase);
+  uint32_t voff[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const uint32_t row = (uint32_t)r * 16u + (lane >> 2);
+    const uint32_t rc = row < rows ? row : rows - 1u;          // ragged last wave
+    const uint32_t part = (lane & 3u) ^ ((row >> 2) & 3u);       // source swizzle
+    voff[r] = rc * (uint32_t)stride + part * 16u;
+  }
+  const uint32_t g = (lane >> 2) & 3u;
+  const uint32_t nfull = len >> 6;
+  typename H::State st = h.init();
+
+  auto read_row = [&](uint4 (&w)[4]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const u32x4 v = *reinterpret_cast<const u32x4*>(img + lane * 64 + ((q ^ g) * 16));
+      w[q] = make_uint4(v.x, v.y, v.z, v.w);
+    }
+  };
+
+  if (nfull) {
+    const uint32_t lastb = nfull - 1;
+    if constexpr (kDma) {
+      // buffer_load_dwordx4 ... lds: per-lane voffset fixed, the stage offset
+      // in soffset, so the refill spends no VALU on addresses
+      auto issue = [&](uint32_t blk) __attribute__((always_inline)) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, img + r * 1024, 16, voff[r], blk * 64u, 0, CP);
+      };
+      issue(0);
+      for (uint32_t blk = 0; blk < nfull; ++blk) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        uint4 w[4];
+        read_row(w);
+        // the DMA below overwrites the image: this wave's reads must be done
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (blk < lastb) issue(blk + 1);
+        h.block(st, w);
+      }
+    } else {
+      auto load_stage = [&](u32x4 (&R)[4], uint32_t blk) __attribute__((always_inline)) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          R[r] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, (int)voff[r], (int)(blk * 64u), CP);
+      };
+      u32x4 R[4];
+      load_stage(R, 0);
+      for (uint32_t blk = 0; blk < nfull; ++blk) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          *reinterpret_cast<u32x4*>(img + r * 1024 + lane * 16) = R[r];
+        __builtin_amdgcn_wave_barrier();
+        uint4 w[4];
+        read_row(w);
+        __builtin_amdgcn_wave_barrier();
+        load_stage(R, min(blk + 1, lastb));
+        __builtin_amdgcn_sched_barrier(0);
+        h.block(st, w);
+      }
+    }
+  }
+  const uint64_t i = wave_first + lane;
+  const uint64_t ci = lane < rows ? i : n - 1;
+  const uint8_t* chunk = base + ci * stride;
+  h.finish(st, chunk + ((uint64_t)nfull << 6), len & 63u, len);
+  if (lane < rows) h.store(out, i, st);
+}
+
+// Dynamic variant: a persistent grid whose waves take 64-chunk groups from a
+// global counter (zeroed by the launcher), so XCDs that run faster under the
+// power cap take more groups instead of idling at the end.
+template <int D, class H = Md5Hasher<false>, int CP = 0>
+__device__ __forceinline__ void fixed_xpose_dyn_body(const uint8_t* __restrict__ base, uint64_t n,
+                                                     uint32_t len, uint64_t stride,
+                                                     typename H::Out* __restrict__ out,
+                                                     uint8_t* lds, uint32_t* counter) {
+  H h;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  uint8_t* img = lds + (size_t)wave * 8192;
+  const uint64_t ngroups = (n + 63) / 64;
+  for (;;) {
+    uint32_t g = 0;
+    if ((threadIdx.x & 63u) == 0) g = atomicAdd(counter, 1u);
+    g = __builtin_amdgcn_readfirstlane(g);
+    if (g >= ngroups) break;
+    fixed_xpose_group<D, H, CP>(h, base, n, len, stride, out, img, (uint64_t)g * 64u);
+  }
+}
+
+
 template __global__ void md5_fixed_direct<2, FoldHasher>(const uint8_t*, uint64_t, uint32_t, uint64_t, uint4*);
 template __global__ void md5_fixed_direct<4, FoldHasher>(const uint8_t*, uint64_t, uint32_t, uint64_t, uint4*);
 template __global__ void md5_fixed_direct<2, FoldHasher, true>(const uint8_t*, uint64_t, uint32_t, uint64_t, uint4*);
