@@ -287,7 +287,7 @@ diag_chain(uint32_t nblocks, uint4* __restrict__ out) {
   out[i] = make_uint4(st.a, st.b, st.c, st.d);
 }
 
-// 64-B-stage candidates at 8 waves per SIMD (md5_kernels.h fixed_x64_body).
+// 64-B-stage candidates at 8 waves per SIMD (fixed_x64_body above).
 template <int CP, bool kDma>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8)))
 diag_x64(const uint8_t* __restrict__ base, uint64_t n, uint32_t len, uint64_t stride,
