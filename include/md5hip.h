@@ -173,6 +173,28 @@ struct md5hip_iov {
 int md5_batch_submit_iov(md5hip_batcher *b, const struct md5hip_iov *segs,
                          const uint64_t *seg_first, uint64_t n, unsigned char *digests);
 
+/* Asynchronous forms: the
+ * call returns once the chunks have been gathered into the batcher's pinned
+ * staging -- the caller's buffers may be reused, except in the zero-copy
+ * gather modes (registered memory is read by the device until the work is
+ * done) -- and *ticket names the submission.  `digests` must stay valid until
+ * md5_batch_wait(b, ticket) returns 0 or md5_batch_poll(b, ticket) returns 1;
+ * both complete every earlier submission of the batcher too.  A later submit
+ * on the same batcher may deliver an earlier submission's digests while it
+ * reuses that work's pipeline slot.  Submissions larger than the pipeline
+ * (nslots x slice_bytes) block inside the call until slots free up. */
+int md5_batch_submit_async(md5hip_batcher *b, const void *const *ptrs, const uint32_t *lens,
+                           uint64_t n, unsigned char *digests, uint64_t *ticket);
+int md5_batch_submit_iov_async(md5hip_batcher *b, const struct md5hip_iov *segs,
+                               const uint64_t *seg_first, uint64_t n, unsigned char *digests,
+                               uint64_t *ticket);
+/* Block until submission `ticket` (and every earlier one) has delivered its
+ * digests: 0 or -errno. */
+int md5_batch_wait(md5hip_batcher *b, uint64_t ticket);
+/* Non-blocking: 1 = `ticket` (and every earlier one) delivered, 0 = still
+ * running, <0 = error. */
+int md5_batch_poll(md5hip_batcher *b, uint64_t ticket);
+
 /* Batched verify (cache read / write verify sites, blk_io.c:665-704,
  * bc_mgr.c:1464-1492): ok[i] = (digest of chunk i == expected[i]), expected
  * holding 16 (MD5) or 4 (CRC32) bytes per chunk.  Returns the number of

@@ -74,6 +74,10 @@ def lib():
         "md5hip_batcher_destroy": (None, [vp]),
         "md5_batch_submit": (i, [vp, vp, vp, u64, vp]),
         "md5_batch_submit_iov": (i, [vp, vp, vp, u64, vp]),
+        "md5_batch_submit_async": (i, [vp, vp, vp, u64, vp, vp]),
+        "md5_batch_submit_iov_async": (i, [vp, vp, vp, u64, vp, vp]),
+        "md5_batch_wait": (i, [vp, u64]),
+        "md5_batch_poll": (i, [vp, u64]),
         "md5hip_batcher_set_digest": (i, [vp, i, u32]),
         "md5hip_batch_verify_iov": (i, [vp, vp, vp, u64, vp, vp]),
         "md5hip_batch_host_fixed": (i, [vp, vp, u64, u32, u64, vp]),
@@ -118,6 +122,7 @@ EXPORTS = ["MD5Init", "MD5Update", "MD5Final", "nc_MD5Init", "nc_MD5Update", "nc
            "md5hip_plan_order", "md5hip_fill_synthetic", "md5hip_batcher_create",
            "crc32hip_fixed", "crc32hip_desc", "crc32hip_fixed_variant",
            "md5hip_batcher_destroy", "md5_batch_submit", "md5_batch_submit_iov",
+           "md5_batch_submit_async", "md5_batch_submit_iov_async", "md5_batch_wait", "md5_batch_poll",
            "md5hip_batcher_set_digest", "md5hip_batch_verify_iov",
            "md5hip_batch_host_fixed", "md5hip_pool_create", "md5hip_pool_destroy",
            "md5hip_pool_ndev", "md5hip_pool_set_digest", "md5hip_pool_submit",

@@ -126,6 +126,7 @@ struct slot {
     void **b_dst, **b_src;            /* DMA-batch gather arrays (plain host memory) */
     size_t *b_len;
     unsigned char *user_dig;          /* where this slot's digests go (NULL = idle) */
+    uint64_t ticket;                  /* submission the in-flight work belongs to */
     uint64_t ndig;
     uint32_t dsz;
     int busy;
@@ -141,6 +142,8 @@ struct md5hip_batcher {
     uint64_t maxn;     /* chunks per slot */
     uint64_t segcap;   /* gather segments per slot (zero-copy modes) */
     int gather;        /* enum md5hip_gather_mode */
+    uint32_t next;     /* slot the next slice goes to (round robin across calls) */
+    uint64_t ticket;   /* last submission ticket issued (md5_batch_wait) */
     struct slot *s;
 };
 
@@ -275,6 +278,7 @@ int md5hip_batcher_set_gather(md5hip_batcher *b, int mode)
 static int slot_launch(const md5hip_batcher *b, struct slot *sl, uint64_t n, uint64_t bytes,
                        uint64_t nseg, uint64_t ndma, unsigned char *user_dig)
 {
+    sl->ticket = b->ticket;
     int rc;
     if (md5hip_plan_order(sl->h_len, n, sl->h_ord) != 0) return -EINVAL;
     if (hipMemcpyAsync(sl->d_off, sl->h_off, 8 * n, hipMemcpyHostToDevice, sl->stream) ||
@@ -377,8 +381,12 @@ static void src_copy(const struct chunk_src *s, uint64_t i, unsigned char *dst)
     }
 }
 
+/* async == 0: returns once every digest is in `digests`.  async != 0:
+ * returns once the host gather is done (the caller's buffers are free again,
+ * except in the zero-copy modes); *ticket names the submission for
+ * md5_batch_wait / md5_batch_poll, which deliver its digests. */
 static int submit_gather(md5hip_batcher *b, const struct chunk_src *src, uint64_t n,
-                         unsigned char *digests)
+                         unsigned char *digests, int async, uint64_t *ticket)
 {
     for (uint64_t i = 0; i < n; i++) {
         const uint64_t L = src_len(src, i);
@@ -392,8 +400,10 @@ static int submit_gather(md5hip_batcher *b, const struct chunk_src *src, uint64_
             if (src_nseg(src, i) > b->segcap) zc = 0;   /* a chunk too fragmented for one table */
     const int dev = b->device < REG_MAXDEV ? b->device : 0;
     int rc = 0;
-    uint32_t k = 0;
+    uint32_t k = b->next;
     uint64_t i = 0;
+    const uint64_t t = ++b->ticket;
+    if (ticket) *ticket = t;
     while (i < n) {
         struct slot *sl = &b->s[k];
         if ((rc = slot_retire(sl))) return rc;
@@ -450,10 +460,37 @@ static int submit_gather(md5hip_batcher *b, const struct chunk_src *src, uint64_
                               digests + (size_t)b->dsz * first)))
             return rc;
         k = (k + 1) % b->nslots;
+        b->next = k;
     }
-    for (uint32_t j = 0; j < b->nslots; j++)
-        if ((rc = slot_retire(&b->s[j]))) return rc;
-    return 0;
+    return async ? 0 : md5_batch_wait(b, t);
+}
+
+int md5_batch_wait(md5hip_batcher *b, uint64_t ticket)
+{
+    if (!b) return -EINVAL;
+    int rc = 0;
+    for (uint32_t j = 0; j < b->nslots; j++) {
+        struct slot *sl = &b->s[j];
+        if (sl->busy && sl->ticket <= ticket) {
+            const int r = slot_retire(sl);
+            if (r && !rc) rc = r;
+        }
+    }
+    return rc;
+}
+
+int md5_batch_poll(md5hip_batcher *b, uint64_t ticket)
+{
+    if (!b) return -EINVAL;
+    for (uint32_t j = 0; j < b->nslots; j++) {
+        const struct slot *sl = &b->s[j];
+        if (!sl->busy || sl->ticket > ticket) continue;
+        const hipError_t e = hipEventQuery(sl->done);
+        if (e == hipErrorNotReady) return 0;
+        if (e != hipSuccess) return -EIO;
+    }
+    const int rc = md5_batch_wait(b, ticket);    /* all complete: deliver, no blocking */
+    return rc ? rc : 1;
 }
 
 int md5_batch_submit(md5hip_batcher *b, const void *const *ptrs, const uint32_t *lens, uint64_t n,
@@ -465,7 +502,20 @@ int md5_batch_submit(md5hip_batcher *b, const void *const *ptrs, const uint32_t 
     for (uint64_t i = 0; i < n; i++)
         if (!ptrs[i] && lens[i]) return -EINVAL;
     const struct chunk_src src = {ptrs, lens, NULL, NULL};
-    return submit_gather(b, &src, n, digests);
+    return submit_gather(b, &src, n, digests, 0, NULL);
+}
+
+int md5_batch_submit_async(md5hip_batcher *b, const void *const *ptrs, const uint32_t *lens,
+                           uint64_t n, unsigned char *digests, uint64_t *ticket)
+{
+    if (!b || !ticket) return -EINVAL;
+    *ticket = b->ticket;                   /* an empty batch is complete at once */
+    if (n == 0) return 0;
+    if (!ptrs || !lens || !digests) return -EINVAL;
+    for (uint64_t i = 0; i < n; i++)
+        if (!ptrs[i] && lens[i]) return -EINVAL;
+    const struct chunk_src src = {ptrs, lens, NULL, NULL};
+    return submit_gather(b, &src, n, digests, 1, ticket);
 }
 
 int md5_batch_submit_iov(md5hip_batcher *b, const struct md5hip_iov *segs,
@@ -480,7 +530,24 @@ int md5_batch_submit_iov(md5hip_batcher *b, const struct md5hip_iov *segs,
             if (!segs[j].base && segs[j].len) return -EINVAL;
     }
     const struct chunk_src src = {NULL, NULL, segs, seg_first};
-    return submit_gather(b, &src, n, digests);
+    return submit_gather(b, &src, n, digests, 0, NULL);
+}
+
+int md5_batch_submit_iov_async(md5hip_batcher *b, const struct md5hip_iov *segs,
+                               const uint64_t *seg_first, uint64_t n, unsigned char *digests,
+                               uint64_t *ticket)
+{
+    if (!b || !ticket) return -EINVAL;
+    *ticket = b->ticket;
+    if (n == 0) return 0;
+    if (!segs || !seg_first || !digests || seg_first[0] != 0) return -EINVAL;
+    for (uint64_t i = 0; i < n; i++) {
+        if (seg_first[i + 1] < seg_first[i]) return -EINVAL;
+        for (uint64_t j = seg_first[i]; j < seg_first[i + 1]; j++)
+            if (!segs[j].base && segs[j].len) return -EINVAL;
+    }
+    const struct chunk_src src = {NULL, NULL, segs, seg_first};
+    return submit_gather(b, &src, n, digests, 1, ticket);
 }
 
 int md5hip_batch_host_fixed(md5hip_batcher *b, const void *h_base, uint64_t n, uint32_t len,
@@ -495,7 +562,8 @@ int md5hip_batch_host_fixed(md5hip_batcher *b, const void *h_base, uint64_t n, u
     uint64_t per = b->cap / stride;
     if (per > b->maxn) per = b->maxn;
     int rc = 0;
-    uint32_t k = 0;
+    uint32_t k = b->next;
+    const uint64_t t = ++b->ticket;
     for (uint64_t i = 0; i < n; i += per) {
         const uint64_t m = n - i < per ? n - i : per;
         struct slot *sl = &b->s[k];
@@ -515,13 +583,13 @@ int md5hip_batch_host_fixed(md5hip_batcher *b, const void *h_base, uint64_t n, u
             return -EIO;
         sl->busy = 1;
         sl->user_dig = digests + (size_t)b->dsz * i;
+        sl->ticket = t;
         sl->ndig = m;
         sl->dsz = b->dsz;
         k = (k + 1) % b->nslots;
+        b->next = k;
     }
-    for (uint32_t j = 0; j < b->nslots; j++)
-        if ((rc = slot_retire(&b->s[j]))) return rc;
-    return 0;
+    return md5_batch_wait(b, t);
 }
 
 /* Batched verify for the cache-read / write-verify sites (blk_io.c:665-704,

@@ -237,7 +237,9 @@ class Batcher:
     _fn = dict(set_digest="md5hip_batcher_set_digest", set_gather="md5hip_batcher_set_gather",
                destroy="md5hip_batcher_destroy",
                submit="md5_batch_submit", submit_iov="md5_batch_submit_iov",
-               verify_iov="md5hip_batch_verify_iov", host_fixed="md5hip_batch_host_fixed")
+               verify_iov="md5hip_batch_verify_iov", host_fixed="md5hip_batch_host_fixed",
+               submit_async="md5_batch_submit_async", submit_iov_async="md5_batch_submit_iov_async",
+               wait="md5_batch_wait", poll="md5_batch_poll")
 
     def __init__(self, device: int = 0, slice_bytes: int = 0, nslots: int = 0,
                  kind: int = 0, fastcrc: int = 0):
@@ -324,6 +326,49 @@ class Batcher:
         check(*self._call("submit_iov", arr, fa.ctypes.data, n, out.ctypes.data))
         del keep
         return self._ret(out, n)
+
+    class Pending:
+        """An asynchronous submission: `ticket`, the output array, and the
+        input references the device may still read (zero-copy modes)."""
+
+        def __init__(self, batcher, ticket, out, n, keep):
+            self.batcher, self.ticket, self._out, self.n, self._keep = batcher, ticket, out, n, keep
+
+        def poll(self) -> bool:
+            name, rc = self.batcher._call("poll", ctypes.c_uint64(self.ticket))
+            if rc < 0:
+                check(name, rc)
+            return rc == 1
+
+        def wait(self) -> np.ndarray:
+            check(*self.batcher._call("wait", ctypes.c_uint64(self.ticket)))
+            self._keep = None
+            return self.batcher._ret(self._out, self.n)
+
+    def submit_async(self, buffers) -> "Batcher.Pending":
+        """md5_batch_submit_async: returns once the chunks are staged; the
+        digests are valid after .wait() (or once .poll() is True)."""
+        n = len(buffers)
+        keep, ptrs = [], (ctypes.c_void_p * max(n, 1))()
+        lens = np.empty(max(n, 1), dtype=np.uint32)
+        for i, b in enumerate(buffers):
+            a, k = _addr(b)
+            keep.append(k)
+            ptrs[i] = a
+            lens[i] = memoryview(b).nbytes
+        out = self._out(n)
+        t = ctypes.c_uint64()
+        check(*self._call("submit_async", ptrs, lens.ctypes.data, n, out.ctypes.data, ctypes.byref(t)))
+        return Batcher.Pending(self, t.value, out, n, (keep, ptrs, lens))
+
+    def submit_iov_async(self, chunks) -> "Batcher.Pending":
+        arr, fa, keep = self._iov(chunks)
+        n = len(chunks)
+        out = self._out(n)
+        t = ctypes.c_uint64()
+        check(*self._call("submit_iov_async", arr, fa.ctypes.data, n, out.ctypes.data,
+                          ctypes.byref(t)))
+        return Batcher.Pending(self, t.value, out, n, (keep, arr, fa))
 
     def verify_iov(self, chunks, expected):
         """(ok[i] bool array, mismatch count): digest(chunks[i]) == expected[i]."""

@@ -124,6 +124,11 @@ def test_argument_errors_before_device_work():
     h = ctypes.c_void_p()
     assert L.md5hip_batcher_create(0, 1 << 20, 99, ctypes.byref(h)) == EINVAL
     assert L.md5_batch_submit(None, None, None, 1, None) == EINVAL
+    t = ctypes.c_uint64()
+    assert L.md5_batch_submit_async(None, None, None, 1, None, ctypes.byref(t)) == EINVAL
+    assert L.md5_batch_submit_iov_async(None, None, None, 1, None, ctypes.byref(t)) == EINVAL
+    assert L.md5_batch_wait(None, 0) == EINVAL
+    assert L.md5_batch_poll(None, 0) == EINVAL
 
 
 def test_plan_order_longest_first():

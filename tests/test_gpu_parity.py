@@ -247,6 +247,38 @@ def test_batcher_submit(cuda):
     assert np.array_equal(got, want)
 
 
+def test_batcher_async_pipeline(cuda):
+    """md5_batch_submit_async / md5_batch_wait / md5_batch_poll: several
+    submissions in flight on one batcher (more slices than slots, so later
+    submits deliver earlier ones while reusing their slots), waited on out of
+    order, mixed with synchronous calls and iov submissions; every digest
+    array equals the oracle."""
+    rng = np.random.default_rng(5150)
+    batches = []
+    for k in range(6):
+        lens = [int(x) for x in rng.integers(0, 300000, 40)]
+        blob = gen.xorshift_bytes(sum(lens) + 1, seed=600 + k)
+        bufs, cur = [], 0
+        for L in lens:
+            bufs.append(blob[cur:cur + L])
+            cur += L
+        offs = np.cumsum([0] + lens[:-1])
+        batches.append((bufs, gen.oracle_digests(np.frombuffer(blob, dtype=np.uint8), offs, lens)))
+    with m.Batcher(device=0, slice_bytes=2 << 20, nslots=3) as b:
+        pend = [b.submit_async(bufs) for bufs, _ in batches[:4]]
+        assert np.array_equal(b.submit(batches[4][0]), batches[4][1])     # sync in between
+        pend.append(b.submit_iov_async([[x[:7], x[7:]] for x in batches[5][0]]))
+        for j in (2, 0, 5, 1, 3, 4):                                      # out of order
+            if j == 4:
+                continue
+            p = pend[j if j < 4 else 4]
+            got = p.wait()
+            assert np.array_equal(got, batches[j][1]), j
+        assert all(p.poll() for p in pend)
+        empty = b.submit_async([])
+        assert empty.poll() and empty.wait().shape[0] == 0
+
+
 def test_batcher_host_fixed(cuda):
     n, L = 5000, 16384
     host = gen.xorshift_array(n * L, seed=8)
