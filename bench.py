@@ -265,19 +265,25 @@ def run_c5(a, rank, world):
     host = torch.empty(n * L, dtype=torch.uint8, pin_memory=True)
     host.view(torch.int64).random_(generator=torch.Generator().manual_seed(5))
     arr = host.numpy()
-    # PCIe H2D alone (the denominator for this config): same slices, warmed up
-    dev = torch.empty(a.c5_slice, dtype=torch.uint8, device="cuda")
+    # PCIe H2D alone (the denominator for this config): the same slices, on one
+    # stream and round-robin over as many streams as the batcher has slots
+    # (concurrent DMA); the better of the two, warmed up
+    nsl = 3
+    devs = [torch.empty(a.c5_slice, dtype=torch.uint8, device="cuda") for _ in range(nsl)]
+    streams = [torch.cuda.Stream() for _ in range(nsl)]
     per = a.c5_slice
-    for _ in range(2):
+    h2d_gbs = 0.0
+    for nst in (1, nsl, 1, nsl):
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        for off in range(0, n * L, per):
+        for k, off in enumerate(range(0, n * L, per)):
             m_ = min(per, n * L - off)
-            dev[:m_].copy_(host[off:off + m_], non_blocking=True)
+            with torch.cuda.stream(streams[k % nst]):
+                devs[k % nst][:m_].copy_(host[off:off + m_], non_blocking=True)
         torch.cuda.synchronize()
-        h2d_gbs = n * L / (time.perf_counter() - t0) / 1e9
-    del dev
-    with m.Batcher(device=torch.cuda.current_device(), slice_bytes=a.c5_slice, nslots=3) as b:
+        h2d_gbs = max(h2d_gbs, n * L / (time.perf_counter() - t0) / 1e9)
+    del devs
+    with m.Batcher(device=torch.cuda.current_device(), slice_bytes=a.c5_slice, nslots=nsl) as b:
         for _ in range(a.warmup):
             b.host_fixed(arr, n, L)
         t0 = time.perf_counter()
@@ -294,7 +300,8 @@ def run_c5(a, rank, world):
                                                           "slots": 3},
             "roofline": {"bound": "pcie", "achieved": round(gbs, 2), "peak": round(h2d_gbs, 2),
                          "unit": "GB/s", "frac": round(gbs / h2d_gbs, 4),
-                         "peak_note": f"measured pinned H2D copy alone; spec {PCIE_PEAK_GBS} GB/s",
+                         "peak_note": (f"measured pinned H2D copy alone, best of 1 and {nsl} "
+                                       f"streams; spec {PCIE_PEAK_GBS} GB/s"),
                          "traffic": None}}
 
 
