@@ -22,6 +22,7 @@
 //   kind 50   load only (xpose1nt loader, xor fold) with clock stamps
 //   kind 51   CRC-32 product body (crc32_fixed_xpose) with clock stamps
 //   kind 52,53 xpose1nt on a persistent grid with a work counter (5 / 4 WGs per CU)
+//   kind 54   xpose1nt without the peeled last stage (clamped re-read)
 //   kind 28-33 serial-chain latency with 64/32/16/1 active lanes (28-31), and
 //             64/32 with the latency-form step (32,33); n = waves, len = bytes
 //   kind 100+K VALU issue-rate probes (instruction K of diag_valu_rate)
@@ -353,6 +354,20 @@ diag_xpose1nt_dyn(const uint8_t* __restrict__ base, uint64_t n, uint32_t len, ui
   fixed_xpose_dyn_body<1, Md5Hasher<false>, 2>(base, n, len, stride, out, img, counter);
 }
 
+// xpose1nt without the peeled last stage (its refill re-reads the last 128 B
+// of every chunk): A/B for the peel.
+__global__ void __launch_bounds__(256)
+diag_xpose1nt_nopeel(const uint8_t* __restrict__ base, uint64_t n, uint32_t len, uint64_t stride,
+                     uint4* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) uint8_t img[4 * 8192];
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint64_t wave_first = ((uint64_t)blockIdx.x * blockDim.x) + wave * 64u;
+  if (wave_first >= n) return;
+  Md5Hasher<false> h;
+  fixed_xpose_group<1, Md5Hasher<false>, 2, false, false>(h, base, n, len, stride, out,
+                                                          img + wave * 8192u, wave_first);
+}
+
 // Ideal streaming read of n*len bytes: grid-stride, 16 B per lane, consecutive
 // lanes consecutive addresses; xor-fold per lane.
 __global__ void __launch_bounds__(256)
@@ -494,6 +509,7 @@ extern "C" int md5diag_run(int kind, const void* base, uint64_t n, uint32_t len,
       hipLaunchKernelGGL(diag_xpose1nt_dyn, dim3(g), dim3(256), 0, s, b, n, len, stride, o, counter);
       break;
     }
+    case 54: hipLaunchKernelGGL(diag_xpose1nt_nopeel, dim3(grid), dim3(256), 0, s, b, n, len, stride, o); break;
     case 51: hipLaunchKernelGGL(diag_crc_clk, dim3(grid), dim3(256), 0, s, b, n, len, stride, o); break;
     case 50: hipLaunchKernelGGL(diag_xpose1nt_clk<FoldHasher>, dim3(grid), dim3(256), 0, s, b, n, len, stride, o); break;
     case 48: hipLaunchKernelGGL(diag_xpose1nt_clk<Md5Hasher<false>>, dim3(grid), dim3(256), 0, s, b, n, len, stride, o); break;

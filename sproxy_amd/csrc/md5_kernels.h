@@ -214,7 +214,7 @@ __device__ __forceinline__ void fixed_lds_body(const uint8_t* __restrict__ base,
 // kPair (D even): the ring is refilled two slots at a time, so a chunk's two
 // adjacent 128-B lines are requested back to back (one DRAM row visit for
 // 256 B instead of two visits a stage apart).
-template <int D, class H = Md5Hasher<false>, int CP = 0, bool kPair = false>
+template <int D, class H = Md5Hasher<false>, int CP = 0, bool kPair = false, bool kPeel = true>
 __device__ __forceinline__ void fixed_xpose_group(H& h, const uint8_t* __restrict__ base,
                                                   uint64_t n, uint32_t len, uint64_t stride,
                                                   typename H::Out* __restrict__ out, uint8_t* img,
@@ -270,20 +270,27 @@ __device__ __forceinline__ void fixed_xpose_group(H& h, const uint8_t* __restric
 #pragma unroll
     for (int j = 0; j < D; ++j) load_stage(R[j], min((uint32_t)j, lasts));
     uint32_t stg = 0;
-    for (; stg + D <= nstage; stg += D) {
+    if constexpr (D == 1 && kPeel) {
+      // the last stage is peeled: no refill past the end (a clamped refill
+      // would re-read the last 128 B of every chunk, +0.7 % HBM bytes)
+      for (; stg + 1 < nstage; ++stg) consume(R[0], stg + 1, 1);
+      consume(R[0], 0, 0);
+    } else {                         // (D == 1 without kPeel: the clamped re-read)
+      for (; stg + D <= nstage; stg += D) {
 #pragma unroll
-      for (int j = 0; j < D; ++j) {
-        if constexpr (kPair) {
-          if (j & 1) consume(R[j], min(stg + j + D, lasts), 2, &R[j - 1]);
-          else consume(R[j], 0, 0);
-        } else {
-          consume(R[j], min(stg + j + D, lasts), 1);
+        for (int j = 0; j < D; ++j) {
+          if constexpr (kPair) {
+            if (j & 1) consume(R[j], min(stg + j + D, lasts), 2, &R[j - 1]);
+            else consume(R[j], 0, 0);
+          } else {
+            consume(R[j], min(stg + j + D, lasts), 1);
+          }
         }
       }
-    }
 #pragma unroll
-    for (int j = 0; j < D - 1; ++j)
-      if (stg + j < nstage) consume(R[j], lasts, 0);
+      for (int j = 0; j < D - 1; ++j)
+        if (stg + j < nstage) consume(R[j], lasts, 0);
+    }
   }
   // leftover odd block, then the tail
   const uint64_t i = wave_first + lane;
@@ -324,7 +331,7 @@ md5_fixed_lds64(const uint8_t* __restrict__ base, uint64_t n, uint32_t len, uint
   fixed_lds_body<64>(base, n, len, stride, out, lds_dyn);
 }
 
-__global__ void __launch_bounds__(256)
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5)))
 md5_fixed_xpose1(const uint8_t* __restrict__ base, uint64_t n, uint32_t len, uint64_t stride,
                  uint4* __restrict__ out) {
   __shared__ __attribute__((aligned(16))) uint8_t img[4 * 8192];
@@ -340,7 +347,7 @@ md5_fixed_xpose2(const uint8_t* __restrict__ base, uint64_t n, uint32_t len, uin
 
 // Non-temporal ("nt", aux = 2) load policy: every byte is read exactly once,
 // so do not let the stream allocate in L2 / Infinity Cache.
-__global__ void __launch_bounds__(256)
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5)))
 md5_fixed_xpose1nt(const uint8_t* __restrict__ base, uint64_t n, uint32_t len, uint64_t stride,
                    uint4* __restrict__ out) {
   __shared__ __attribute__((aligned(16))) uint8_t img[4 * 8192];
@@ -503,7 +510,7 @@ md5_desc(const uint8_t* __restrict__ base, const uint64_t* __restrict__ offs,
 // kHalf: 4 KiB half image (rows 0-31, then rows 32-63, as xpose_half_group) so
 // a hasher with large LDS tables fits beside 16 waves' images; `first` is the
 // wave's first position in `order` (< n), the hasher is set up by the caller.
-template <int CP, class H, uint32_t kLong = 0, int D = 1, bool kHalf = false>
+template <int CP, class H, uint32_t kLong = 0, int D = 1, bool kHalf = false, bool kPeel = true>
 __device__ __forceinline__ void desc_xpose_group(H& h, const uint8_t* __restrict__ base,
                                                  const uint64_t* __restrict__ offs,
                                                  const uint32_t* __restrict__ lens,
@@ -572,7 +579,8 @@ __device__ __forceinline__ void desc_xpose_group(H& h, const uint8_t* __restrict
         w[q >> 2][q & 3] = make_uint4(v.x, v.y, v.z, v.w);
       }
     };
-    auto consume = [&](u32x4 (&R)[8], uint32_t stg, uint32_t next) __attribute__((always_inline)) {
+    auto consume = [&](u32x4 (&R)[8], uint32_t stg, uint32_t next, bool refill = true)
+        __attribute__((always_inline)) {
       uint4 w[2][4];
       if constexpr (kHalf) {
 #pragma unroll
@@ -594,7 +602,7 @@ __device__ __forceinline__ void desc_xpose_group(H& h, const uint8_t* __restrict
         read_row(w);
       }
       __builtin_amdgcn_wave_barrier();
-      load_stage(R, next);
+      if (refill) load_stage(R, next);
       __builtin_amdgcn_sched_barrier(0);
       if (stg < nst) {
         h.block(st, w[0]);
@@ -607,13 +615,18 @@ __device__ __forceinline__ void desc_xpose_group(H& h, const uint8_t* __restrict
 #pragma unroll
     for (int j = 0; j < D; ++j) load_stage(R[j], min((uint32_t)j, lasts));
     uint32_t stg = 0;
-    for (; stg + D <= smax; stg += D) {
+    if constexpr (D == 1 && kPeel) {
+      for (; stg + 1 < smax; ++stg) consume(R[0], stg, stg + 1);   // last stage peeled:
+      consume(R[0], stg, 0, false);                               // no re-read past the end
+    } else {
+      for (; stg + D <= smax; stg += D) {
 #pragma unroll
-      for (int j = 0; j < D; ++j) consume(R[j], stg + j, min(stg + j + D, lasts));
+        for (int j = 0; j < D; ++j) consume(R[j], stg + j, min(stg + j + D, lasts));
+      }
+#pragma unroll
+      for (int j = 0; j < D - 1; ++j)
+        if (stg + j < smax) consume(R[j], stg + j, lasts);
     }
-#pragma unroll
-    for (int j = 0; j < D - 1; ++j)
-      if (stg + j < smax) consume(R[j], stg + j, lasts);
   }
   if (live) {
     if (nfull & 1u) {
@@ -831,8 +844,8 @@ crc32_desc_xperm16(const uint8_t* __restrict__ base, const uint64_t* __restrict_
   uint8_t* img = lds + Crc32PermHasher::kLdsBytes + wave * 4096u;
   const uint64_t ngroups = (n + 63) / 64;
   for (uint64_t gi = (uint64_t)wave * gridDim.x + blockIdx.x; gi < ngroups; gi += (uint64_t)gridDim.x * 16u)
-    desc_xpose_group<2, Crc32PermHasher, 0, 1, true>(h, base, offs, lens, order, n, gi * 64u, out,
-                                                     img);   // (wave-major, as above)
+    desc_xpose_group<2, Crc32PermHasher, 0, 1, true, false>(h, base, offs, lens, order, n,
+                                                            gi * 64u, out, img);   // (wave-major, as above)
 }
 
 // fastcrc (blk_io.c:408-424): len <= f -> crc(all), else crc(first f bytes)
