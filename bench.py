@@ -344,8 +344,10 @@ def run_c5(a, rank, world):
 def main():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=20)
-    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--steps", type=int, default=50)
+    p.add_argument("--warmup", type=int, default=20,
+                   help="untimed launches first: the board settles its clock over the first ~15 "
+                        "launches of a 3 ms kernel (slow start, profiles/r01_bench_kernel_trace_startup.json)")
     p.add_argument("--config", default="c2", choices=["c2", "c3", "c5", "crc"])
     p.add_argument("--chunks", type=int, default=1 << 20, help="chunks per GPU (C2, weak scaling)")
     p.add_argument("--total-chunks", type=int, default=0,
