@@ -149,6 +149,33 @@ def test_desc_long_and_short_waves(cuda, dv):
         assert np.array_equal(got, want), order is None
 
 
+@pytest.mark.parametrize("dv", DESC)
+def test_desc_offsets_beyond_4gib(cuda, dv):
+    """Descriptor offsets past 2^32 (64-bit row pointers): chunks scattered
+    over a 5 GiB arena, half of them above 4 GiB, one wave straddling."""
+    arena = torch.empty(5 << 30, dtype=torch.uint8, device=cuda)
+    m.fill_synthetic(arena, seed=0x4646)
+    rng = np.random.default_rng(46)
+    n = 200
+    lens = [int(x) for x in rng.integers(0, 70000, n)]
+    lo = rng.integers(0, (4 << 30) // 16 - 8192, n // 2) * 16
+    hi = rng.integers((4 << 30) // 16, (5 << 30) // 16 - 8192, n - n // 2) * 16
+    offs = np.concatenate([lo, hi]).astype(np.int64)
+    rng.shuffle(offs)
+    want = np.empty((n, 16), dtype=np.uint8)
+    for i in range(n):
+        chunk = arena[int(offs[i]):int(offs[i]) + lens[i]].cpu().numpy()
+        want[i] = gen.oracle_digests(chunk, [0], [lens[i]])[0] if lens[i] else \
+            np.frombuffer(bytes.fromhex("d41d8cd98f00b204e9800998ecf8427e"), dtype=np.uint8)
+    order = m.plan_order(lens).astype(np.int32)
+    got = m.digest_desc(arena, torch.from_numpy(offs).to(cuda),
+                        torch.tensor(lens, dtype=torch.int32, device=cuda), _dev(order, cuda),
+                        variant=dv).cpu().numpy()
+    assert np.array_equal(got, want)
+    del arena
+    torch.cuda.empty_cache()
+
+
 def test_unaligned_fixed_falls_back_bit_exact(cuda):
     n, L = 300, 1000
     host = gen.xorshift_array(n * L + 8, seed=9)
