@@ -672,3 +672,18 @@ extern "C" int md5diag_desc_trace(int tpb, const void* base, const uint64_t* off
                        (const uint8_t*)base, offs, lens, order, n, (uint4*)out, (uint64_t*)rec);
   return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }
+
+// The product descriptor kernel (md5_desc_xpose) with `extra` bytes of dynamic
+// LDS per 64-thread workgroup, which caps how many of its waves a CU holds
+// (160 KiB / (8 KiB + extra)): a throttled short-chunk launch beside long
+// chains (scripts/c3_throttle.py).
+extern "C" int md5diag_desc_xpose_lds(const void* base, const uint64_t* offs, const uint32_t* lens,
+                                      const uint32_t* order, uint64_t n, void* out,
+                                      uint32_t extra, void* stream) {
+  if (extra > 32768)
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(md5_desc_xpose),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)extra);
+  hipLaunchKernelGGL(md5_desc_xpose, dim3((uint32_t)((n + 63) / 64)), dim3(64), extra,
+                     (hipStream_t)stream, (const uint8_t*)base, offs, lens, order, n, (uint4*)out);
+  return hipGetLastError() == hipSuccess ? 0 : -EIO;
+}
