@@ -56,13 +56,17 @@ __device__ __forceinline__ void load_tail(const uint8_t* tail, uint32_t r, uint3
 // ---------------------------------------------------------------------------
 // MD5 (md5.c).  Digest = A,B,C,D little-endian (md5.c:262-263).
 // ---------------------------------------------------------------------------
-template <bool kLat = false>
+// kX3 (default): round 3 as v_xad_u32 pairs, 316 instead of 324 VALU per
+// block -- measured 1.2 % faster at the board's power cap.
+template <bool kLat = false, bool kX3 = true>
 struct Md5Hasher {
   using State = md5hip::State;
   using Out = uint4;
   __device__ __forceinline__ void setup(uint8_t*) {}
   __device__ __forceinline__ State init() { return initial_state(); }
-  __device__ __forceinline__ void block(State& st, const uint4 (&w)[4]) { compress_regs<kLat>(st, w); }
+  __device__ __forceinline__ void block(State& st, const uint4 (&w)[4]) {
+    compress_regs<kLat, kX3>(st, w);
+  }
   // 0x80, zeros, 64-bit bit count (md5.c:221-261); one or two final blocks.
   __device__ __forceinline__ void finish(State& st, const uint8_t* tail, uint32_t r,
                                          uint64_t len_bytes) {

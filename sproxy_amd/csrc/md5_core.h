@@ -72,10 +72,28 @@ __device__ __forceinline__ uint32_t md5_sum(uint32_t w, uint32_t m, uint32_t k, 
 #define MD5HIP_STEP(F, w, x, y, z, m, k, s) \
   w = x + rotl(md5_sum<kLat>(w, (m), (k), F(x, y, z)), s)
 
+// Round 3 (H = x ^ y ^ z, md5.c:51) two steps at a time (kX3): step k uses
+// H(b, c, d) and step k+1 H(a', b, c), so b ^ c serves both, and each step's
+// "+ H" becomes one v_xad_u32 ((p ^ q) + t): 3 VALU instead of 4 per two
+// steps (316 instead of 324 per block), and step k+1's serial chain is
+// a' -> xad -> alignbit -> add.
+template <bool kLat>
+__device__ __forceinline__ uint32_t md5_xsum(uint32_t w, uint32_t m, uint32_t k, uint32_t p,
+                                             uint32_t q) {
+  const uint32_t t = w + m + k;
+  uint32_t r;   // hipcc splits (p ^ q) + t into v_xor + v_add; ask for v_xad_u32
+  asm("v_xad_u32 %0, %1, %2, %3" : "=v"(r) : "v"(p), "v"(q), "v"(t));
+  return r;
+}
+#define MD5HIP_STEP3_PAIR(w1, w2, x, y, m1, k1, s1, m2, k2, s2) \
+  { const uint32_t cx = x ^ y;                                   \
+    w1 = x + rotl(md5_xsum<kLat>(w1, (m1), (k1), cx, w2), s1);     \
+    w2 = w1 + rotl(md5_xsum<kLat>(w2, (m2), (k2), cx, w1), s2); }
+
 // One 64-byte block, message words m[0..15] little-endian (byteReverse is a
 // no-op on little-endian gfx950, md5.c:24-25).  The 64 K literals are the
 // RFC 1321 T table (md5.c:74-139).
-template <bool kLat = false, typename MsgFn>
+template <bool kLat = false, bool kX3 = true, typename MsgFn>
 __device__ __forceinline__ void compress(State& st, MsgFn M) {
   uint32_t a = st.a, b = st.b, c = st.c, d = st.d;
   MD5HIP_STEP(f1, a, b, c, d, M(0), 0xd76aa478u, 7);
@@ -112,6 +130,17 @@ __device__ __forceinline__ void compress(State& st, MsgFn M) {
   MD5HIP_STEP(f2, c, d, a, b, M(7), 0x676f02d9u, 14);
   MD5HIP_STEP(f2, b, c, d, a, M(12), 0x8d2a4c8au, 20);
 
+  if constexpr (kX3) {
+    // pair (a; b,c,d), (d; a,b,c): shared b ^ c; pair (c; d,a,b), (b; c,d,a): shared d ^ a
+    MD5HIP_STEP3_PAIR(a, d, b, c, M(5), 0xfffa3942u, 4, M(8), 0x8771f681u, 11);
+    MD5HIP_STEP3_PAIR(c, b, d, a, M(11), 0x6d9d6122u, 16, M(14), 0xfde5380cu, 23);
+    MD5HIP_STEP3_PAIR(a, d, b, c, M(1), 0xa4beea44u, 4, M(4), 0x4bdecfa9u, 11);
+    MD5HIP_STEP3_PAIR(c, b, d, a, M(7), 0xf6bb4b60u, 16, M(10), 0xbebfbc70u, 23);
+    MD5HIP_STEP3_PAIR(a, d, b, c, M(13), 0x289b7ec6u, 4, M(0), 0xeaa127fau, 11);
+    MD5HIP_STEP3_PAIR(c, b, d, a, M(3), 0xd4ef3085u, 16, M(6), 0x04881d05u, 23);
+    MD5HIP_STEP3_PAIR(a, d, b, c, M(9), 0xd9d4d039u, 4, M(12), 0xe6db99e5u, 11);
+    MD5HIP_STEP3_PAIR(c, b, d, a, M(15), 0x1fa27cf8u, 16, M(2), 0xc4ac5665u, 23);
+  } else {
   MD5HIP_STEP(f3, a, b, c, d, M(5), 0xfffa3942u, 4);
   MD5HIP_STEP(f3, d, a, b, c, M(8), 0x8771f681u, 11);
   MD5HIP_STEP(f3, c, d, a, b, M(11), 0x6d9d6122u, 16);
@@ -128,6 +157,7 @@ __device__ __forceinline__ void compress(State& st, MsgFn M) {
   MD5HIP_STEP(f3, d, a, b, c, M(12), 0xe6db99e5u, 11);
   MD5HIP_STEP(f3, c, d, a, b, M(15), 0x1fa27cf8u, 16);
   MD5HIP_STEP(f3, b, c, d, a, M(2), 0xc4ac5665u, 23);
+  }
 
   MD5HIP_STEP(f4, a, b, c, d, M(0), 0xf4292244u, 6);
   MD5HIP_STEP(f4, d, a, b, c, M(7), 0x432aff97u, 10);
@@ -153,11 +183,12 @@ __device__ __forceinline__ void compress(State& st, MsgFn M) {
 }
 
 #undef MD5HIP_STEP
+#undef MD5HIP_STEP3_PAIR
 
 // Compress 16 words held in four uint4 registers.
-template <bool kLat = false>
+template <bool kLat = false, bool kX3 = true>
 __device__ __forceinline__ void compress_regs(State& st, const uint4 (&w)[4]) {
-  compress<kLat>(st, [&](int i) __attribute__((always_inline)) -> uint32_t {
+  compress<kLat, kX3>(st, [&](int i) __attribute__((always_inline)) -> uint32_t {
     const uint4& q = w[i >> 2];
     switch (i & 3) {
       case 0: return q.x;
@@ -171,9 +202,9 @@ __device__ __forceinline__ void compress_regs(State& st, const uint4 (&w)[4]) {
 // The final padding block of a message whose length is a multiple of 64:
 // 0x80, 52 zero bytes, then the 64-bit bit count (md5.c:221-261).  All but
 // words 14/15 are compile-time constants, so M + K folds into one literal.
-template <bool kLat = false>
+template <bool kLat = false, bool kX3 = true>
 __device__ __forceinline__ void compress_pad_only(State& st, uint32_t bits_lo, uint32_t bits_hi) {
-  compress<kLat>(st, [&](int i) __attribute__((always_inline)) -> uint32_t {
+  compress<kLat, kX3>(st, [&](int i) __attribute__((always_inline)) -> uint32_t {
     return i == 0 ? 0x80u : i == 14 ? bits_lo : i == 15 ? bits_hi : 0u;
   });
 }

@@ -23,6 +23,7 @@
 //   kind 51   CRC-32 product body (crc32_fixed_xpose) with clock stamps
 //   kind 52,53 xpose1nt on a persistent grid with a work counter (5 / 4 WGs per CU)
 //   kind 54   xpose1nt without the peeled last stage (clamped re-read)
+//   kind 55,56 xpose1nt / compute only with the PLAIN round-3 form (kX3 off; A/B)
 //   kind 28-33 serial-chain latency with 64/32/16/1 active lanes (28-31), and
 //             64/32 with the latency-form step (32,33); n = waves, len = bytes
 //   kind 100+K VALU issue-rate probes (instruction K of diag_valu_rate)
@@ -368,6 +369,37 @@ diag_xpose1nt_nopeel(const uint8_t* __restrict__ base, uint64_t n, uint32_t len,
                                                           img + wave * 8192u, wave_first);
 }
 
+// Plain round-3 form (md5_core.h kX3 = false, the product before the xad
+// pairs): the product loader and the compute-only body, for A/B.
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5)))
+diag_xpose1nt_plain3(const uint8_t* __restrict__ base, uint64_t n, uint32_t len, uint64_t stride,
+                 uint4* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) uint8_t img[4 * 8192];
+  fixed_xpose_body<1, Md5Hasher<false, false>, 2>(base, n, len, stride, out, img);
+}
+
+__global__ void __launch_bounds__(256)
+diag_compute_plain3(uint64_t n, uint32_t nblocks, uint4* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) uint8_t rows[256 * 64];
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  uint32_t* my = reinterpret_cast<uint32_t*>(rows + threadIdx.x * 64);
+#pragma unroll
+  for (int k = 0; k < 16; ++k) my[k] = (uint32_t)i * 2654435761u + (uint32_t)k;
+  __builtin_amdgcn_wave_barrier();
+  State st = initial_state();
+  for (uint32_t b = 0; b < nblocks; ++b) {
+    uint4 w[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t q = ((uint32_t)k + b) & 3u;
+      w[k] = *reinterpret_cast<const uint4*>(rows + threadIdx.x * 64 + q * 16);
+    }
+    compress_regs<false, false>(st, w);
+  }
+  compress_pad_only(st, nblocks * 512u, 0u);
+  if (i < n) out[i] = make_uint4(st.a, st.b, st.c, st.d);
+}
+
 // Ideal streaming read of n*len bytes: grid-stride, 16 B per lane, consecutive
 // lanes consecutive addresses; xor-fold per lane.
 __global__ void __launch_bounds__(256)
@@ -509,6 +541,8 @@ extern "C" int md5diag_run(int kind, const void* base, uint64_t n, uint32_t len,
       hipLaunchKernelGGL(diag_xpose1nt_dyn, dim3(g), dim3(256), 0, s, b, n, len, stride, o, counter);
       break;
     }
+    case 55: hipLaunchKernelGGL(diag_xpose1nt_plain3, dim3(grid), dim3(256), 0, s, b, n, len, stride, o); break;
+    case 56: hipLaunchKernelGGL(diag_compute_plain3, dim3(grid), dim3(256), 0, s, n, len >> 6, o); break;
     case 54: hipLaunchKernelGGL(diag_xpose1nt_nopeel, dim3(grid), dim3(256), 0, s, b, n, len, stride, o); break;
     case 51: hipLaunchKernelGGL(diag_crc_clk, dim3(grid), dim3(256), 0, s, b, n, len, stride, o); break;
     case 50: hipLaunchKernelGGL(diag_xpose1nt_clk<FoldHasher>, dim3(grid), dim3(256), 0, s, b, n, len, stride, o); break;
