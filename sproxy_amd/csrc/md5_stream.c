@@ -40,43 +40,55 @@ static inline uint32_t get_le32(const unsigned char *p)
     return v;
 }
 
-/* One 64-byte block.  The four 16-step rounds are loops the compiler fully
- * unrolls (constant tables fold into immediates). */
+/* One 64-byte block.  Each step is written for a short serial chain (the
+ * host MD5 is one dependent chain, so latency, not throughput, bounds it):
+ * the parts of f that do not involve the newest word are computed off the
+ * chain, as is w + M + K, so the chain per step is f-tail -> add -> rotate ->
+ * add.  Round 2 adds its two disjoint halves (G = (b & d) + (c & ~d)) so only
+ * b & d waits for b.  The rounds are loops the compiler fully unrolls
+ * (constant tables fold into immediates). */
+#define STEP1(a, b, c, d, m, k, s) \
+    { uint32_t t_ = a + (m) + (k); t_ += d ^ (b & (c ^ d)); a = b + rol32(t_, s); }
+#define STEP2(a, b, c, d, m, k, s) \
+    { uint32_t t_ = a + (m) + (k) + (c & ~d); t_ += b & d; a = b + rol32(t_, s); }
+#define STEP3(a, b, c, d, m, k, s) \
+    { uint32_t t_ = a + (m) + (k); t_ += b ^ (c ^ d); a = b + rol32(t_, s); }
+#define STEP4(a, b, c, d, m, k, s) \
+    { uint32_t t_ = a + (m) + (k); t_ += c ^ (b | ~d); a = b + rol32(t_, s); }
+
 static void md5_blocks(uint32_t st[4], const unsigned char *p, size_t nblocks)
 {
     while (nblocks--) {
         uint32_t m[16];
         for (int i = 0; i < 16; i++) m[i] = get_le32(p + 4 * i);
-        uint32_t a = st[0], b = st[1], c = st[2], d = st[3], t;
+        uint32_t a = st[0], b = st[1], c = st[2], d = st[3];
 #pragma GCC unroll 16
         for (int i = 0; i < 16; i += 4) {
-            a = b + rol32(a + (d ^ (b & (c ^ d))) + m[i] + k_add[i], 7);
-            d = a + rol32(d + (c ^ (a & (b ^ c))) + m[i + 1] + k_add[i + 1], 12);
-            c = d + rol32(c + (b ^ (d & (a ^ b))) + m[i + 2] + k_add[i + 2], 17);
-            b = c + rol32(b + (a ^ (c & (d ^ a))) + m[i + 3] + k_add[i + 3], 22);
+            STEP1(a, b, c, d, m[i], k_add[i], 7);
+            STEP1(d, a, b, c, m[i + 1], k_add[i + 1], 12);
+            STEP1(c, d, a, b, m[i + 2], k_add[i + 2], 17);
+            STEP1(b, c, d, a, m[i + 3], k_add[i + 3], 22);
         }
 #pragma GCC unroll 16
         for (int i = 0; i < 16; i += 4) {
-            a = b + rol32(a + (c ^ (d & (b ^ c))) + m[(5 * i + 1) & 15] + k_add[16 + i], 5);
-            d = a + rol32(d + (b ^ (c & (a ^ b))) + m[(5 * i + 6) & 15] + k_add[17 + i], 9);
-            c = d + rol32(c + (a ^ (b & (d ^ a))) + m[(5 * i + 11) & 15] + k_add[18 + i], 14);
-            b = c + rol32(b + (d ^ (a & (c ^ d))) + m[(5 * i) & 15] + k_add[19 + i], 20);
+            STEP2(a, b, c, d, m[(5 * i + 1) & 15], k_add[16 + i], 5);
+            STEP2(d, a, b, c, m[(5 * i + 6) & 15], k_add[17 + i], 9);
+            STEP2(c, d, a, b, m[(5 * i + 11) & 15], k_add[18 + i], 14);
+            STEP2(b, c, d, a, m[(5 * i) & 15], k_add[19 + i], 20);
         }
 #pragma GCC unroll 16
         for (int i = 0; i < 16; i += 4) {
-            t = b ^ c;
-            a = b + rol32(a + (t ^ d) + m[(3 * i + 5) & 15] + k_add[32 + i], 4);
-            d = a + rol32(d + (t ^ a) + m[(3 * i + 8) & 15] + k_add[33 + i], 11);
-            t = d ^ a;
-            c = d + rol32(c + (t ^ b) + m[(3 * i + 11) & 15] + k_add[34 + i], 16);
-            b = c + rol32(b + (t ^ c) + m[(3 * i + 14) & 15] + k_add[35 + i], 23);
+            STEP3(a, b, c, d, m[(3 * i + 5) & 15], k_add[32 + i], 4);
+            STEP3(d, a, b, c, m[(3 * i + 8) & 15], k_add[33 + i], 11);
+            STEP3(c, d, a, b, m[(3 * i + 11) & 15], k_add[34 + i], 16);
+            STEP3(b, c, d, a, m[(3 * i + 14) & 15], k_add[35 + i], 23);
         }
 #pragma GCC unroll 16
         for (int i = 0; i < 16; i += 4) {
-            a = b + rol32(a + (c ^ (b | ~d)) + m[(7 * i) & 15] + k_add[48 + i], 6);
-            d = a + rol32(d + (b ^ (a | ~c)) + m[(7 * i + 7) & 15] + k_add[49 + i], 10);
-            c = d + rol32(c + (a ^ (d | ~b)) + m[(7 * i + 14) & 15] + k_add[50 + i], 15);
-            b = c + rol32(b + (d ^ (c | ~a)) + m[(7 * i + 21) & 15] + k_add[51 + i], 21);
+            STEP4(a, b, c, d, m[(7 * i) & 15], k_add[48 + i], 6);
+            STEP4(d, a, b, c, m[(7 * i + 7) & 15], k_add[49 + i], 10);
+            STEP4(c, d, a, b, m[(7 * i + 14) & 15], k_add[50 + i], 15);
+            STEP4(b, c, d, a, m[(7 * i + 21) & 15], k_add[51 + i], 21);
         }
         st[0] += a;
         st[1] += b;
@@ -85,6 +97,10 @@ static void md5_blocks(uint32_t st[4], const unsigned char *p, size_t nblocks)
         p += 64;
     }
 }
+#undef STEP1
+#undef STEP2
+#undef STEP3
+#undef STEP4
 
 void MD5Init(struct MD5Context *ctx)
 {
