@@ -44,7 +44,8 @@ enum md5hip_variant {
     MD5HIP_XPOSE1NT = 7,    /* xpose1 with non-temporal loads */
     MD5HIP_XPOSE2NT = 8,    /* xpose2 with non-temporal loads */
     MD5HIP_LDS128NT = 9,    /* lds128 with non-temporal loads */
-    MD5HIP_NUM_VARIANTS = 10
+    MD5HIP_XDMA1NT = 10,    /* xpose image filled by LDS-DMA (no VGPR staging), non-temporal */
+    MD5HIP_NUM_VARIANTS = 11
 };
 
 int md5hip_abi_version(void);

@@ -58,12 +58,12 @@ def main():
              "lds128": prod("lds128"), "compute_only": diag(0), "load_direct2": diag(1),
              "load_direct4": diag(2), "load_lds64": diag(3), "load_lds128": diag(4),
              "stream_read": diag(5), "xpose1": prod("xpose1"), "xpose2": prod("xpose2"),
-             "xpose1nt": prod("xpose1nt"), "xpose2nt": prod("xpose2nt"), "lds128nt": prod("lds128nt"),
+             "xpose1nt": prod("xpose1nt"), "xdma1nt": prod("xdma1nt"), "xpose2nt": prod("xpose2nt"), "lds128nt": prod("lds128nt"),
              "load_xpose1": diag(6), "load_xpose2": diag(7), "crc32": crc(),
              "load_direct2p": diag(8), "load_direct4p": diag(9), "direct2p": diag(10), "direct4p": diag(11),
              "crc_lane32u": diag(27),
              "x64nt": diag(38), "x64": diag(39), "d64nt": diag(44), "d64": diag(45),
-             "x2pairnt": diag(46), "x2pair": diag(47), "dyn5": diag(52), "dyn4": diag(53), "nopeel": diag(54), "plain3": diag(55), "comp_plain3": diag(56),
+             "x2pairnt": diag(46), "x2pair": diag(47), "dyn5": diag(52), "dyn4": diag(53), "nopeel": diag(54), "plain3": diag(55), "comp_plain3": diag(56), "xdmant": diag(57), "xdma": diag(58),
              "comp32": diag(40), "comp24": diag(41), "comp20": diag(42), "comp16": diag(43),
              "occ20": diag(34), "occ16": diag(35), "occ12": diag(36), "occ8": diag(37), "crc_shared8": crc("shared8"), "crc_lane32": crc("lane32"), "crc_lane16": crc("lane16"), "crc_xlane16": crc("xlane16"), "crc_xperm16": crc("xperm16"),
              "cp0": diag(20), "cp_sc0": diag(21), "cp_nt": diag(22), "cp_sc0nt": diag(23),

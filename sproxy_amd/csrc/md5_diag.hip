@@ -24,6 +24,7 @@
 //   kind 52,53 xpose1nt on a persistent grid with a work counter (5 / 4 WGs per CU)
 //   kind 54   xpose1nt without the peeled last stage (clamped re-read)
 //   kind 55,56 xpose1nt / compute only with the PLAIN round-3 form (kX3 off; A/B)
+//   kind 57,58 xpose image filled by LDS-DMA, one image per wave (nt / default)
 //   kind 28-33 serial-chain latency with 64/32/16/1 active lanes (28-31), and
 //             64/32 with the latency-form step (32,33); n = waves, len = bytes
 //   kind 100+K VALU issue-rate probes (instruction K of diag_valu_rate)
@@ -400,6 +401,72 @@ diag_compute_plain3(uint64_t n, uint32_t nblocks, uint4* __restrict__ out) {
   if (i < n) out[i] = make_uint4(st.a, st.b, st.c, st.d);
 }
 
+// xpose layout filled by LDS-DMA instead of through VGPRs: per 128-B stage,
+// 8 buffer_load_dwordx4 ... lds (8 rows x 128 B each, lane-linear
+// destination = the xpose image layout), one 8 KiB image per wave; the DMA of
+// stage s+1 is issued once this lane's reads of stage s have returned and
+// runs under stage s's compression.  Saves the 8 ds_write_b128 per stage and
+// the VGPR round trip of the data.
+template <int CP>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5)))
+diag_xdma(const uint8_t* __restrict__ base, uint64_t n, uint32_t len, uint64_t stride,
+          uint4* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds[4 * 8192];
+  Md5Hasher<false> h;
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  uint8_t* img = lds + wave * 8192u;
+  const uint64_t wave_first = ((uint64_t)blockIdx.x * blockDim.x) + wave * 64u;
+  if (wave_first >= n) return;
+  const uint64_t left = n - wave_first;
+  const uint32_t rows = left < 64 ? (uint32_t)left : 64u;
+  const __amdgpu_buffer_rsrc_t rsrc = uniform_rsrc(base + wave_first * stride);
+  uint32_t voff[8];
+#pragma unroll
+  for (int r = 0; r < 8; ++r) {
+    const uint32_t row = (uint32_t)r * 8u + (lane >> 3);
+    const uint32_t rc = row < rows ? row : rows - 1u;
+    const uint32_t part = (lane & 7u) ^ ((row >> 1) & 7u);
+    voff[r] = rc * (uint32_t)stride + part * 16u;
+  }
+  const uint32_t g = (lane >> 1) & 7u;
+  const uint32_t nfull = len >> 6;
+  const uint32_t nstage = nfull >> 1;
+  typename Md5Hasher<false>::State st = h.init();
+  auto issue = [&](uint32_t stg) __attribute__((always_inline)) {
+#pragma unroll
+    for (int r = 0; r < 8; ++r)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, img + r * 1024, 16, voff[r], stg * 128u, 0, CP);
+  };
+  if (nstage) {
+    issue(0);
+    for (uint32_t stg = 0; stg < nstage; ++stg) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      uint4 w[2][4];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const u32x4 v = *reinterpret_cast<const u32x4*>(img + lane * 128 + ((q ^ g) * 16));
+        w[q >> 2][q & 3] = make_uint4(v.x, v.y, v.z, v.w);
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if (stg + 1 < nstage) issue(stg + 1);
+      __builtin_amdgcn_sched_barrier(0);
+      h.block(st, w[0]);
+      h.block(st, w[1]);
+    }
+  }
+  const uint64_t i = wave_first + lane;
+  const uint64_t ci = lane < rows ? i : n - 1;
+  const uint8_t* chunk = base + ci * stride;
+  if (nfull & 1u) {
+    uint4 w[4];
+    load_block(w, reinterpret_cast<const uint4*>(chunk + ((uint64_t)(nfull - 1) << 6)));
+    h.block(st, w);
+  }
+  h.finish(st, chunk + ((uint64_t)nfull << 6), len & 63u, len);
+  if (lane < rows) h.store(out, i, st);
+}
+
 // Ideal streaming read of n*len bytes: grid-stride, 16 B per lane, consecutive
 // lanes consecutive addresses; xor-fold per lane.
 __global__ void __launch_bounds__(256)
@@ -543,6 +610,8 @@ extern "C" int md5diag_run(int kind, const void* base, uint64_t n, uint32_t len,
     }
     case 55: hipLaunchKernelGGL(diag_xpose1nt_plain3, dim3(grid), dim3(256), 0, s, b, n, len, stride, o); break;
     case 56: hipLaunchKernelGGL(diag_compute_plain3, dim3(grid), dim3(256), 0, s, n, len >> 6, o); break;
+    case 57: hipLaunchKernelGGL(diag_xdma<2>, dim3(grid), dim3(256), 0, s, b, n, len, stride, o); break;
+    case 58: hipLaunchKernelGGL(diag_xdma<0>, dim3(grid), dim3(256), 0, s, b, n, len, stride, o); break;
     case 54: hipLaunchKernelGGL(diag_xpose1nt_nopeel, dim3(grid), dim3(256), 0, s, b, n, len, stride, o); break;
     case 51: hipLaunchKernelGGL(diag_crc_clk, dim3(grid), dim3(256), 0, s, b, n, len, stride, o); break;
     case 50: hipLaunchKernelGGL(diag_xpose1nt_clk<FoldHasher>, dim3(grid), dim3(256), 0, s, b, n, len, stride, o); break;

@@ -322,6 +322,80 @@ __device__ __forceinline__ void fixed_xpose_body(const uint8_t* __restrict__ bas
 }
 
 
+// ---------------------------------------------------------------------------
+// Fixed-length, xpose image filled by LDS-DMA ("xdma"; the default).
+// The same 8 chunks x 128 B wave-instructions and the same LDS image layout
+// as the xpose kernels (lane-linear destination = row r*8 + lane/8, slot
+// lane%8 holding part (lane%8) ^ ((row>>1)&7)), but issued as
+// buffer_load_dwordx4 ... lds: the data skips the VGPRs and the 8
+// ds_write_b128 per stage.  One 8 KiB image per wave: once this lane's
+// ds_reads of stage s have returned, the DMA of stage s+1 is issued and runs
+// under stage s's compression.  The kernel is power-bound, so
+// the saved instructions and register traffic buy clock: 1.7 % faster.
+// Requires 64 * stride < 2^31 (checked by the launcher).
+// ---------------------------------------------------------------------------
+template <class H = Md5Hasher<false>, int CP = 2>
+__device__ __forceinline__ void fixed_xdma_body(const uint8_t* __restrict__ base, uint64_t n,
+                                                uint32_t len, uint64_t stride,
+                                                typename H::Out* __restrict__ out, uint8_t* lds) {
+  H h;
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  uint8_t* img = lds + wave * 8192u;
+  const uint64_t wave_first = ((uint64_t)blockIdx.x * blockDim.x) + wave * 64u;
+  if (wave_first >= n) return;
+  const uint64_t left = n - wave_first;
+  const uint32_t rows = left < 64 ? (uint32_t)left : 64u;
+  const __amdgpu_buffer_rsrc_t rsrc = uniform_rsrc(base + wave_first * stride);
+  uint32_t voff[8];
+#pragma unroll
+  for (int r = 0; r < 8; ++r) {
+    const uint32_t row = (uint32_t)r * 8u + (lane >> 3);
+    const uint32_t rc = row < rows ? row : rows - 1u;            // ragged last wave
+    const uint32_t part = (lane & 7u) ^ ((row >> 1) & 7u);       // source swizzle
+    voff[r] = rc * (uint32_t)stride + part * 16u;
+  }
+  const uint32_t g = (lane >> 1) & 7u;
+  const uint32_t nfull = len >> 6;
+  const uint32_t nstage = nfull >> 1;
+  typename H::State st = h.init();
+  auto issue = [&](uint32_t stg) __attribute__((always_inline)) {
+#pragma unroll
+    for (int r = 0; r < 8; ++r)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, img + r * 1024, 16, voff[r], stg * 128u, 0, CP);
+  };
+  if (nstage) {
+    issue(0);
+    for (uint32_t stg = 0; stg < nstage; ++stg) {
+      // hipcc does not order ds_read after an LDS-DMA into the same bytes, so
+      // wait explicitly; exactly one stage is in flight here
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      uint4 w[2][4];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const u32x4 v = *reinterpret_cast<const u32x4*>(img + lane * 128 + ((q ^ g) * 16));
+        w[q >> 2][q & 3] = make_uint4(v.x, v.y, v.z, v.w);
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // reads done before the refill
+      if (stg + 1 < nstage) issue(stg + 1);
+      __builtin_amdgcn_sched_barrier(0);
+      h.block(st, w[0]);
+      h.block(st, w[1]);
+    }
+  }
+  // leftover odd block, then the tail
+  const uint64_t i = wave_first + lane;
+  const uint64_t ci = lane < rows ? i : n - 1;
+  const uint8_t* chunk = base + ci * stride;
+  if (nfull & 1u) {
+    uint4 w[4];
+    load_block(w, reinterpret_cast<const uint4*>(chunk + ((uint64_t)(nfull - 1) << 6)));
+    h.block(st, w);
+  }
+  h.finish(st, chunk + ((uint64_t)nfull << 6), len & 63u, len);
+  if (lane < rows) h.store(out, i, st);
+}
+
 // Non-template entry points (hipcc mis-handles explicitly instantiated
 // __global__ templates that declare extern __shared__).
 __global__ void __launch_bounds__(256)
@@ -352,6 +426,13 @@ md5_fixed_xpose1nt(const uint8_t* __restrict__ base, uint64_t n, uint32_t len, u
                    uint4* __restrict__ out) {
   __shared__ __attribute__((aligned(16))) uint8_t img[4 * 8192];
   fixed_xpose_body<1, Md5Hasher<false>, 2>(base, n, len, stride, out, img);
+}
+
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5)))
+md5_fixed_xdma1nt(const uint8_t* __restrict__ base, uint64_t n, uint32_t len, uint64_t stride,
+                  uint4* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) uint8_t img[4 * 8192];
+  fixed_xdma_body<Md5Hasher<false>, 2>(base, n, len, stride, out, img);
 }
 
 __global__ void __launch_bounds__(256)

@@ -61,7 +61,7 @@ int env_int(const char* name, int lo, int hi, int dflt) {
 
 int default_variant() {
   static const int v = env_int("MD5HIP_VARIANT", 1, MD5HIP_NUM_VARIANTS,
-                               MD5HIP_XPOSE1NT);   // measured best, DESIGN.md
+                               MD5HIP_XDMA1NT);   // measured best, DESIGN.md §4
   return v;
 }
 
@@ -131,6 +131,7 @@ const char* md5hip_variant_name(int v) {
     case MD5HIP_XPOSE1: return "xpose1";
     case MD5HIP_XPOSE2: return "xpose2";
     case MD5HIP_XPOSE1NT: return "xpose1nt";
+    case MD5HIP_XDMA1NT: return "xdma1nt";
     case MD5HIP_XPOSE2NT: return "xpose2nt";
     case MD5HIP_LDS128NT: return "lds128nt";
     default: return "?";
@@ -234,11 +235,13 @@ int md5hip_digest_fixed_variant(const void* d_base, uint64_t n, uint32_t len, ui
     case MD5HIP_XPOSE1:
     case MD5HIP_XPOSE2:
     case MD5HIP_XPOSE1NT:
+    case MD5HIP_XDMA1NT:
     case MD5HIP_XPOSE2NT: {
       typedef void (*K)(const uint8_t*, uint64_t, uint32_t, uint64_t, uint4*);
       K k = variant == MD5HIP_XPOSE1 ? md5_fixed_xpose1
           : variant == MD5HIP_XPOSE2 ? md5_fixed_xpose2
-          : variant == MD5HIP_XPOSE1NT ? md5_fixed_xpose1nt : md5_fixed_xpose2nt;
+          : variant == MD5HIP_XPOSE1NT ? md5_fixed_xpose1nt
+          : variant == MD5HIP_XDMA1NT ? md5_fixed_xdma1nt : md5_fixed_xpose2nt;
       if (stride >= (1ull << 31) / 64) k = md5_fixed_direct<2, Md5Hasher<false>>;  // 32-bit buffer offsets
       hipLaunchKernelGGL(k, dim3((uint32_t)grid), dim3(kBlock), 0, s, base, n, len, stride, out);
       return launched();

@@ -28,10 +28,10 @@ except Exception:  # pragma: no cover
 
 MD5_DIGEST_SIZE = 16
 
-AUTO, DIRECT2, DIRECT4, LDS64, LDS128, XPOSE1, XPOSE2, XPOSE1NT, XPOSE2NT, LDS128NT = range(10)
+AUTO, DIRECT2, DIRECT4, LDS64, LDS128, XPOSE1, XPOSE2, XPOSE1NT, XPOSE2NT, LDS128NT, XDMA1NT = range(11)
 VARIANTS = {"auto": AUTO, "direct2": DIRECT2, "direct4": DIRECT4, "lds64": LDS64, "lds128": LDS128,
             "xpose1": XPOSE1, "xpose2": XPOSE2, "xpose1nt": XPOSE1NT, "xpose2nt": XPOSE2NT,
-            "lds128nt": LDS128NT}
+            "lds128nt": LDS128NT, "xdma1nt": XDMA1NT}
 
 
 # ---------------------------------------------------------------- per message
