@@ -1,0 +1,280 @@
+/*
+ * tests/c/netcache_site.c -- the netcache block-checksum call site of
+ * INTEGRATION.md §2 / §2a / §2e / §2g, compiled as plain C against
+ * include/md5hip.h and include/md5.h and linked with libmd5hip.so: no Python,
+ * no torch, exactly what sproxy's build would see.
+ *
+ * The netcache types are reduced to what the call site touches:
+ *   fc_blk_t   blkno + pages[i]->memory          (netcache/include/block.h:121, :143-146)
+ *   fc_inode_t object size, chunk_size, blockcrc  (netcache.h:262, :408-410)
+ *   blk_valid_len                                 (blk_io.c:377: last block is short)
+ * Pages are 16 KiB slots carved from one 4 KiB-aligned heap (bc_mgr.c:1260-1290)
+ * and handed to blocks in a scrambled order, so a block's pages are scattered.
+ *
+ * Checked against the oracle (oracle/md5_oracle.c, oracle/crc32_oracle.c,
+ * linked in as the checker only) over each block's gathered bytes:
+ *   1. MD5 per block through md5_batch_submit_iov
+ *   2. netcache CRC-32, whole block and fastcrc head^tail (§2a,
+ *      blk_io.c:408-424), stored into inode->blockcrc
+ *   3. md5hip_batch_verify_iov flags exactly one corrupted block (§2a,
+ *      the blk_io.c:693-703 EAGAIN policy input)
+ *   4. md5_batch_submit_iov_async + md5_batch_poll / md5_batch_wait (§2g)
+ *   5. zero-copy: md5hip_host_register of the heap, gather modes DEVICE,
+ *      DMA, AUTO (§2e)
+ *   6. md5hip_pool over device 0 listed twice (§2d)
+ *   7. MD5Init/Update/Final page by page (the per-message drop-in, §1)
+ *
+ * Exit 0 = all equal; 1 = a mismatch or error; 77 = no usable HIP device
+ * (md5hip_batcher_create returned -ENODEV: the batched entries fail loudly,
+ * they never fall back to the host).
+ */
+#include <errno.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <unistd.h>
+
+#include "md5.h"
+#include "md5hip.h"
+
+/* oracle (checker) */
+void oracle_md5(const void *data, uint64_t len, unsigned char digest[16]);
+uint32_t oracle_blk_crc(const void *data, uint64_t remained, uint32_t fastcrc);
+void oracle_xorshift_fill(void *dst, uint64_t nbytes, uint64_t seed);
+
+#define NC_PAGE_SIZE 16384u
+#define CHUNK_SIZE (4u * NC_PAGE_SIZE) /* netcache chunk_size 64 KiB */
+#define PAGES_PER_BLOCK (CHUNK_SIZE / NC_PAGE_SIZE)
+#define NBLK_MAX 96
+
+typedef struct { void *memory; } nc_page_t;
+typedef struct { uint32_t blkno; nc_page_t *pages[PAGES_PER_BLOCK]; } fc_blk_t;
+typedef struct {
+    uint64_t size;
+    uint32_t chunk_size;
+    uint32_t blockcrc[NBLK_MAX];
+} fc_inode_t;
+
+static long long blk_valid_len(const fc_inode_t *inode, const fc_blk_t *blk)
+{
+    long long off = (long long)blk->blkno * inode->chunk_size;
+    long long rem = (long long)inode->size - off;
+    return rem < (long long)inode->chunk_size ? rem : (long long)inode->chunk_size;
+}
+
+static int failures;
+#define CHECK(cond, ...)                                                   \
+    do {                                                                   \
+        if (!(cond)) {                                                     \
+            fprintf(stderr, "FAIL %s:%d: ", __FILE__, __LINE__);           \
+            fprintf(stderr, __VA_ARGS__);                                  \
+            fputc('\n', stderr);                                           \
+            failures++;                                                    \
+        }                                                                  \
+    } while (0)
+
+/* page list of every block -> segments + seg_first */
+static uint64_t blk_segments(const fc_inode_t *inode, fc_blk_t *const *blks, int nblk,
+                             struct md5hip_iov *segs, uint64_t *first)
+{
+    uint64_t ns = 0;
+    for (int b = 0; b < nblk; b++) {
+        long long remained = blk_valid_len(inode, blks[b]);
+        first[b] = ns;
+        for (int p = 0; remained > 0; p++) {
+            uint32_t take = remained < NC_PAGE_SIZE ? (uint32_t)remained : NC_PAGE_SIZE;
+            segs[ns].base = blks[b]->pages[p]->memory;
+            segs[ns].len = take;
+            ns++;
+            remained -= take;
+        }
+    }
+    first[nblk] = ns;
+    return ns;
+}
+
+/* the block's bytes, gathered on the host for the oracle */
+static void gather(const fc_inode_t *inode, const fc_blk_t *blk, unsigned char *dst)
+{
+    long long remained = blk_valid_len(inode, blk);
+    for (int p = 0; remained > 0; p++) {
+        uint32_t take = remained < NC_PAGE_SIZE ? (uint32_t)remained : NC_PAGE_SIZE;
+        memcpy(dst + (size_t)p * NC_PAGE_SIZE, blk->pages[p]->memory, take);
+        remained -= take;
+    }
+}
+
+int main(void)
+{
+    /* an object of 83 full 64 KiB blocks plus a 12,345-byte last block */
+    const int nblk = 84;
+    fc_inode_t inode;
+    memset(&inode, 0, sizeof inode);
+    inode.chunk_size = CHUNK_SIZE;
+    inode.size = (uint64_t)(nblk - 1) * CHUNK_SIZE + 12345u;
+
+    const int npages = nblk * (int)PAGES_PER_BLOCK;
+    const size_t heap_bytes = (size_t)npages * NC_PAGE_SIZE;
+    unsigned char *heap = NULL;
+    if (posix_memalign((void **)&heap, 4096, heap_bytes) != 0) return 1;
+    oracle_xorshift_fill(heap, heap_bytes, 0x6e63ull);
+
+    /* scatter: page slot k goes to position (k * 37) mod npages (37 is coprime to npages) */
+    static nc_page_t pages[NBLK_MAX * PAGES_PER_BLOCK];
+    static fc_blk_t blkstore[NBLK_MAX];
+    fc_blk_t *blks[NBLK_MAX];
+    for (int k = 0; k < npages; k++)
+        pages[k].memory = heap + (size_t)((k * 37) % npages) * NC_PAGE_SIZE;
+    for (int b = 0; b < nblk; b++) {
+        blkstore[b].blkno = (uint32_t)b;
+        for (unsigned p = 0; p < PAGES_PER_BLOCK; p++)
+            blkstore[b].pages[p] = &pages[b * PAGES_PER_BLOCK + p];
+        blks[b] = &blkstore[b];
+    }
+
+    static struct md5hip_iov segs[NBLK_MAX * PAGES_PER_BLOCK];
+    uint64_t first[NBLK_MAX + 1];
+    blk_segments(&inode, blks, nblk, segs, first);
+
+    /* expected values from the oracle over each block's gathered bytes */
+    static unsigned char want_md5[NBLK_MAX][16];
+    static uint32_t want_crc[NBLK_MAX], want_fast[NBLK_MAX];
+    unsigned char *tmp = malloc(CHUNK_SIZE);
+    if (!tmp) return 1;
+    for (int b = 0; b < nblk; b++) {
+        long long len = blk_valid_len(&inode, blks[b]);
+        gather(&inode, blks[b], tmp);
+        oracle_md5(tmp, (uint64_t)len, want_md5[b]);
+        want_crc[b] = oracle_blk_crc(tmp, (uint64_t)len, 0);
+        want_fast[b] = oracle_blk_crc(tmp, (uint64_t)len, 4096);
+    }
+
+    md5hip_batcher *t_md5 = NULL;
+    int rc = md5hip_batcher_create(0, 64u << 20, 3, &t_md5); /* INTEGRATION §2 */
+    if (rc == -ENODEV) {
+        printf("netcache_site: no usable HIP device (md5hip_batcher_create = %d)\n", rc);
+        return 77;
+    }
+    CHECK(rc == 0 && t_md5, "md5hip_batcher_create = %d", rc);
+    if (rc != 0) return 1;
+
+    /* 1. MD5 per block */
+    static unsigned char digest[NBLK_MAX][16];
+    memset(digest, 0, sizeof digest);
+    rc = md5_batch_submit_iov(t_md5, segs, first, (uint64_t)nblk, &digest[0][0]);
+    CHECK(rc == 0, "md5_batch_submit_iov = %d", rc);
+    for (int b = 0; b < nblk; b++)
+        CHECK(memcmp(digest[b], want_md5[b], 16) == 0, "MD5 block %d", b);
+
+    /* 2. netcache CRC-32, whole block then fastcrc window */
+    uint32_t crc[NBLK_MAX];
+    rc = md5hip_batcher_set_digest(t_md5, MD5HIP_DIGEST_CRC32, 0);
+    CHECK(rc == 0, "set_digest(CRC32, 0) = %d", rc);
+    rc = md5_batch_submit_iov(t_md5, segs, first, (uint64_t)nblk, (unsigned char *)crc);
+    CHECK(rc == 0, "CRC submit = %d", rc);
+    for (int b = 0; b < nblk; b++) {
+        CHECK(crc[b] == want_crc[b], "CRC block %d: %08x vs %08x", b, crc[b], want_crc[b]);
+        inode.blockcrc[blks[b]->blkno] = crc[b]; /* dm_update_block_crc_nolock */
+    }
+    rc = md5hip_batcher_set_digest(t_md5, MD5HIP_DIGEST_CRC32, 4096);
+    CHECK(rc == 0, "set_digest(CRC32, 4096) = %d", rc);
+    rc = md5_batch_submit_iov(t_md5, segs, first, (uint64_t)nblk, (unsigned char *)crc);
+    CHECK(rc == 0, "fastcrc submit = %d", rc);
+    for (int b = 0; b < nblk; b++)
+        CHECK(crc[b] == want_fast[b], "fastcrc block %d: %08x vs %08x", b, crc[b], want_fast[b]);
+
+    /* 3. verify against the stored array with one corrupted block */
+    rc = md5hip_batcher_set_digest(t_md5, MD5HIP_DIGEST_CRC32, 0);
+    CHECK(rc == 0, "set_digest = %d", rc);
+    uint32_t want[NBLK_MAX];
+    unsigned char ok[NBLK_MAX];
+    for (int b = 0; b < nblk; b++) want[b] = inode.blockcrc[blks[b]->blkno];
+    unsigned char *victim = (unsigned char *)blks[5]->pages[2]->memory + 777;
+    *victim ^= 0x40;
+    rc = md5hip_batch_verify_iov(t_md5, segs, first, (uint64_t)nblk, want, ok);
+    CHECK(rc == 1, "verify mismatches = %d, want 1", rc);
+    for (int b = 0; b < nblk; b++) CHECK(ok[b] == (b != 5), "verify ok[%d] = %d", b, ok[b]);
+    *victim ^= 0x40;
+    rc = md5hip_batch_verify_iov(t_md5, segs, first, (uint64_t)nblk, want, ok);
+    CHECK(rc == 0, "verify after restore = %d", rc);
+
+    /* 4. asynchronous submit: two block vectors in flight, poll then wait */
+    rc = md5hip_batcher_set_digest(t_md5, MD5HIP_DIGEST_MD5, 0);
+    CHECK(rc == 0, "set_digest(MD5) = %d", rc);
+    static unsigned char da[NBLK_MAX][16], db[NBLK_MAX][16];
+    memset(da, 0, sizeof da);
+    memset(db, 0, sizeof db);
+    const int half = nblk / 2;
+    uint64_t t1 = 0, t2 = 0;
+    uint64_t first_b[NBLK_MAX + 1];
+    for (int b = half; b <= nblk; b++) first_b[b - half] = first[b] - first[half];
+    rc = md5_batch_submit_iov_async(t_md5, segs, first, (uint64_t)half, &da[0][0], &t1);
+    CHECK(rc == 0, "submit_iov_async(1) = %d", rc);
+    rc = md5_batch_submit_iov_async(t_md5, segs + first[half], first_b, (uint64_t)(nblk - half),
+                                    &db[0][0], &t2);
+    CHECK(rc == 0, "submit_iov_async(2) = %d", rc);
+    int polled = 0;
+    for (int spin = 0; spin < 200000 && (polled = md5_batch_poll(t_md5, t1)) == 0; spin++)
+        usleep(50); /* bounded: ~10 s */
+    CHECK(polled == 1, "md5_batch_poll(t1) = %d", polled);
+    rc = md5_batch_wait(t_md5, t2);
+    CHECK(rc == 0, "md5_batch_wait(t2) = %d", rc);
+    for (int b = 0; b < half; b++) CHECK(memcmp(da[b], want_md5[b], 16) == 0, "async A %d", b);
+    for (int b = half; b < nblk; b++)
+        CHECK(memcmp(db[b - half], want_md5[b], 16) == 0, "async B %d", b);
+
+    /* 5. zero-copy: register the page heap, every gather mode */
+    rc = md5hip_host_register(heap, heap_bytes);
+    CHECK(rc == 0, "md5hip_host_register = %d", rc);
+    const int modes[3] = {MD5HIP_GATHER_DEVICE, MD5HIP_GATHER_DMA, MD5HIP_GATHER_AUTO};
+    for (int k = 0; k < 3; k++) {
+        rc = md5hip_batcher_set_gather(t_md5, modes[k]);
+        CHECK(rc == 0, "set_gather(%d) = %d", modes[k], rc);
+        memset(digest, 0, sizeof digest);
+        rc = md5_batch_submit_iov(t_md5, segs, first, (uint64_t)nblk, &digest[0][0]);
+        CHECK(rc == 0, "zero-copy submit mode %d = %d", modes[k], rc);
+        for (int b = 0; b < nblk; b++)
+            CHECK(memcmp(digest[b], want_md5[b], 16) == 0, "zero-copy mode %d block %d", modes[k], b);
+    }
+    md5hip_batcher_destroy(t_md5);
+    rc = md5hip_host_unregister(heap);
+    CHECK(rc == 0, "md5hip_host_unregister = %d", rc);
+
+    /* 6. pool over device 0 listed twice: each half writes its own slice */
+    md5hip_pool *pool = NULL;
+    const int devs[2] = {0, 0};
+    rc = md5hip_pool_create(devs, 2, 64u << 20, 3, &pool);
+    CHECK(rc == 0 && pool, "md5hip_pool_create = %d", rc);
+    if (rc == 0) {
+        CHECK(md5hip_pool_ndev(pool) == 2, "pool ndev %d", md5hip_pool_ndev(pool));
+        memset(digest, 0, sizeof digest);
+        rc = md5hip_pool_submit_iov(pool, segs, first, (uint64_t)nblk, &digest[0][0]);
+        CHECK(rc == 0, "md5hip_pool_submit_iov = %d", rc);
+        for (int b = 0; b < nblk; b++)
+            CHECK(memcmp(digest[b], want_md5[b], 16) == 0, "pool block %d", b);
+        md5hip_pool_destroy(pool);
+    }
+
+    /* 7. per-message drop-in, one MD5Update per page (md5.h:41-51) */
+    for (int b = 0; b < nblk; b += 41) {
+        struct MD5Context ctx;
+        unsigned char d[MD5_DIGEST_SIZE];
+        MD5Init(&ctx);
+        for (uint64_t s = first[b]; s < first[b + 1]; s++)
+            MD5Update(&ctx, segs[s].base, segs[s].len);
+        MD5Final(d, &ctx);
+        CHECK(memcmp(d, want_md5[b], 16) == 0, "MD5Init/Update/Final block %d", b);
+    }
+
+    free(tmp);
+    free(heap);
+    if (failures) {
+        fprintf(stderr, "netcache_site: %d failure(s)\n", failures);
+        return 1;
+    }
+    printf("netcache_site ok: %d blocks (%llu bytes, %d pages scattered), MD5 / CRC-32 / fastcrc / "
+           "verify / async / zero-copy x3 / pool / MD5Init-Update-Final bit-exact vs oracle\n",
+           nblk, (unsigned long long)inode.size, npages);
+    return 0;
+}

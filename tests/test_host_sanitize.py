@@ -34,8 +34,10 @@ def asan_run():
            os.path.join(gen.REPO, "tests", "c", "host_abi_check.c")] + \
           [os.path.join(CSRC, s) for s in SRCS] + ["-lpthread", "-o", exe]
     subprocess.run(cmd, check=True, capture_output=True, text=True)
-    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=1")
-    env.pop("LD_PRELOAD", None)
+    # verify_asan_link_order=0: the environment may preload other libraries
+    # ahead of the ASan runtime; the environment itself is passed unchanged
+    env = dict(os.environ,
+               ASAN_OPTIONS="detect_leaks=1:abort_on_error=1:verify_asan_link_order=0")
     out = subprocess.run([exe], capture_output=True, text=True, env=env, timeout=120)
     assert out.returncode == 0, out.stderr[-2000:]
     return [ln.split() for ln in out.stdout.splitlines()]
