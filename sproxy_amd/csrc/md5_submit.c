@@ -381,6 +381,69 @@ static void src_copy(const struct chunk_src *s, uint64_t i, unsigned char *dst)
     }
 }
 
+/* Host gather of one slice: chunks [first, first + m) into the pinned
+ * staging at sl->h_off[].  One thread's memcpy from pageable memory into
+ * pinned staging runs ~15 GB/s (zero-copy table), well below
+ * the PCIe H2D rate, so a large slice is cut by bytes into parts copied by
+ * MD5HIP_GATHER_THREADS threads (default 4; the calling thread copies the
+ * first part).  Threads are started per slice: a slice worth splitting
+ * (>= 8 MiB) takes milliseconds to copy, a pthread_create microseconds. */
+struct gather_part {
+    const struct chunk_src *src;
+    uint64_t first, jlo, jhi;
+    const uint64_t *off;
+    unsigned char *dst;
+};
+
+static void *gather_run(void *arg)
+{
+    const struct gather_part *p = arg;
+    for (uint64_t j = p->jlo; j < p->jhi; j++) src_copy(p->src, p->first + j, p->dst + p->off[j]);
+    return NULL;
+}
+
+static pthread_once_t g_gather_once = PTHREAD_ONCE_INIT;
+static int g_gather_threads = 4;
+
+static void gather_threads_init(void)
+{
+    const char *e = getenv("MD5HIP_GATHER_THREADS");
+    if (e && *e) {
+        const int t = atoi(e);
+        g_gather_threads = t < 1 ? 1 : t > 32 ? 32 : t;
+    }
+}
+
+#define GATHER_SPLIT_MIN (8ull << 20)   /* bytes per slice before it is split */
+#define GATHER_PART_MIN (2ull << 20)    /* and at least this many bytes per part */
+
+static void gather_slice(const struct chunk_src *src, uint64_t first, uint64_t m,
+                         const uint64_t *off, unsigned char *dst, uint64_t used)
+{
+    pthread_once(&g_gather_once, gather_threads_init);
+    uint64_t T = (uint64_t)g_gather_threads;
+    if (used < GATHER_SPLIT_MIN) T = 1;
+    if (T > used / GATHER_PART_MIN) T = used / GATHER_PART_MIN ? used / GATHER_PART_MIN : 1;
+    if (T > m) T = m ? m : 1;
+    struct gather_part part[32];
+    pthread_t tid[32];
+    int started[32] = {0};
+    uint64_t j = 0;
+    for (uint64_t t = 0; t < T; t++) {      /* part t: chunks whose offset < (t+1) * used / T */
+        const uint64_t lim = t + 1 == T ? UINT64_MAX : (t + 1) * used / T;
+        part[t] = (struct gather_part){src, first, j, j, off, dst};
+        while (j < m && off[j] < lim) j++;
+        part[t].jhi = j;
+    }
+    for (uint64_t t = 1; t < T; t++)
+        started[t] = pthread_create(&tid[t], NULL, gather_run, &part[t]) == 0;
+    gather_run(&part[0]);
+    for (uint64_t t = 1; t < T; t++) {
+        if (started[t]) pthread_join(tid[t], NULL);
+        else gather_run(&part[t]);           /* no thread: copy it here */
+    }
+}
+
 /* async == 0: returns once every digest is in `digests`.  async != 0:
  * returns once the host gather is done (the caller's buffers are free again,
  * except in the zero-copy modes); *ticket names the submission for
@@ -446,8 +509,6 @@ static int submit_gather(md5hip_batcher *b, const struct chunk_src *src, uint64_
                     }
                     at += len;
                 }
-            } else {
-                src_copy(src, i, sl->h_data + used);
             }
             sl->h_off[m] = used;
             sl->h_len[m] = (uint32_t)L;
@@ -456,6 +517,7 @@ static int submit_gather(md5hip_batcher *b, const struct chunk_src *src, uint64_
             i++;
         }
         if (zc) pthread_rwlock_unlock(&g_reg_lock);
+        else gather_slice(src, first, m, sl->h_off, sl->h_data, used);
         if ((rc = slot_launch(b, sl, m, used ? used : 16, zc ? nseg : 0, ndma,
                               digests + (size_t)b->dsz * first)))
             return rc;
