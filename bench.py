@@ -275,13 +275,22 @@ def run_c3(a, rank, world):
     s_wall = max_over_ranks(time.perf_counter() - t0, world, COLL_DEVICE)
     barrier(world)
     ok = all(torch.equal(o, out) for o in outs[:min(ns, a.steps)])
+    # imbalance vs uniform -- the same payload bytes of the
+    # same arena hashed as uniform 16 KiB chunks by the fixed-length kernel
+    n_u = int(payload) // 16384
+    dig_u = torch.empty((n_u, 16), dtype=torch.uint8, device="cuda")
+    _, u_ms = timed_steps(lambda: m.digest_fixed(data, n_u, 16384, out=dig_u), max(5, a.steps // 2),
+                          a.warmup, world)
+    del dig_u
     return {"metric": "device-resident MD5 GiB/s, mixed 4 KiB-1 MiB chunks (C3)",
             "value": round(value, 2), "unit": "GiB/s", "n_gpus": world, "steps": a.steps,
             "warmup": a.warmup, "ms_per_step": round(wall_max / a.steps * 1e3, 4),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32",
             "data": "synthetic", "config": {"workload": "C3 mixed lengths", "chunks": int(lens.size),
                                             "payload_bytes": int(payload),
-                                            "longest": int(lens.max()), "plan_ms": round(plan_ms, 3)},
+                                            "longest": int(lens.max()), "plan_ms": round(plan_ms, 3),
+                                            "uniform_16k_ms": round(u_ms, 4),
+                                            "imbalance_vs_uniform": round(dev_ms / u_ms, 3)},
             "roofline": {"bound": "hbm", "achieved": round(payload / (dev_ms * 1e-3) / 1e9, 1),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(payload / (dev_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),

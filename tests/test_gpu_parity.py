@@ -338,6 +338,41 @@ def test_batcher_submit_iov_pages(cuda):
     assert np.array_equal(got, want)
 
 
+def test_batcher_threaded_host_gather(cuda):
+    """Slices of >= 8 MiB are gathered into pinned staging on several threads
+    (MD5HIP_GATHER_THREADS, default 4), each copying a byte range of the
+    slice's chunks: page-list blocks of mixed sizes (ragged last pages, empty
+    blocks) and flat buffers over 24 MiB slices, MD5 and CRC-32, against the
+    oracle."""
+    rng = np.random.default_rng(31)
+    page = 16384
+    heap = gen.xorshift_array(6000 * page, seed=4242)
+    perm = rng.permutation(6000)
+    blocks, joined, k = [], [], 0
+    while k < 5800:
+        npages = int(rng.integers(1, 65))
+        tail = int(rng.integers(0, page + 1)) if rng.integers(0, 4) == 0 else page
+        ids = perm[k:k + npages]
+        k += npages
+        pages = [heap[i * page:(i + 1) * page] for i in ids[:-1]]
+        pages.append(heap[ids[-1] * page:ids[-1] * page + tail])
+        if rng.integers(0, 50) == 0:
+            pages = []
+        blocks.append(pages)
+        joined.append(b"".join(p.tobytes() for p in pages))
+    blob = b"".join(joined) + b"\0"
+    offs = np.cumsum([0] + [len(j) for j in joined[:-1]])
+    lens = [len(j) for j in joined]
+    want = gen.oracle_digests(np.frombuffer(blob, dtype=np.uint8), offs, lens)
+    with m.Batcher(device=0, slice_bytes=24 << 20, nslots=3) as bt:
+        assert np.array_equal(bt.submit_iov(blocks), want)
+        assert np.array_equal(bt.submit(joined), want)
+        bt.set_digest(m.Batcher.CRC32, 0)
+        crcs = bt.submit(joined).view("<u4").ravel()
+    want_crc = gen.oracle_crc32_batch(np.frombuffer(blob, dtype=np.uint8), offs, lens)
+    assert np.array_equal(crcs, want_crc)
+
+
 def test_batcher_crc32_and_verify(cuda):
     """The block-checksum call site end to end: a batcher in netcache CRC-32
     mode (fastcrc window) and the batched verify with a corrupted block."""
@@ -450,6 +485,23 @@ def test_huge_stride_and_large_chunks(cuda):
         assert np.array_equal(got, gen.oracle_digests(arena, offs, lens)), dv
     got = m.crc32_desc(da, t_off, t_len).cpu().numpy().view(np.uint32)
     assert np.array_equal(got, gen.oracle_crc32_batch(arena, offs, lens))
+
+
+def test_chunk_past_512mib_bit_count_high_word(cuda):
+    """A chunk of 2^29 + 123 bytes: its bit count no longer fits 32 bits, so
+    the length words of the final block carry bits[1] = 1 (md5.c:179-182,
+    :258-259).  One lane hashes it as one 8.4 M-compression chain (~5 s),
+    through the fixed entry (a stride this large takes the lane-direct
+    kernel) and the descriptor entry at an odd offset."""
+    L = (1 << 29) + 123
+    buf = gen.xorshift_array(L + 64, seed=4099)
+    want = gen.oracle_digests(buf, [0], [L])
+    d = _dev(buf, cuda)
+    assert np.array_equal(m.digest_fixed(d, 1, L, (L + 15) // 16 * 16).cpu().numpy(), want)
+    want_odd = gen.oracle_digests(buf, [7], [L - 7])
+    got = m.digest_desc(d, torch.tensor([7], dtype=torch.int64, device=cuda),
+                        torch.tensor([L - 7], dtype=torch.int32, device=cuda)).cpu().numpy()
+    assert np.array_equal(got, want_odd)
 
 
 def test_zero_copy_gather_modes(cuda):
