@@ -282,6 +282,17 @@ def run_c3(a, rank, world):
     _, u_ms = timed_steps(lambda: m.digest_fixed(data, n_u, 16384, out=dig_u), max(5, a.steps // 2),
                           a.warmup, world)
     del dig_u
+    # the bound of one mixed batch: each chunk is one serial chain on one lane
+    # (md5.c:204-210, 64 dependent steps per block), so the batch ends no
+    # earlier than its longest chunks -- timed alone (every chunk of the
+    # maximum length, same kernel; one lone chunk would understate the chip's
+    # clock, which drops when a single wave is active)
+    il = np.flatnonzero(lens == lens.max())
+    d_off1 = torch.from_numpy(offs[il]).cuda()
+    d_len1 = torch.from_numpy(lens[il].astype(np.int32)).cuda()
+    dig1 = torch.empty((il.size, 16), dtype=torch.uint8, device="cuda")
+    _, chain_ms = timed_steps(lambda: m.digest_desc(data, d_off1, d_len1, out=dig1), 5, 2, world)
+    del dig1
     return {"metric": "device-resident MD5 GiB/s, mixed 4 KiB-1 MiB chunks (C3)",
             "value": round(value, 2), "unit": "GiB/s", "n_gpus": world, "steps": a.steps,
             "warmup": a.warmup, "ms_per_step": round(wall_max / a.steps * 1e3, 4),
@@ -294,7 +305,12 @@ def run_c3(a, rank, world):
             "roofline": {"bound": "hbm", "achieved": round(payload / (dev_ms * 1e-3) / 1e9, 1),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(payload / (dev_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-                         "traffic": None},
+                         "traffic": None,
+                         "longest_alone_ms": round(chain_ms, 4),
+                         "n_longest": int(il.size),
+                         "frac_of_longest_alone": round(chain_ms / dev_ms, 4),
+                         "note": "one batch ends with its longest chunks' serial chains "
+                                 "(longest_alone_ms: those chunks hashed alone); see streamed"},
             "streamed": {"streams": ns, "value": round(payload * world * a.steps / s_wall / GIB, 2),
                          "unit": "GiB/s", "ms_per_batch": round(s_wall / a.steps * 1e3, 4),
                          "digests_equal_single": ok,
