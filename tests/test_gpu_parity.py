@@ -7,6 +7,9 @@ Small sizes are compared digest by digest; at BASELINE.json's full size
 (b) every kernel variant producing the identical 16 MiB digest array
 (checksum of checksums).
 """
+import ctypes
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -502,6 +505,41 @@ def test_chunk_past_512mib_bit_count_high_word(cuda):
     got = m.digest_desc(d, torch.tensor([7], dtype=torch.int64, device=cuda),
                         torch.tensor([L - 7], dtype=torch.int32, device=cuda)).cpu().numpy()
     assert np.array_equal(got, want_odd)
+
+
+REF_LIB = os.path.join(gen.REPO, "oracle", "_ref", "libmd5_ref.so")
+
+
+@pytest.mark.skipif(not os.path.exists(REF_LIB), reason="oracle/_ref not built")
+def test_gpu_equals_reference_md5c_build(cuda):
+    """North-star check without the restatement in between: the reference
+    md5.c itself (compiled where it lies, oracle/_ref/libmd5_ref.so; it travels
+    with the tree) digests the same inputs as the product kernels -- 1,000
+    random-length chunks at random 16-B offsets (descriptor kernel) and 4,096
+    x 16 KiB (fixed kernel, the C2 shape)."""
+    ref = ctypes.CDLL(REF_LIB)
+    rng = np.random.default_rng(20261016)
+
+    def md5c(view):
+        ctx = ctypes.create_string_buffer(88)
+        ref.MD5Init(ctx)
+        ref.MD5Update(ctx, ctypes.c_void_p(view.ctypes.data), ctypes.c_uint(view.size))
+        out = (ctypes.c_ubyte * 16)()
+        ref.MD5Final(out, ctx)
+        return bytes(out)
+
+    lens = [int(x) for x in rng.integers(0, 200000, 1000)]
+    offs, total = gen.pack_offsets(lens, align=16)
+    buf = gen.xorshift_array(total + 64, seed=606)
+    want = [md5c(buf[o:o + L]) for o, L in zip(offs, lens)]
+    got = m.digest_desc(_dev(buf, cuda), torch.tensor(offs, dtype=torch.int64, device=cuda),
+                        torch.tensor(lens, dtype=torch.int32, device=cuda),
+                        _dev(m.plan_order(lens).astype(np.int32), cuda)).cpu().numpy()
+    assert [bytes(x) for x in got] == want
+    n, L = 4096, 16384
+    fx = gen.xorshift_array(n * L, seed=607)
+    got = m.digest_fixed(_dev(fx, cuda), n, L).cpu().numpy()
+    assert [bytes(x) for x in got] == [md5c(fx[i * L:(i + 1) * L]) for i in range(n)]
 
 
 def test_zero_copy_gather_modes(cuda):
