@@ -83,7 +83,9 @@ enum md5hip_desc_variant {
                                waves with an unaligned chunk fall back to LANE */
     MD5HIP_DESC_HYBRID = 3, /* XPOSE, but the first waves (one per CU, env MD5HIP_DESC_NLONG)
                                go lane-direct when they hold a chunk >= 256 KiB */
-    MD5HIP_DESC_NUM_VARIANTS = 4
+    MD5HIP_DESC_XDMA = 4,   /* XPOSE with the image filled by LDS-DMA (no VGPR staging);
+                               the default */
+    MD5HIP_DESC_NUM_VARIANTS = 5
 };
 int md5hip_digest_desc_variant(const void *d_base, const uint64_t *d_offsets,
                                const uint32_t *d_lens, const uint32_t *d_order, uint64_t n,

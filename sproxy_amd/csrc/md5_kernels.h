@@ -591,7 +591,12 @@ md5_desc(const uint8_t* __restrict__ base, const uint64_t* __restrict__ offs,
 // kHalf: 4 KiB half image (rows 0-31, then rows 32-63, as xpose_half_group) so
 // a hasher with large LDS tables fits beside 16 waves' images; `first` is the
 // wave's first position in `order` (< n), the hasher is set up by the caller.
-template <int CP, class H, uint32_t kLong = 0, int D = 1, bool kHalf = false, bool kPeel = true>
+// kDma (full image, D = 1): the 8 row loads of a stage are LDS-DMA
+// (global_load_lds_dwordx4 from the same per-row addresses) straight into the
+// image, as fixed_xdma_body: no VGPR staging, no ds_write; the DMA of stage
+// s+1 is issued once this wave's row reads of stage s have returned.
+template <int CP, class H, uint32_t kLong = 0, int D = 1, bool kHalf = false, bool kPeel = true,
+          bool kDma = false>
 __device__ __forceinline__ void desc_xpose_group(H& h, const uint8_t* __restrict__ base,
                                                  const uint64_t* __restrict__ offs,
                                                  const uint32_t* __restrict__ lens,
@@ -690,6 +695,29 @@ __device__ __forceinline__ void desc_xpose_group(H& h, const uint8_t* __restrict
         h.block(st, w[1]);
       }
     };
+    if constexpr (kDma) {
+      static_assert(D == 1 && !kHalf, "LDS-DMA image: one full 8 KiB stage");
+      auto issue = [&](uint32_t stg) __attribute__((always_inline)) {
+#pragma unroll
+        for (int r = 0; r < 8; ++r)
+          __builtin_amdgcn_global_load_lds(rptr[r] + (min(stg, rlast[r]) << 7), img + r * 1024,
+                                           16, 0, CP);
+      };
+      issue(0);
+      for (uint32_t stg = 0; stg < smax; ++stg) {
+        // hipcc does not order ds_read after an LDS-DMA into the same bytes
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        uint4 w[2][4];
+        read_row(w);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // reads done before the refill
+        if (stg + 1 < smax) issue(stg + 1);
+        __builtin_amdgcn_sched_barrier(0);
+        if (stg < nst) {
+          h.block(st, w[0]);
+          h.block(st, w[1]);
+        }
+      }
+    } else {
     // D-stage register ring (2*D blocks of prefetch per lane)
     const uint32_t lasts = smax - 1;
     u32x4 R[D][8];
@@ -708,6 +736,7 @@ __device__ __forceinline__ void desc_xpose_group(H& h, const uint8_t* __restrict
       for (int j = 0; j < D - 1; ++j)
         if (stg + j < smax) consume(R[j], stg + j, lasts);
     }
+    }
   }
   if (live) {
     if (nfull & 1u) {
@@ -720,7 +749,7 @@ __device__ __forceinline__ void desc_xpose_group(H& h, const uint8_t* __restrict
   }
 }
 
-template <int CP, class H = Md5Hasher<true>, uint32_t kLong = 0, int D = 1>
+template <int CP, class H = Md5Hasher<true>, uint32_t kLong = 0, int D = 1, bool kDma = false>
 __device__ __forceinline__ void desc_xpose_body(const uint8_t* __restrict__ base,
                                                 const uint64_t* __restrict__ offs,
                                                 const uint32_t* __restrict__ lens,
@@ -730,7 +759,8 @@ __device__ __forceinline__ void desc_xpose_body(const uint8_t* __restrict__ base
   H h;
   const uint64_t first = ((uint64_t)blockIdx.x * blockDim.x) + (threadIdx.x & ~63u);
   if (first >= n) return;
-  desc_xpose_group<CP, H, kLong, D>(h, base, offs, lens, order, n, first, out, img, nlong);
+  desc_xpose_group<CP, H, kLong, D, false, true, kDma>(h, base, offs, lens, order, n, first, out,
+                                                      img, nlong);
 }
 
 __global__ void __launch_bounds__(64)
@@ -739,6 +769,14 @@ md5_desc_xpose(const uint8_t* __restrict__ base, const uint64_t* __restrict__ of
                uint4* __restrict__ out) {
   __shared__ __attribute__((aligned(16))) uint8_t img[8192];
   desc_xpose_body<2>(base, offs, lens, order, n, out, img);
+}
+
+__global__ void __launch_bounds__(64)
+md5_desc_xdma(const uint8_t* __restrict__ base, const uint64_t* __restrict__ offs,
+              const uint32_t* __restrict__ lens, const uint32_t* __restrict__ order, uint64_t n,
+              uint4* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) uint8_t img[8192];
+  desc_xpose_body<2, Md5Hasher<true>, 0, 1, true>(base, offs, lens, order, n, out, img);
 }
 
 __global__ void __launch_bounds__(64)

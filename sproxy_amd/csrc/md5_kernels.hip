@@ -140,7 +140,7 @@ const char* md5hip_variant_name(int v) {
 
 int default_desc_variant() {
   static const int v = env_int("MD5HIP_DESC_VARIANT", 1, MD5HIP_DESC_NUM_VARIANTS,
-                               MD5HIP_DESC_XPOSE);
+                               MD5HIP_DESC_XDMA);    // DESIGN.md §5 (profiles/r01_desc_xdma_ab.json)
   return v;
 }
 
@@ -177,10 +177,10 @@ int md5hip_digest_desc_variant(const void* d_base, const uint64_t* d_offsets,
                        desc_nlong());
     return launched();
   }
-  if (variant == MD5HIP_DESC_XPOSE) {
+  if (variant == MD5HIP_DESC_XPOSE || variant == MD5HIP_DESC_XDMA) {
     const uint64_t g = (n + 63) / 64;
     if (g > 0x7fffffffull) return -EINVAL;
-    hipLaunchKernelGGL(md5_desc_xpose, dim3((uint32_t)g), dim3(64), 0, (hipStream_t)stream,
+    hipLaunchKernelGGL(variant == MD5HIP_DESC_XDMA ? md5_desc_xdma : md5_desc_xpose, dim3((uint32_t)g), dim3(64), 0, (hipStream_t)stream,
                        (const uint8_t*)d_base, d_offsets, d_lens, d_order, n, (uint4*)d_digests);
     return launched();
   }
