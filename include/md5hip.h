@@ -111,7 +111,8 @@ enum crc32hip_variant {
     CRC32HIP_LANE16 = 3,    /* slicing-by-4, 16 table copies (64 KiB LDS) */
     CRC32HIP_XLANE16 = 4,   /* slicing-by-4, 16 table copies + whole-line xpose loads */
     CRC32HIP_XPERM16 = 5,   /* as XLANE16, copies laid out for one-v_perm addressing */
-    CRC32HIP_NUM_VARIANTS = 6
+    CRC32HIP_XDMA16 = 6,    /* XPERM16 tables, full images filled by LDS-DMA, 12 waves/CU */
+    CRC32HIP_NUM_VARIANTS = 7
 };
 int crc32hip_fixed_variant(const void *d_base, uint64_t n, uint32_t len, uint64_t stride,
                            uint32_t fastcrc, uint32_t *d_crcs, void *stream, int variant);

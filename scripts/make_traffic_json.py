@@ -10,7 +10,7 @@ KERNEL = {"direct2": "md5_fixed_direct<2, 0>", "direct4": "md5_fixed_direct<4, 0
           "lds64": "md5_fixed_lds64", "lds128": "md5_fixed_lds128", "xpose1": "md5_fixed_xpose1",
           "xpose2": "md5_fixed_xpose2", "xpose1nt": "md5_fixed_xpose1nt",
           "xpose2nt": "md5_fixed_xpose2nt", "lds128nt": "md5_fixed_lds128nt",
-          "xdma1nt": "md5_fixed_xdma1nt", "crc32 xperm16": "crc32_fixed_xperm16", "crc32 shared8": "crc32_fixed_xpose"}
+          "xdma1nt": "md5_fixed_xdma1nt", "crc32 xperm16": "crc32_fixed_xperm16", "crc32 xdma16": "crc32_fixed_xdma16", "crc32 shared8": "crc32_fixed_xpose"}
 summ = json.load(open(sys.argv[1]))
 src = sys.argv[2] if len(sys.argv) > 2 else sys.argv[1]
 prev = json.load(open(sys.argv[3])) if len(sys.argv) > 3 else {}

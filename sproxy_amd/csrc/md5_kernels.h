@@ -334,16 +334,13 @@ __device__ __forceinline__ void fixed_xpose_body(const uint8_t* __restrict__ bas
 // the saved instructions and register traffic buy clock: 1.7 % faster.
 // Requires 64 * stride < 2^31 (checked by the launcher).
 // ---------------------------------------------------------------------------
-template <class H = Md5Hasher<false>, int CP = 2>
-__device__ __forceinline__ void fixed_xdma_body(const uint8_t* __restrict__ base, uint64_t n,
-                                                uint32_t len, uint64_t stride,
-                                                typename H::Out* __restrict__ out, uint8_t* lds) {
-  H h;
+// xdma_group: one wave hashes the 64-chunk group starting at wave_first (< n)
+// through its 8 KiB image `img`; the hasher is set up by the caller.
+template <class H, int CP = 2>
+__device__ __forceinline__ void xdma_group(H& h, const uint8_t* __restrict__ base, uint64_t n,
+                                           uint32_t len, uint64_t stride, uint64_t wave_first,
+                                           typename H::Out* __restrict__ out, uint8_t* img) {
   const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  uint8_t* img = lds + wave * 8192u;
-  const uint64_t wave_first = ((uint64_t)blockIdx.x * blockDim.x) + wave * 64u;
-  if (wave_first >= n) return;
   const uint64_t left = n - wave_first;
   const uint32_t rows = left < 64 ? (uint32_t)left : 64u;
   const __amdgpu_buffer_rsrc_t rsrc = uniform_rsrc(base + wave_first * stride);
@@ -394,6 +391,17 @@ __device__ __forceinline__ void fixed_xdma_body(const uint8_t* __restrict__ base
   }
   h.finish(st, chunk + ((uint64_t)nfull << 6), len & 63u, len);
   if (lane < rows) h.store(out, i, st);
+}
+
+template <class H = Md5Hasher<false>, int CP = 2>
+__device__ __forceinline__ void fixed_xdma_body(const uint8_t* __restrict__ base, uint64_t n,
+                                                uint32_t len, uint64_t stride,
+                                                typename H::Out* __restrict__ out, uint8_t* lds) {
+  H h;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint64_t wave_first = ((uint64_t)blockIdx.x * blockDim.x) + wave * 64u;
+  if (wave_first >= n) return;
+  xdma_group<H, CP>(h, base, n, len, stride, wave_first, out, lds + wave * 8192u);
 }
 
 // Non-template entry points (hipcc mis-handles explicitly instantiated
@@ -949,6 +957,24 @@ crc32_fixed_xperm16(const uint8_t* __restrict__ base, uint64_t n, uint32_t len, 
   crc32_xlane_body<Crc32PermHasher>(base, n, len, stride, out, lds, lds + Crc32PermHasher::kLdsBytes);
 }
 
+// XDMA16: the XPERM16 tables (64 KiB) beside twelve waves' full 8 KiB images
+// filled by LDS-DMA (xdma_group, as the MD5 default): no VGPR staging, no
+// ds_write, one image read per stage instead of two half-image rounds.  One
+// 768-thread workgroup per CU (160 KiB LDS), grid-stride over 64-chunk groups,
+// wave-major as crc32_xlane_body.
+__global__ void __launch_bounds__(768)
+crc32_fixed_xdma16(const uint8_t* __restrict__ base, uint64_t n, uint32_t len, uint64_t stride,
+                   uint32_t* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds[Crc32PermHasher::kLdsBytes + 12 * 8192];
+  Crc32PermHasher h;
+  h.setup(lds);
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  uint8_t* img = lds + Crc32PermHasher::kLdsBytes + wave * 8192u;
+  const uint64_t ngroups = (n + 63) / 64;
+  for (uint64_t gi = (uint64_t)wave * gridDim.x + blockIdx.x; gi < ngroups; gi += (uint64_t)gridDim.x * 12u)
+    xdma_group<Crc32PermHasher, 2>(h, base, n, len, stride, gi * 64u, out, img);
+}
+
 // Descriptor batches (ragged netcache blocks) with the XPERM16 tables: the
 // descriptor xpose loader (desc_xpose_group) with half images, one 1024-thread
 // workgroup per CU, grid-stride over 64-chunk groups of `order`.
@@ -965,6 +991,23 @@ crc32_desc_xperm16(const uint8_t* __restrict__ base, const uint64_t* __restrict_
   for (uint64_t gi = (uint64_t)wave * gridDim.x + blockIdx.x; gi < ngroups; gi += (uint64_t)gridDim.x * 16u)
     desc_xpose_group<2, Crc32PermHasher, 0, 1, true, false>(h, base, offs, lens, order, n,
                                                             gi * 64u, out, img);   // (wave-major, as above)
+}
+
+// Descriptor batches with XDMA16's layout: the descriptor loader's per-row
+// loads as LDS-DMA into twelve waves' full 8 KiB images beside the tables.
+__global__ void __launch_bounds__(768)
+crc32_desc_xdma16(const uint8_t* __restrict__ base, const uint64_t* __restrict__ offs,
+                  const uint32_t* __restrict__ lens, const uint32_t* __restrict__ order,
+                  uint64_t n, uint32_t* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds[Crc32PermHasher::kLdsBytes + 12 * 8192];
+  Crc32PermHasher h;
+  h.setup(lds);
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  uint8_t* img = lds + Crc32PermHasher::kLdsBytes + wave * 8192u;
+  const uint64_t ngroups = (n + 63) / 64;
+  for (uint64_t gi = (uint64_t)wave * gridDim.x + blockIdx.x; gi < ngroups; gi += (uint64_t)gridDim.x * 12u)
+    desc_xpose_group<2, Crc32PermHasher, 0, 1, false, true, true>(h, base, offs, lens, order, n,
+                                                                  gi * 64u, out, img);
 }
 
 // fastcrc (blk_io.c:408-424): len <= f -> crc(all), else crc(first f bytes)

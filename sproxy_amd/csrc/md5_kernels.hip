@@ -78,7 +78,7 @@ int cu_count() {
 
 int default_crc_variant() {
   static const int v = env_int("CRC32HIP_VARIANT", 1, CRC32HIP_NUM_VARIANTS,
-                               CRC32HIP_XPERM16);  // measured best, DESIGN.md §5
+                               CRC32HIP_XDMA16);   // measured best, DESIGN.md §5
   return v;
 }
 
@@ -287,6 +287,14 @@ int crc32hip_fixed_variant(const void* d_base, uint64_t n, uint32_t len, uint64_
                        n, len, stride, d_crcs);
     return launched();
   }
+  if (aligned && stride < (1ull << 31) / 64 && variant == CRC32HIP_XDMA16) {
+    // one 768-thread workgroup per CU (160 KiB LDS), grid-stride, wave-major
+    const uint64_t need = (n + 63) / 64;
+    const uint64_t cap = (uint64_t)cu_count();
+    hipLaunchKernelGGL(crc32_fixed_xdma16, dim3((uint32_t)(need < cap ? need : cap)), dim3(768), 0,
+                       s, base, n, len, stride, d_crcs);
+    return launched();
+  }
   if (aligned && stride < (1ull << 31) / 64) {
     const uint64_t g = (n + kBlock - 1) / kBlock;
     if (g > 0x7fffffffull) return -EINVAL;
@@ -321,6 +329,12 @@ int crc32hip_desc(const void* d_base, const uint64_t* d_offsets, const uint32_t*
     hipLaunchKernelGGL(crc32_fast<false>, dim3((uint32_t)g), dim3(kDescBlock), 0, s,
                        (const uint8_t*)d_base, d_offsets, d_lens, n, (uint64_t)0, 0u, fastcrc,
                        d_crcs);
+  } else if (default_crc_variant() == CRC32HIP_XDMA16) {
+    // XDMA16: one 768-thread workgroup per CU, LDS-DMA images
+    const uint64_t need = (n + 63) / 64;
+    const uint64_t cap = (uint64_t)cu_count();
+    hipLaunchKernelGGL(crc32_desc_xdma16, dim3((uint32_t)(need < cap ? need : cap)), dim3(768), 0,
+                       s, (const uint8_t*)d_base, d_offsets, d_lens, d_order, n, d_crcs);
   } else if (default_crc_variant() == CRC32HIP_XPERM16) {
     // XPERM16 tables + descriptor xpose loads: one 1024-thread workgroup per CU
     const uint64_t need = (n + 63) / 64;

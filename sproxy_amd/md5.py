@@ -157,7 +157,8 @@ def digest_desc(base, offsets, lens, order=None, out=None, stream=None, variant=
     return out
 
 
-CRC_VARIANTS = {"auto": 0, "shared8": 1, "lane32": 2, "lane16": 3, "xlane16": 4, "xperm16": 5}   # enum crc32hip_variant
+CRC_VARIANTS = {"auto": 0, "shared8": 1, "lane32": 2, "lane16": 3, "xlane16": 4, "xperm16": 5,
+                "xdma16": 6}   # enum crc32hip_variant
 
 
 def crc32_fixed(data, n: int = None, length: int = None, stride: int = None, fastcrc: int = 0,
