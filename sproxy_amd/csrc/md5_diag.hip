@@ -467,6 +467,76 @@ diag_xdma(const uint8_t* __restrict__ base, uint64_t n, uint32_t len, uint64_t s
   if (lane < rows) h.store(out, i, st);
 }
 
+// Double-buffered xdma: two 8 KiB images per wave, the DMA of stage s+2 goes
+// into stage s's image as soon as this wave has read it, so a whole stage of
+// compression covers each DMA's latency (one more stage in flight per wave,
+// half the waves per CU: WPB waves per workgroup, 16 KiB LDS each).
+template <int WPB>
+__global__ void __launch_bounds__(64 * WPB)
+diag_xdma2(const uint8_t* __restrict__ base, uint64_t n, uint32_t len, uint64_t stride,
+           uint4* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds[WPB * 16384];
+  Md5Hasher<false> h;
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  uint8_t* img = lds + wave * 16384u;
+  const uint64_t wave_first = ((uint64_t)blockIdx.x * blockDim.x) + wave * 64u;
+  if (wave_first >= n) return;
+  const uint64_t left = n - wave_first;
+  const uint32_t rows = left < 64 ? (uint32_t)left : 64u;
+  const __amdgpu_buffer_rsrc_t rsrc = uniform_rsrc(base + wave_first * stride);
+  uint32_t voff[8];
+#pragma unroll
+  for (int r = 0; r < 8; ++r) {
+    const uint32_t row = (uint32_t)r * 8u + (lane >> 3);
+    const uint32_t rc = row < rows ? row : rows - 1u;
+    const uint32_t part = (lane & 7u) ^ ((row >> 1) & 7u);
+    voff[r] = rc * (uint32_t)stride + part * 16u;
+  }
+  const uint32_t g = (lane >> 1) & 7u;
+  const uint32_t nfull = len >> 6;
+  const uint32_t nstage = nfull >> 1;
+  typename Md5Hasher<false>::State st = h.init();
+  auto issue = [&](uint32_t stg) __attribute__((always_inline)) {
+    uint8_t* im = img + (stg & 1u) * 8192u;
+#pragma unroll
+    for (int r = 0; r < 8; ++r)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, im + r * 1024, 16, voff[r], stg * 128u, 0, 2);
+  };
+  if (nstage) {
+    issue(0);
+    if (nstage > 1) issue(1);
+    for (uint32_t stg = 0; stg < nstage; ++stg) {
+      // loads complete in order: with stage s+1's 8 DMAs still in flight,
+      // vmcnt(8) means stage s has landed
+      if (stg + 1 < nstage) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const uint8_t* im = img + (stg & 1u) * 8192u;
+      uint4 w[2][4];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const u32x4 v = *reinterpret_cast<const u32x4*>(im + lane * 128 + ((q ^ g) * 16));
+        w[q >> 2][q & 3] = make_uint4(v.x, v.y, v.z, v.w);
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if (stg + 2 < nstage) issue(stg + 2);
+      __builtin_amdgcn_sched_barrier(0);
+      h.block(st, w[0]);
+      h.block(st, w[1]);
+    }
+  }
+  const uint64_t i = wave_first + lane;
+  const uint64_t ci = lane < rows ? i : n - 1;
+  const uint8_t* chunk = base + ci * stride;
+  if (nfull & 1u) {
+    uint4 w[4];
+    load_block(w, reinterpret_cast<const uint4*>(chunk + ((uint64_t)(nfull - 1) << 6)));
+    h.block(st, w);
+  }
+  h.finish(st, chunk + ((uint64_t)nfull << 6), len & 63u, len);
+  if (lane < rows) h.store(out, i, st);
+}
+
 // Ideal streaming read of n*len bytes: grid-stride, 16 B per lane, consecutive
 // lanes consecutive addresses; xor-fold per lane.
 __global__ void __launch_bounds__(256)
@@ -611,6 +681,8 @@ extern "C" int md5diag_run(int kind, const void* base, uint64_t n, uint32_t len,
     case 55: hipLaunchKernelGGL(diag_xpose1nt_plain3, dim3(grid), dim3(256), 0, s, b, n, len, stride, o); break;
     case 56: hipLaunchKernelGGL(diag_compute_plain3, dim3(grid), dim3(256), 0, s, n, len >> 6, o); break;
     case 57: hipLaunchKernelGGL(diag_xdma<2>, dim3(grid), dim3(256), 0, s, b, n, len, stride, o); break;
+    case 59: hipLaunchKernelGGL(diag_xdma2<2>, dim3((uint32_t)((n + 127) / 128)), dim3(128), 0, s, b, n, len, stride, o); break;
+    case 60: hipLaunchKernelGGL(diag_xdma2<1>, dim3((uint32_t)((n + 63) / 64)), dim3(64), 0, s, b, n, len, stride, o); break;
     case 58: hipLaunchKernelGGL(diag_xdma<0>, dim3(grid), dim3(256), 0, s, b, n, len, stride, o); break;
     case 54: hipLaunchKernelGGL(diag_xpose1nt_nopeel, dim3(grid), dim3(256), 0, s, b, n, len, stride, o); break;
     case 51: hipLaunchKernelGGL(diag_crc_clk, dim3(grid), dim3(256), 0, s, b, n, len, stride, o); break;
