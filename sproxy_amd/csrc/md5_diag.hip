@@ -660,6 +660,13 @@ extern "C" int md5diag_run(int kind, const void* base, uint64_t n, uint32_t len,
       hipLaunchKernelGGL(md5_fixed_xpose1nt, dim3(grid), dim3(256), extra, s, b, n, len, stride, o);
       break;
     }
+    case 61: case 62: {
+      // occupancy A/B of the product xdma1nt kernel (as 34-37): 61: +8 KiB
+      // (4 WG = 16 waves per CU), 62: +22 KiB (3 WG = 12 waves)
+      const size_t extra = kind == 61 ? 8192 : 22528;
+      hipLaunchKernelGGL(md5_fixed_xdma1nt, dim3(grid), dim3(256), extra, s, b, n, len, stride, o);
+      break;
+    }
     case 38: hipLaunchKernelGGL((diag_x64<2, false>), dim3(grid), dim3(256), 0, s, b, n, len, stride, o); break;
     case 39: hipLaunchKernelGGL((diag_x64<0, false>), dim3(grid), dim3(256), 0, s, b, n, len, stride, o); break;
     case 44: hipLaunchKernelGGL((diag_x64<2, true>), dim3(grid), dim3(256), 0, s, b, n, len, stride, o); break;
