@@ -81,7 +81,7 @@ enum md5hip_desc_variant {
     MD5HIP_DESC_LANE = 1,   /* each lane streams its own chunk (8-block register ring) */
     MD5HIP_DESC_XPOSE = 2,  /* whole-line loads of 8 chunks x 128 B + LDS transpose;
                                waves with an unaligned chunk fall back to LANE */
-    MD5HIP_DESC_HYBRID = 3, /* XPOSE, but the first waves (one per CU, env MD5HIP_DESC_NLONG)
+    MD5HIP_DESC_HYBRID = 3, /* XDMA, but the first waves (one per CU, env MD5HIP_DESC_NLONG)
                                go lane-direct when they hold a chunk >= 256 KiB */
     MD5HIP_DESC_XDMA = 4,   /* XPOSE with the image filled by LDS-DMA (no VGPR staging);
                                the default */
@@ -127,6 +127,26 @@ int crc32hip_desc(const void *d_base, const uint64_t *d_offsets, const uint32_t 
  * descending (stable counting sort, O(n)).  Synchronous, host memory.
  */
 int md5hip_plan_order(const uint32_t *lens, uint64_t n, uint32_t *order);
+
+/*
+ * Batch arena: `bytes` of device memory on `device` at a 1 GiB-aligned
+ * virtual address (reserved + mapped through the HIP virtual memory API), so
+ * the GPU page tables can use large fragments for the whole range.  Chunks
+ * hashed by lane-direct chains (HYBRID's long waves) touch 64 pages per load;
+ * they run faster from an arena than from a 2 MiB-aligned hipMalloc buffer.
+ * 0 / -EINVAL / -ENODEV / -ENOMEM / -EIO; free with md5hip_arena_free.
+ */
+int md5hip_arena_alloc(int device, uint64_t bytes, void **d_ptr);
+int md5hip_arena_free(void *d_ptr);
+
+/*
+ * Host planner for a descriptor batch: fills order[] as md5hip_plan_order and
+ * returns the enum md5hip_desc_variant to launch it with (>= 0), or -errno.
+ * HYBRID when the batch's longest chunks (>= 256 KiB) stand out -- the chunk
+ * two waves per CU deep in the order is at most a quarter as long, so their
+ * serial chains bound the launch -- else XDMA.
+ */
+int md5hip_plan_desc(const uint32_t *lens, uint64_t n, uint32_t *order);
 
 /*
  * Synthetic-data generator for benches/tests: fills nbytes (multiple of 16)

@@ -30,7 +30,7 @@ def time_once(f, reps=5):
     return e0.elapsed_time(e1) / reps
 
 
-def ab(fns, rounds=6):
+def ab(fns, rounds=6, reps=5):
     for f in fns.values():
         f()
     torch.cuda.synchronize()
@@ -38,7 +38,7 @@ def ab(fns, rounds=6):
     keys = list(fns)
     for r in range(rounds):
         for k in keys[r % len(keys):] + keys[:r % len(keys)]:
-            ts[k].append(time_once(fns[k]))
+            ts[k].append(time_once(fns[k], reps))
     return {k: round(float(np.median(v)), 4) for k, v in ts.items()}
 
 
@@ -46,7 +46,9 @@ def main():
     data = torch.empty(16 << 30, dtype=torch.uint8, device="cuda")
     m.fill_synthetic(data, seed=0xD3A)
     res = {}
-    for S in (4096, 16384, 65536, 262144):
+    sweep = (4096, 16384, 65536, 262144, 524288, 1048576)
+    kinds = ("xdma", "hybrid") if "--hybrid" in sys.argv else ("xpose", "xdma")
+    for S in (() if "--c3-only" in sys.argv else sweep):
         n = (16 << 30) // S
         rng = np.random.default_rng(S)
         lens = np.full(n, S, dtype=np.int64)
@@ -55,12 +57,12 @@ def main():
         offs = torch.arange(n, dtype=torch.int64, device="cuda") * S
         d_len = torch.from_numpy(lens.astype(np.int32)).cuda()
         order = torch.from_numpy(m.plan_order(lens.astype(np.uint32)).astype(np.int32)).cuda()
-        outs = {k: torch.empty((n, 16), dtype=torch.uint8, device="cuda") for k in ("xpose", "xdma", "fixed")}
+        outs = {k: torch.empty((n, 16), dtype=torch.uint8, device="cuda") for k in kinds + ("fixed",)}
         fns = {k: (lambda k=k: m.digest_desc(data, offs, d_len, order, out=outs[k], variant=k))
-               for k in ("xpose", "xdma")}
+               for k in kinds}
         fns["fixed"] = lambda: m.digest_fixed(data, n, S, out=outs["fixed"])
         t = ab(fns)
-        same = bool(torch.equal(outs["xpose"], outs["xdma"]))
+        same = bool(torch.equal(outs[kinds[0]], outs[kinds[1]]))
         res[f"ragged_{S}"] = {"ms": t, "payload_GiBps": {k: round(float(lens.sum()) / GIB / (v * 1e-3), 1)
                                                          for k, v in t.items() if k != "fixed"},
                               "digests_equal": same}
@@ -71,7 +73,8 @@ def main():
     rng = np.random.default_rng(1000)
     classes = [4096 << k for k in range(9)]
     lens, tot = [], 0
-    while tot < (16 << 30) - (2 << 20):
+    exact = "--bench-batch" in sys.argv     # bench.py run_c3's batch exactly (own arena)
+    while tot < (16 << 30) - (0 if exact else 2 << 20):
         c = classes[int(rng.integers(0, 9))]
         if rng.integers(0, 8) == 0:
             c = int(rng.integers(1, c))
@@ -79,16 +82,34 @@ def main():
         tot += c
     lens = np.array(lens, dtype=np.int64)
     offs = np.concatenate([[0], np.cumsum((lens + 15) // 16 * 16)[:-1]])
+    if exact:
+        del data
+        torch.cuda.empty_cache()
+        total = int(offs[-1] + lens[-1] + 16)
+        data = torch.empty((total + 15) // 16 * 16, dtype=torch.uint8, device="cuda")
+        m.fill_synthetic(data, seed=0xC3)
     keep = offs + lens <= data.numel()
     lens, offs = lens[keep], offs[keep]
     d_off = torch.from_numpy(offs).cuda()
     d_len = torch.from_numpy(lens.astype(np.int32)).cuda()
     order = torch.from_numpy(m.plan_order(lens.astype(np.uint32)).astype(np.int32)).cuda()
-    outs = {k: torch.empty((lens.size, 16), dtype=torch.uint8, device="cuda") for k in ("xpose", "xdma")}
-    fns = {k: (lambda k=k: m.digest_desc(data, d_off, d_len, order, out=outs[k], variant=k))
-           for k in ("xpose", "xdma")}
-    t = ab(fns, rounds=4)
-    res["c3_mixed"] = {"ms": t, "chunks": int(lens.size), "digests_equal": bool(torch.equal(outs["xpose"], outs["xdma"]))}
+    ks = ("xdma", "hybrid") if "--hybrid" in sys.argv else ("xpose", "xdma", "hybrid")
+    outs = {k: torch.empty((lens.size, 16), dtype=torch.uint8, device="cuda") for k in ks}
+    fns = {k: (lambda k=k: m.digest_desc(data, d_off, d_len, order, out=outs[k], variant=k)) for k in ks}
+    t = ab(fns, rounds=6)
+    res["c3_mixed_sustained50"] = ab(fns, rounds=2, reps=50)
+    if "--solo" in sys.argv:      # each kernel alone, 3 x 50 back-to-back, no alternation
+        res["c3_mixed_solo"] = {k: ab({k: f}, rounds=3, reps=50)[k] for k, f in fns.items()}
+    res["c3_mixed"] = {"ms": t, "chunks": int(lens.size),
+                       "digests_equal": all(torch.equal(outs[ks[0]], outs[k]) for k in ks)}
+    # its longest chunks alone (the batch's serial-chain bound)
+    il = np.flatnonzero(lens == lens.max())
+    o1, l1 = torch.from_numpy(offs[il]).cuda(), torch.from_numpy(lens[il].astype(np.int32)).cuda()
+    out1 = torch.empty((il.size, 16), dtype=torch.uint8, device="cuda")
+    res["c3_longest_alone"] = {"n": int(il.size), "ms": ab({k: (lambda k=k: m.digest_desc(
+        data, o1, l1, out=out1, variant=k)) for k in ks}, rounds=4)}
+    if "--c3-only" in sys.argv:
+        res = {k: v for k, v in res.items() if k.startswith("c3")}
     print(json.dumps(res))
 
 

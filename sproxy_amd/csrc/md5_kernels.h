@@ -591,7 +591,10 @@ md5_desc(const uint8_t* __restrict__ base, const uint64_t* __restrict__ offs,
 // ---------------------------------------------------------------------------
 // kLong > 0: the first `nlong` waves (one per CU; with longest-first order
 // these hold the batch's longest chunks) take the lane-direct path with an
-// 8-block register ring when their longest chunk has >= kLong blocks.  Such a
+// 8-block register ring when their longest chunk has >= kLong blocks.  The
+// host planner (md5hip_plan_desc) picks this variant only for batches whose
+// longest chunks stand out; a test inside the kernel cost the lane-direct
+// ring its loads in flight (hipcc kept 7 instead of 28 outstanding).  Such a
 // wave is a serial chain that runs nearly alone on its SIMD: the xpose
 // stage's LDS round trip (8 ds_write_b128 + 8 ds_read_b128 + waits per
 // 128 B) sits on its critical path, while one lane-direct wave per CU does
@@ -603,6 +606,24 @@ md5_desc(const uint8_t* __restrict__ base, const uint64_t* __restrict__ offs,
 // (global_load_lds_dwordx4 from the same per-row addresses) straight into the
 // image, as fixed_xdma_body: no VGPR staging, no ds_write; the DMA of stage
 // s+1 is issued once this wave's row reads of stage s have returned.
+// HYBRID's test that a wave's long chunks are the batch's critical path: in
+// longest-first order, the chunk `depth` positions in (two waves per CU) is at
+// most a quarter of this wave's longest.  A batch of equal-length blocks
+// (a netcache chunk_size sweep) fails it and keeps the xpose/xdma loader for
+// every wave; a mixed batch (C3) or a batch of fewer chunks than two waves
+// per CU passes, and its first waves run their chains lane-direct.
+__device__ __forceinline__ bool long_outlier(const uint32_t* __restrict__ lens,
+                                             const uint32_t* __restrict__ order, uint64_t n,
+                                             uint64_t depth, uint32_t bmax) {
+  const uint64_t p = depth < n - 1 ? depth : n - 1;
+  const uint32_t probe = lens[order[p]] >> 6;
+  return 4u * (uint64_t)probe <= bmax;
+}
+
+// HYBRID's lane-direct threshold: a wave whose longest chunk has this many
+// 64-B blocks (256 KiB)
+constexpr uint32_t kHybridLongBlocks = 4096;
+
 template <int CP, class H, uint32_t kLong = 0, int D = 1, bool kHalf = false, bool kPeel = true,
           bool kDma = false>
 __device__ __forceinline__ void desc_xpose_group(H& h, const uint8_t* __restrict__ base,
@@ -792,7 +813,8 @@ md5_desc_hybrid(const uint8_t* __restrict__ base, const uint64_t* __restrict__ o
                 const uint32_t* __restrict__ lens, const uint32_t* __restrict__ order, uint64_t n,
                 uint4* __restrict__ out, uint32_t nlong) {
   __shared__ __attribute__((aligned(16))) uint8_t img[8192];
-  desc_xpose_body<2, Md5Hasher<true>, 4096>(base, offs, lens, order, n, out, img, nlong);   // >= 256 KiB
+  desc_xpose_body<2, Md5Hasher<true>, kHybridLongBlocks, 1, true>(base, offs, lens, order, n, out,
+                                                                  img, nlong);   // else xdma
 }
 
 // ---------------------------------------------------------------------------

@@ -30,6 +30,8 @@ template __global__ void crc32_fast<true>(const uint8_t*, const uint64_t*, const
 #include <errno.h>
 #include <stdlib.h>
 #include <string.h>
+#include <mutex>
+#include <vector>
 
 #include "../../include/md5hip.h"
 #include "md5_internal.h"
@@ -411,6 +413,106 @@ int md5hip_plan_order(const uint32_t* lens, uint64_t n, uint32_t* order) {
   };
   qsort_r(order, (size_t)n, sizeof(uint32_t), Cmp::f, (void*)lens);
   return 0;
+}
+
+// ---------------------------------------------------------------------------
+// Batch arenas: device memory whose virtual range is reserved with 1 GiB
+// alignment (hipMemAddressReserve + hipMemCreate + hipMemMap), so the page
+// tables can use large fragments throughout.  A lane-direct chain walks its
+// own chunk, so a wave touches 64 distinct pages per load; HYBRID's long
+// chains on C3 ran 9.7 ms in a 16 MiB-aligned buffer and 10.4-11.5 ms in a
+// 2 MiB-aligned one (scripts/alloc_probe.py).  The whole-line
+// loaders are indifferent.
+// ---------------------------------------------------------------------------
+namespace {
+struct Arena {
+  void* ptr;       // mapped, kArenaAlign-aligned
+  size_t size;
+  void* base;      // the reservation (the runtime ignores a reservation's
+  size_t rsize;    // alignment argument, so it is over-reserved by kArenaAlign)
+  hipMemGenericAllocationHandle_t h;
+};
+std::mutex g_arena_mu;
+std::vector<Arena> g_arenas;
+constexpr size_t kArenaAlign = size_t(1) << 30;
+}  // namespace
+
+int md5hip_arena_alloc(int device, uint64_t bytes, void** out) {
+  if (!out || bytes == 0) return -EINVAL;
+  *out = nullptr;
+  hipMemAllocationProp prop = {};
+  prop.type = hipMemAllocationTypePinned;
+  prop.location.type = hipMemLocationTypeDevice;
+  prop.location.id = device;
+  size_t gran = 0;
+  if (hipMemGetAllocationGranularity(&gran, &prop, hipMemAllocationGranularityRecommended) !=
+          hipSuccess || gran == 0)
+    return -ENODEV;
+  if (gran < (size_t(2) << 20)) gran = size_t(2) << 20;
+  const size_t size = (size_t)((bytes + gran - 1) / gran * gran);
+  void* base = nullptr;
+  const size_t rsize = size + kArenaAlign;
+  hipMemGenericAllocationHandle_t h{};
+  if (hipMemAddressReserve(&base, rsize, kArenaAlign, nullptr, 0) != hipSuccess) return -ENOMEM;
+  void* ptr = (void*)(((uintptr_t)base + kArenaAlign - 1) & ~(uintptr_t)(kArenaAlign - 1));
+  if (hipMemCreate(&h, size, &prop, 0) != hipSuccess) {
+    (void)hipMemAddressFree(base, rsize);
+    return -ENOMEM;
+  }
+  hipMemAccessDesc acc = {};
+  acc.location = prop.location;
+  acc.flags = hipMemAccessFlagsProtReadWrite;
+  if (hipMemMap(ptr, size, 0, h, 0) != hipSuccess) {
+    (void)hipMemRelease(h);
+    (void)hipMemAddressFree(base, rsize);
+    return -ENOMEM;
+  }
+  if (hipMemSetAccess(ptr, size, &acc, 1) != hipSuccess) {
+    (void)hipMemUnmap(ptr, size);
+    (void)hipMemRelease(h);
+    (void)hipMemAddressFree(base, rsize);
+    return -EIO;
+  }
+  {
+    std::lock_guard<std::mutex> lk(g_arena_mu);
+    g_arenas.push_back(Arena{ptr, size, base, rsize, h});
+  }
+  *out = ptr;
+  return 0;
+}
+
+int md5hip_arena_free(void* ptr) {
+  if (!ptr) return -EINVAL;
+  Arena a{};
+  {
+    std::lock_guard<std::mutex> lk(g_arena_mu);
+    size_t k = 0;
+    while (k < g_arenas.size() && g_arenas[k].ptr != ptr) ++k;
+    if (k == g_arenas.size()) return -ENOENT;
+    a = g_arenas[k];
+    g_arenas.erase(g_arenas.begin() + (long)k);
+  }
+  int rc = 0;
+  if (hipMemUnmap(a.ptr, a.size) != hipSuccess) rc = -EIO;
+  if (hipMemRelease(a.h) != hipSuccess) rc = -EIO;
+  if (hipMemAddressFree(a.base, a.rsize) != hipSuccess) rc = -EIO;
+  return rc;
+}
+
+// Planner for descriptor batches: the longest-first order, and HYBRID when
+// the first waves' chunks (>= 256 KiB) stand out from the batch -- the chunk
+// two waves per CU deep in the order is at most a quarter as long -- so that
+// their serial chains, not the bytes, bound the launch (a mixed C3 batch, or
+// fewer long chunks than two waves per CU); XDMA otherwise (equal-length
+// netcache blocks).  DESIGN.md §5, profiles/r01_desc_hybrid_ab.json.
+int md5hip_plan_desc(const uint32_t* lens, uint64_t n, uint32_t* order) {
+  if (int e = md5hip_plan_order(lens, n, order)) return e;
+  if (n == 0) return MD5HIP_DESC_XDMA;
+  const uint32_t bmax = lens[order[0]] >> 6;
+  if (bmax < kHybridLongBlocks) return MD5HIP_DESC_XDMA;
+  const uint64_t depth = (uint64_t)cu_count() * 128u;
+  const uint64_t p = depth < n - 1 ? depth : n - 1;
+  return 4ull * (lens[order[p]] >> 6) <= bmax ? MD5HIP_DESC_HYBRID : MD5HIP_DESC_XDMA;
 }
 
 }  // extern "C"

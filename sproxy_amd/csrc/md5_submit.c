@@ -280,7 +280,8 @@ static int slot_launch(const md5hip_batcher *b, struct slot *sl, uint64_t n, uin
 {
     sl->ticket = b->ticket;
     int rc;
-    if (md5hip_plan_order(sl->h_len, n, sl->h_ord) != 0) return -EINVAL;
+    const int dvar = md5hip_plan_desc(sl->h_len, n, sl->h_ord);
+    if (dvar < 0) return -EINVAL;
     if (hipMemcpyAsync(sl->d_off, sl->h_off, 8 * n, hipMemcpyHostToDevice, sl->stream) ||
         hipMemcpyAsync(sl->d_len, sl->h_len, 4 * n, hipMemcpyHostToDevice, sl->stream) ||
         hipMemcpyAsync(sl->d_ord, sl->h_ord, 4 * n, hipMemcpyHostToDevice, sl->stream))
@@ -310,8 +311,8 @@ static int slot_launch(const md5hip_batcher *b, struct slot *sl, uint64_t n, uin
         rc = crc32hip_desc(sl->d_data, sl->d_off, sl->d_len, sl->d_ord, n, b->fastcrc,
                            (uint32_t *)sl->d_dig, sl->stream);
     else
-        rc = md5hip_digest_desc(sl->d_data, sl->d_off, sl->d_len, sl->d_ord, n, sl->d_dig,
-                                sl->stream);
+        rc = md5hip_digest_desc_variant(sl->d_data, sl->d_off, sl->d_len, sl->d_ord, n, sl->d_dig,
+                                        sl->stream, dvar);
     if (rc) return rc;
     if (hipMemcpyAsync(sl->h_dig, sl->d_dig, (size_t)b->dsz * n, hipMemcpyDeviceToHost, sl->stream) ||
         hipEventRecord(sl->done, sl->stream))

@@ -196,6 +196,46 @@ def crc32_desc(base, offsets, lens, order=None, fastcrc: int = 0, out=None, stre
     return out
 
 
+class _Arena:
+    """Owner of one md5hip_arena_alloc block, exposed through
+    __cuda_array_interface__ so torch can wrap it without a copy."""
+
+    def __init__(self, nbytes: int, device: int):
+        p = ctypes.c_void_p()
+        check("md5hip_arena_alloc", lib().md5hip_arena_alloc(device, nbytes, ctypes.byref(p)))
+        self.ptr, self.nbytes = p.value, nbytes
+        self.__cuda_array_interface__ = {"shape": (nbytes,), "typestr": "|u1", "data": (self.ptr, False),
+                                         "strides": None, "version": 2}
+
+    def __del__(self):
+        if getattr(self, "ptr", None):
+            lib().md5hip_arena_free(ctypes.c_void_p(self.ptr))
+            self.ptr = None
+
+
+def arena_empty(nbytes: int, device=None) -> torch.Tensor:
+    """uint8 [nbytes] device tensor in a batch arena (md5hip_arena_alloc:
+    1 GiB-aligned virtual range, large page-table fragments).  The arena is
+    freed when the tensor is."""
+    dev = torch.cuda.current_device() if device is None else int(device)
+    owner = _Arena(int(nbytes), dev)
+    with torch.cuda.device(dev):
+        t = torch.as_tensor(owner, device=f"cuda:{dev}")
+    t._md5hip_arena = owner            # keep the owner alive with the tensor
+    return t
+
+
+def plan_desc(lens):
+    """(order, variant name): md5hip_plan_desc -- the longest-first order and
+    the descriptor kernel the planner picks for this batch shape."""
+    L = np.ascontiguousarray(lens, dtype=np.uint32)
+    order = np.empty(max(L.size, 1), dtype=np.uint32)
+    v = lib().md5hip_plan_desc(L.ctypes.data, L.size, order.ctypes.data)
+    if v < 0:
+        raise MD5HipError("md5hip_plan_desc", v)
+    return order[:L.size], {x: k for k, x in DESC_VARIANTS.items()}[v]
+
+
 def plan_order(lens) -> np.ndarray:
     """Longest-first lane order (md5hip_plan_order), host arrays."""
     L = np.ascontiguousarray(lens, dtype=np.uint32)
@@ -441,7 +481,8 @@ def pool_plan(lens, nparts: int) -> np.ndarray:
     return first
 
 
-__all__ = ["MD5Context", "MD5Init", "MD5Update", "MD5Final", "MD5_DIGEST_SIZE", "MD5HipError",
+__all__ = ["MD5Context", "MD5Init", "MD5Update", "MD5Final", "MD5_DIGEST_SIZE", "MD5HipError", "arena_empty",
+           "plan_desc",
            "md5", "digest_fixed", "digest_desc", "crc32_fixed", "crc32_desc", "plan_order", "fill_synthetic", "Batcher",
            "Pool", "pool_plan", "CRC_VARIANTS", "DESC_VARIANTS",
            "register_host", "unregister_host",

@@ -147,6 +147,25 @@ def test_plan_order_longest_first():
     assert m.plan_order(np.array([], dtype=np.uint32)).size == 0
 
 
+def test_plan_desc_picks_hybrid_only_for_standout_long_chunks():
+    """md5hip_plan_desc: the same order as md5hip_plan_order, and HYBRID only
+    when the longest chunks (>= 256 KiB) stand out (the chunk two waves per CU
+    deep -- 256 CUs when no device is visible -- is <= 1/4 as long)."""
+    rng = np.random.default_rng(5)
+    mixed = np.array([4096 << int(k) for k in rng.integers(0, 9, 80000)], dtype=np.uint32)
+    order, v = m.plan_desc(mixed)
+    assert np.array_equal(order, m.plan_order(mixed)) and v == "hybrid"           # C3 shape
+    assert m.plan_desc(np.full(65536, 262144, np.uint32))[1] == "xdma"            # equal blocks
+    ragged = np.full(65536, 262144, np.uint32)
+    ragged[::8] = rng.integers(1, 262144, 8192)
+    assert m.plan_desc(ragged)[1] == "xdma"                # probe 32,768 deep is still full size
+    few = np.full(1000, 1 << 20, np.uint32)
+    few[-1] = 100
+    assert m.plan_desc(few)[1] == "hybrid"                 # fewer chunks than two waves per CU
+    assert m.plan_desc(np.full(5000, 65536, np.uint32))[1] == "xdma"              # < 256 KiB
+    assert m.plan_desc(np.array([], np.uint32))[0].size == 0
+
+
 def test_device_api_rejects_host_tensors():
     import pytest
     import torch

@@ -542,6 +542,39 @@ def test_gpu_equals_reference_md5c_build(cuda):
     assert [bytes(x) for x in got] == [md5c(fx[i * L:(i + 1) * L]) for i in range(n)]
 
 
+def test_arena_batches(cuda):
+    """md5hip_arena_alloc: a 1 GiB-aligned device arena wrapped as a torch
+    tensor (no copy); fixed, descriptor (every variant) and CRC batches over it
+    equal the oracle; free / double free behave."""
+    t = m.arena_empty(3 << 30)
+    assert t.is_cuda and t.numel() == 3 << 30 and t.data_ptr() % (1 << 30) == 0
+    m.fill_synthetic(t, seed=0xA7E)
+    n, L = 4096, 65536
+    host = t[:n * L].cpu().numpy()
+    want = gen.oracle_digests_fixed(host, n, L)
+    assert np.array_equal(m.digest_fixed(t, n, L).cpu().numpy(), want)
+    lens = [int(x) for x in np.random.default_rng(3).integers(0, 1 << 21, 600)]
+    offs, total = gen.pack_offsets(lens, align=16)
+    arena = t[:total + 64].cpu().numpy()
+    want = gen.oracle_digests(arena, offs, lens)
+    order, v = m.plan_desc(lens)
+    d_off = torch.tensor(offs, dtype=torch.int64, device=cuda)
+    d_len = torch.tensor(lens, dtype=torch.int32, device=cuda)
+    d_ord = _dev(order.astype(np.int32), cuda)
+    for dv in DESC + [v]:
+        assert np.array_equal(m.digest_desc(t, d_off, d_len, d_ord, variant=dv).cpu().numpy(), want), dv
+    crc = m.crc32_desc(t, d_off, d_len, d_ord).cpu().numpy().view(np.uint32)
+    assert np.array_equal(crc, gen.oracle_crc32_batch(arena, offs, lens))
+    owner = t._md5hip_arena
+    p = owner.ptr
+    del t
+    torch.cuda.synchronize()
+    from sproxy_amd._lib import lib
+    assert owner.ptr is not None                   # still referenced here: not yet freed
+    owner.__del__()
+    assert lib().md5hip_arena_free(ctypes.c_void_p(p)) == -2          # -ENOENT: already freed
+
+
 def test_zero_copy_gather_modes(cuda):
     """Registered host memory (md5hip_host_register) pulled by the device
     gather kernel or per-segment DMA instead of the host memcpy: same digests
