@@ -38,6 +38,7 @@ def main():
     p = argparse.ArgumentParser()
     p.add_argument("--prealloc", action="store_true")
     p.add_argument("--arena", action="store_true", help="md5hip_arena_alloc (1 GiB-aligned VA)")
+    p.add_argument("--c2-all", action="store_true")
     a = p.parse_args()
     if a.prealloc:
         tmp = torch.empty(16 << 30, dtype=torch.uint8, device="cuda")
@@ -54,6 +55,10 @@ def main():
            "align_log2": int((addr & -addr).bit_length() - 1)}
     out = torch.empty((n, 16), dtype=torch.uint8, device="cuda")
     res["c2_xdma1nt_ms"] = per_launch(lambda: m.digest_fixed(data, n, L, out=out))
+    if "--c2-all" in sys.argv:
+        for v in ("direct2", "direct4", "xpose1nt"):
+            res[f"c2_{v}_ms"] = per_launch(lambda: m.digest_fixed(data, n, L, out=out, variant=v))
+        res["c2_xdma1nt_ms_again"] = per_launch(lambda: m.digest_fixed(data, n, L, out=out))
     rng = np.random.default_rng(1000)
     classes = np.array([4096 << k for k in range(9)], dtype=np.int64)
     lens, tot = [], 0
