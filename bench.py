@@ -218,18 +218,20 @@ def run_c3(a, rank, world):
     """Mixed lengths 4 KiB..1 MiB (netcache chunk_size range, httpd.c:7968) with
     1-in-8 ragged tails, packed 16-B aligned, lanes packed longest-first."""
     import numpy as np
-    rng = np.random.default_rng(1000 + rank)
-    classes = np.array([4096 << k for k in range(9)], dtype=np.int64)
-    target = a.c3_bytes
-    lens = []
-    tot = 0
-    while tot < target:
-        c = int(classes[rng.integers(0, 9)])
-        if rng.integers(0, 8) == 0:
-            c = int(rng.integers(1, c))
-        lens.append(c)
-        tot += c
-    lens = np.array(lens, dtype=np.int64)
+
+    def c3_lens(seed):
+        rng = np.random.default_rng(seed)
+        classes = np.array([4096 << k for k in range(9)], dtype=np.int64)
+        out, tot = [], 0
+        while tot < a.c3_bytes:
+            c = int(classes[rng.integers(0, 9)])
+            if rng.integers(0, 8) == 0:
+                c = int(rng.integers(1, c))
+            out.append(c)
+            tot += c
+        return np.array(out, dtype=np.int64)
+
+    lens = c3_lens(1000 + rank)
     offs = np.concatenate([[0], np.cumsum((lens + 15) // 16 * 16)[:-1]])
     total = int(offs[-1] + lens[-1] + 16)
     # the batch lives in an arena (md5hip_arena_alloc: 1 GiB-aligned virtual
@@ -280,6 +282,33 @@ def run_c3(a, rank, world):
     s_wall = max_over_ranks(time.perf_counter() - t0, world, COLL_DEVICE)
     barrier(world)
     ok = all(torch.equal(o, out) for o in outs[:min(ns, a.steps)])
+    del outs
+    # coalesced: K such batches (own lengths, own bytes) planned and launched
+    # as one descriptor batch -- what a batcher holding K submissions does;
+    # the long chains of all K then overlap inside one launch
+    coal = None
+    K = a.c3_coalesce
+    if K > 1:
+        lk = [lens] + [c3_lens(2000 + 17 * j + rank) for j in range(1, K)]
+        ok_ = [np.concatenate([[0], np.cumsum((x + 15) // 16 * 16)[:-1]]) for x in lk]
+        spans = [int((o[-1] + x[-1] + 16 + 15) // 16 * 16) for o, x in zip(ok_, lk)]
+        starts = np.concatenate([[0], np.cumsum(spans)[:-1]])
+        big = m.arena_empty(int(sum(spans)))
+        m.fill_synthetic(big, seed=0xC3C + rank)
+        L_all = np.concatenate(lk)
+        O_all = np.concatenate([o + st for o, st in zip(ok_, starts)])
+        ordK, varK = m.plan_desc(L_all.astype(np.uint32))
+        dO, dL = torch.from_numpy(O_all).cuda(), torch.from_numpy(L_all.astype(np.int32)).cuda()
+        dR = torch.from_numpy(ordK.astype(np.int32)).cuda()
+        outK = torch.empty((L_all.size, 16), dtype=torch.uint8, device="cuda")
+        _, k_ms = timed_steps(lambda: m.digest_desc(big, dO, dL, dR, out=outK, variant=varK),
+                              max(5, a.steps // 2), max(2, a.warmup // 4), world)
+        pay = float(L_all.sum())
+        coal = {"batches": K, "chunks": int(L_all.size), "payload_bytes": int(pay), "kernel": varK,
+                "ms_per_launch": round(k_ms, 4), "ms_per_batch": round(k_ms / K, 4),
+                "value": round(pay * world / (k_ms * 1e-3) / GIB, 2), "unit": "GiB/s",
+                "note": "K C3 batches coalesced into one planned descriptor launch (distinct bytes)"}
+        del big, dO, dL, dR, outK
     # imbalance vs uniform -- the same payload bytes of the
     # same arena hashed as uniform 16 KiB chunks by the fixed-length kernel
     n_u = int(payload) // 16384
@@ -322,7 +351,8 @@ def run_c3(a, rank, world):
                          "unit": "GiB/s", "ms_per_batch": round(s_wall / a.steps * 1e3, 4),
                          "digests_equal_single": ok,
                          "note": "the same K batches, round-robin over streams, "
-                                 "batch k+1 overlapping batch k's long chains"}}
+                                 "batch k+1 overlapping batch k's long chains"},
+            "coalesced": coal}
 
 
 def run_c5(a, rank, world):
@@ -393,6 +423,8 @@ def main():
     p.add_argument("--c3-bytes", type=int, default=16 << 30)
     p.add_argument("--c3-variant", default="plan", choices=["plan"] + sorted(m.DESC_VARIANTS),
                    help="descriptor kernel for C3 (plan = md5hip_plan_desc's choice)")
+    p.add_argument("--c3-coalesce", type=int, default=3,
+                   help="C3 batches planned and launched together for the coalesced rate (0/1 = off)")
     p.add_argument("--c3-streams", type=int, default=3,
                    help="streams for C3's streamed rate (batches in flight)")
     p.add_argument("--c5-chunks", type=int, default=1 << 18)

@@ -19,27 +19,30 @@ from desc_xdma_ab import time_once  # noqa: E402
 
 def main():
     cus = torch.cuda.get_device_properties(0).multi_processor_count
-    data = m.arena_empty(16 << 30)
+    coal = "--coalesced" in sys.argv
+    data = m.arena_empty((52 if coal else 16) << 30)
     m.fill_synthetic(data, seed=0x4E4C)
     res = {"cus": cus}
     shapes = {}
-    for S in (262144, 524288, 1048576):
+    for S in (() if coal else (262144, 524288, 1048576)):
         n = (16 << 30) // S
         rng = np.random.default_rng(S)
         lens = np.full(n, S, dtype=np.int64)
         tail = rng.integers(0, 8, n) == 0
         lens[tail] = rng.integers(1, S, int(tail.sum()))
         shapes[f"ragged_{S}"] = (lens, np.arange(n, dtype=np.int64) * S)
-    rng = np.random.default_rng(1000)
-    lens, tot = [], 0
-    while tot < (16 << 30) - (2 << 20):
-        c = 4096 << int(rng.integers(0, 9))
-        if rng.integers(0, 8) == 0:
-            c = int(rng.integers(1, c))
-        lens.append(c)
-        tot += c
-    lens = np.array(lens, dtype=np.int64)
-    shapes["c3"] = (lens, np.concatenate([[0], np.cumsum((lens + 15) // 16 * 16)[:-1]]))
+    def c3(seed):
+        rng = np.random.default_rng(seed)
+        lens, tot = [], 0
+        while tot < (16 << 30) - (2 << 20):
+            c = 4096 << int(rng.integers(0, 9))
+            if rng.integers(0, 8) == 0:
+                c = int(rng.integers(1, c))
+            lens.append(c)
+            tot += c
+        return np.array(lens, dtype=np.int64)
+    lens = c3(1000) if not coal else np.concatenate([c3(1000), c3(2017), c3(2034)])
+    shapes["c3x3" if coal else "c3"] = (lens, np.concatenate([[0], np.cumsum((lens + 15) // 16 * 16)[:-1]]))
     for name, (lens, offs) in shapes.items():
         order, v = m.plan_desc(lens.astype(np.uint32))
         d_off = torch.from_numpy(offs).cuda()
