@@ -64,6 +64,7 @@ def main():
              "crc_lane32u": diag(27),
              "x64nt": diag(38), "x64": diag(39), "d64nt": diag(44), "d64": diag(45),
              "x2pairnt": diag(46), "x2pair": diag(47), "dyn5": diag(52), "dyn4": diag(53), "nopeel": diag(54), "plain3": diag(55), "comp_plain3": diag(56), "xdmant": diag(57), "xdma": diag(58), "xdma2w2": diag(59), "xdma2w1": diag(60), "xdma_occ16": diag(61), "xdma_occ12": diag(62),
+             "xdma_cp3": diag(63), "xdma_cp18": diag(64), "xdma_cp19": diag(65), "xdma_cp1": diag(66),
              "comp32": diag(40), "comp24": diag(41), "comp20": diag(42), "comp16": diag(43),
              "occ20": diag(34), "occ16": diag(35), "occ12": diag(36), "occ8": diag(37), "crc_shared8": crc("shared8"), "crc_lane32": crc("lane32"), "crc_lane16": crc("lane16"), "crc_xlane16": crc("xlane16"), "crc_xperm16": crc("xperm16"), "crc_xdma16": crc("xdma16"),
              "cp0": diag(20), "cp_sc0": diag(21), "cp_nt": diag(22), "cp_sc0nt": diag(23),

@@ -688,6 +688,10 @@ extern "C" int md5diag_run(int kind, const void* base, uint64_t n, uint32_t len,
     case 55: hipLaunchKernelGGL(diag_xpose1nt_plain3, dim3(grid), dim3(256), 0, s, b, n, len, stride, o); break;
     case 56: hipLaunchKernelGGL(diag_compute_plain3, dim3(grid), dim3(256), 0, s, n, len >> 6, o); break;
     case 57: hipLaunchKernelGGL(diag_xdma<2>, dim3(grid), dim3(256), 0, s, b, n, len, stride, o); break;
+    case 63: hipLaunchKernelGGL(diag_xdma<3>, dim3(grid), dim3(256), 0, s, b, n, len, stride, o); break;
+    case 64: hipLaunchKernelGGL(diag_xdma<18>, dim3(grid), dim3(256), 0, s, b, n, len, stride, o); break;
+    case 65: hipLaunchKernelGGL(diag_xdma<19>, dim3(grid), dim3(256), 0, s, b, n, len, stride, o); break;
+    case 66: hipLaunchKernelGGL(diag_xdma<1>, dim3(grid), dim3(256), 0, s, b, n, len, stride, o); break;
     case 59: hipLaunchKernelGGL(diag_xdma2<2>, dim3((uint32_t)((n + 127) / 128)), dim3(128), 0, s, b, n, len, stride, o); break;
     case 60: hipLaunchKernelGGL(diag_xdma2<1>, dim3((uint32_t)((n + 63) / 64)), dim3(64), 0, s, b, n, len, stride, o); break;
     case 58: hipLaunchKernelGGL(diag_xdma<0>, dim3(grid), dim3(256), 0, s, b, n, len, stride, o); break;
