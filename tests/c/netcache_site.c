@@ -23,6 +23,8 @@
  *      DMA, AUTO (§2e)
  *   6. md5hip_pool over device 0 listed twice (§2d)
  *   7. MD5Init/Update/Final page by page (the per-message drop-in, §1)
+ *   8. the device entry: blocks packed into a batch arena (md5hip_arena_alloc),
+ *      order and kernel from md5hip_plan_desc, md5hip_digest_desc_variant
  *
  * Exit 0 = all equal; 1 = a mismatch or error; 77 = no usable HIP device
  * (md5hip_batcher_create returned -ENODEV: the batched entries fail loudly,
@@ -34,6 +36,8 @@
 #include <stdlib.h>
 #include <string.h>
 #include <unistd.h>
+
+#include <hip/hip_runtime_api.h>
 
 #include "md5.h"
 #include "md5hip.h"
@@ -267,6 +271,53 @@ int main(void)
         CHECK(memcmp(d, want_md5[b], 16) == 0, "MD5Init/Update/Final block %d", b);
     }
 
+    /* 8. device-resident producer: the blocks packed into a
+     * batch arena, planned on the host, hashed by the device entry */
+    {
+        void *d_arena = NULL, *d_off = NULL, *d_len = NULL, *d_ord = NULL, *d_dig = NULL;
+        uint64_t offs[NBLK_MAX], at = 0;
+        uint32_t lens[NBLK_MAX], order[NBLK_MAX];
+        for (int b = 0; b < nblk; b++) {
+            lens[b] = (uint32_t)blk_valid_len(&inode, blks[b]);
+            offs[b] = at;
+            at += (lens[b] + 15u) & ~15u;
+        }
+        rc = md5hip_arena_alloc(0, at + 64, &d_arena);
+        CHECK(rc == 0 && d_arena && ((uintptr_t)d_arena & ((1u << 30) - 1)) == 0,
+              "md5hip_arena_alloc = %d", rc);
+        const int var = md5hip_plan_desc(lens, (uint64_t)nblk, order);
+        CHECK(var >= 0, "md5hip_plan_desc = %d", var);
+        int ok = rc == 0 && var >= 0 &&
+                 hipMalloc(&d_off, sizeof offs) == hipSuccess &&
+                 hipMalloc(&d_len, sizeof lens) == hipSuccess &&
+                 hipMalloc(&d_ord, sizeof order) == hipSuccess &&
+                 hipMalloc(&d_dig, 16 * NBLK_MAX) == hipSuccess;
+        for (int b = 0; ok && b < nblk; b++) {
+            gather(&inode, blks[b], tmp);
+            ok = hipMemcpy((unsigned char *)d_arena + offs[b], tmp, lens[b],
+                           hipMemcpyHostToDevice) == hipSuccess;
+        }
+        ok = ok && hipMemcpy(d_off, offs, sizeof offs, hipMemcpyHostToDevice) == hipSuccess &&
+             hipMemcpy(d_len, lens, sizeof lens, hipMemcpyHostToDevice) == hipSuccess &&
+             hipMemcpy(d_ord, order, sizeof order, hipMemcpyHostToDevice) == hipSuccess;
+        CHECK(ok, "arena staging");
+        if (ok) {
+            rc = md5hip_digest_desc_variant(d_arena, d_off, d_len, d_ord, (uint64_t)nblk, d_dig,
+                                            NULL, var);
+            CHECK(rc == 0, "md5hip_digest_desc_variant(%d) = %d", var, rc);
+            memset(digest, 0, sizeof digest);
+            CHECK(hipMemcpy(digest, d_dig, 16 * (size_t)nblk, hipMemcpyDeviceToHost) == hipSuccess,
+                  "digest copy");
+            for (int b = 0; b < nblk; b++)
+                CHECK(memcmp(digest[b], want_md5[b], 16) == 0, "arena block %d", b);
+        }
+        (void)hipFree(d_off);
+        (void)hipFree(d_len);
+        (void)hipFree(d_ord);
+        (void)hipFree(d_dig);
+        if (d_arena) CHECK(md5hip_arena_free(d_arena) == 0, "md5hip_arena_free");
+    }
+
     free(tmp);
     free(heap);
     if (failures) {
@@ -274,7 +325,7 @@ int main(void)
         return 1;
     }
     printf("netcache_site ok: %d blocks (%llu bytes, %d pages scattered), MD5 / CRC-32 / fastcrc / "
-           "verify / async / zero-copy x3 / pool / MD5Init-Update-Final bit-exact vs oracle\n",
+           "verify / async / zero-copy x3 / pool / MD5Init-Update-Final / arena+plan bit-exact vs oracle\n",
            nblk, (unsigned long long)inode.size, npages);
     return 0;
 }
