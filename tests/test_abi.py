@@ -129,6 +129,12 @@ def test_argument_errors_before_device_work():
     assert L.md5_batch_submit_iov_async(None, None, None, 1, None, ctypes.byref(t)) == EINVAL
     assert L.md5_batch_wait(None, 0) == EINVAL
     assert L.md5_batch_poll(None, 0) == EINVAL
+    p = ctypes.c_void_p()
+    assert L.md5hip_arena_alloc(0, 0, ctypes.byref(p)) == EINVAL
+    assert L.md5hip_arena_alloc(0, 1 << 20, None) == EINVAL
+    assert L.md5hip_arena_free(None) == EINVAL
+    assert L.md5hip_arena_free(ctypes.c_void_p(1 << 30)) == -errno.ENOENT     # not an arena
+    assert L.md5hip_plan_desc(None, 5, None) == EINVAL
 
 
 def test_plan_order_longest_first():
