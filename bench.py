@@ -1,65 +1,181 @@
 #!/usr/bin/env python3
 """bench.py -- device-resident batched MD5 throughput on MI355X.
 
-Metric (BASELINE.json): device-resident MD5 GiB/s on batched 16 KiB chunks.
-A "step" = one pass of the batched-MD5 kernel over the rank's whole batch
-(default 1,048,576 x 16 KiB = 16 GiB, BASELINE config C2), inputs already in
-HBM (filled on the device by md5hip_fill_synthetic, per-rank seed).
+Metric (BASELINE.json): device-resident MD5 GiB/s on batched 16 KiB chunks at
+1/2/4/8 MI355X.  A "step" = one pass of the batched-MD5 kernel over the rank's
+whole batch, inputs already in HBM (filled on the device by
+md5hip_fill_synthetic, per-rank seed).  Per GPU: 1,048,576 x 16 KiB (C2) at
+N = 1, 2,097,152 x 16 KiB (the C4 shard: 16 M chunks over 8 GPUs) at N > 1.
 
-    python bench.py [--gpus N --steps K --warmup W] [--config c2|c3|c5|crc]
+    python bench.py [--gpus N --steps K --warmup W] [--config c2|c3|c3q|c5|crc]
 
-N > 1: one process per GPU (torch.distributed.run); each rank hashes its own
-shard of independent chunks (weak scaling, no data-path collective); barrier +
+N > 1: one process per GPU.  Under torch.distributed.run (WORLD_SIZE set) the
+ranks are the launcher's and WORLD_SIZE must equal N.  A plain
+`python bench.py --gpus N` starts torch.distributed.run itself, as a CHILD
+process before this process touches the GPU (never an exec), and exits with
+its status: rank 0's JSON line is the output.  Each rank hashes its own shard
+of independent chunks (weak scaling, no data-path collective); barrier +
 device sync bracket the K timed steps and the MAX time over ranks is used.
-Rank 0 prints ONE JSON line.  The cpu_baseline leg (rank 0, N=1 only) runs the
-reference md5.c (oracle/_ref, else the oracle port) on the C1 sample; it is the
-only use of oracle/ here.
+The line carries `per_gpu` (each rank's own GiB/s) and `ranks_seen` (world
+size, backend, and the device every rank hashed on).
+
+The cpu_baseline leg (the only use of oracle/ here) runs the host reference
+md5.c (oracle/_ref, else the oracle port): timed on the C1 sample (rank 0,
+N = 1), and -- as the checker, outside the timed region -- re-digesting a
+sample of the very batch each rank hashed (`parity` in the line).
 """
 import argparse
+import ctypes
 import json
 import os
 import platform
+import socket
 import subprocess
 import sys
 import time
-
-import torch
+from concurrent.futures import ThreadPoolExecutor
 
 REPO = os.path.dirname(os.path.abspath(__file__))
-sys.path.insert(0, REPO)
-from sproxy_amd import md5 as m  # noqa: E402
-from sproxy_amd.shard import barrier, env_rank, max_over_ranks, shard_range  # noqa: E402
-
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 PCIE_PEAK_GBS = 63.0           # PCIe Gen5 x16 (spec)
 METRIC = "device-resident MD5 GiB/s on batched 16 KiB chunks at 1/2/4/8 MI355X"
 GIB = float(1 << 30)
+CPU_SHARE = 16                 # host cores a one-GPU box grants a job (the box's CPU share)
+
+torch = m = None               # imported after the launcher decision (see main)
+COLL_DEVICE = "cuda"           # where the control-plane scalars live (cpu under gloo)
 
 
-COLL_DEVICE = "cuda"             # where the control-plane scalars live (cpu under gloo)
+# --------------------------------------------------------------------------- launch
+def parse_args(argv):
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=50)
+    p.add_argument("--warmup", type=int, default=20,
+                   help="untimed launches first: the board settles its clock over the first ~15 "
+                        "launches of a 3 ms kernel (slow start, profiles/r01_bench_kernel_trace_startup.json)")
+    p.add_argument("--config", default="c2", choices=["c2", "c3", "c3q", "c5", "crc"])
+    p.add_argument("--chunks", type=int, default=0,
+                   help="chunks per GPU (weak scaling); 0 = 1,048,576 (C2) at N=1, "
+                        "2,097,152 (the C4 shard) at N>1")
+    p.add_argument("--total-chunks", type=int, default=0,
+                   help="one global batch split across ranks (strong scaling; C4 = 16777216)")
+    p.add_argument("--len", type=int, default=16384)
+    p.add_argument("--variant", default="auto")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--parity-sample", type=int, default=4096,
+                   help="chunks per rank re-digested by the host reference after timing (0 = off)")
+    p.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                   help="control-plane backend for N > 1 (barrier + scalar MAX + gathers only)")
+    p.add_argument("--dry-run", action="store_true",
+                   help="CPU only (no GPU): exercises launch, ranks and aggregation with the "
+                        "product's host MD5 (md5_stream.c) on a small host batch")
+    p.add_argument("--traffic", default=os.path.join(REPO, "profiles", "traffic.json"))
+    p.add_argument("--fastcrc", type=int, default=0, help="--config crc: blk_make_crc fastcrc window")
+    p.add_argument("--c3-bytes", type=int, default=16 << 30)
+    p.add_argument("--c3-variant", default="plan",
+                   help="descriptor kernel for C3 (plan = md5hip_plan_desc's choice)")
+    p.add_argument("--c3-coalesce", type=int, default=3,
+                   help="C3 batches planned and launched together for the coalesced rate (0/1 = off)")
+    p.add_argument("--c3-streams", type=int, default=3,
+                   help="streams for C3's streamed rate (batches in flight)")
+    p.add_argument("--c3-legs", default="all", choices=["all", "main"],
+                   help="main: only the single-batch launches (PMC passes count one kernel)")
+    p.add_argument("--c3q-batches", type=int, default=6,
+                   help="--config c3q: C3 submissions streamed through one md5hip_queue")
+    p.add_argument("--c5-chunks", type=int, default=1 << 18)
+    p.add_argument("--c5-slice", type=int, default=64 << 20)
+    return p.parse_args(argv)
 
 
-def dist_setup(ngpus, backend="nccl"):
-    """One process per GPU.  The only collectives are a barrier and one scalar
-    MAX, so `--dist-backend gloo` (CPU) is equivalent; it lets N ranks share
-    one GPU for a rehearsal of the N > 1 path on a one-GPU box."""
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def spawn_ranks(a, argv):
+    """`--gpus N` (N > 1) without a launcher: run torch.distributed.run as a
+    child process -- this process has not initialised the GPU, and it is not
+    replaced (no exec) -- and return the child's exit status.  Rank 0 of the
+    child prints the JSON line on the inherited stdout."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={a.gpus}", "--master-addr=127.0.0.1", f"--master-port={free_port()}",
+           os.path.abspath(__file__), *argv]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.setdefault("OMP_NUM_THREADS", "1")
+    return subprocess.call(cmd, env=env)
+
+
+def env_rank():
+    return (int(os.environ.get("RANK", "0")), int(os.environ.get("WORLD_SIZE", "1")),
+            int(os.environ.get("LOCAL_RANK", "0")))
+
+
+def dist_setup(a):
+    """One process per GPU.  The collectives are a barrier, scalar MAX/SUM
+    reductions and small object gathers, so gloo (CPU) serves as well as RCCL;
+    it lets N ranks share one GPU for a rehearsal on a one-GPU box."""
     global COLL_DEVICE
     rank, world, local = env_rank()
-    if world != ngpus and world > 1:
-        raise SystemExit(f"--gpus {ngpus} but WORLD_SIZE={world}")
-    ndev = torch.cuda.device_count()
-    if backend == "nccl" and world > 1 and local >= ndev:
-        raise SystemExit(f"LOCAL_RANK {local} but only {ndev} GPUs visible")
-    torch.cuda.set_device(local % ndev)
+    if world != a.gpus:
+        raise SystemExit(f"bench.py: --gpus {a.gpus} but WORLD_SIZE={world}")
+    backend = "gloo" if a.dry_run else a.dist_backend
+    device = None
+    if not a.dry_run:
+        ndev = torch.cuda.device_count()
+        if ndev < 1:
+            raise SystemExit("bench.py: no HIP device visible (use --dry-run on a CPU host)")
+        if backend == "nccl" and world > 1 and local >= ndev:
+            raise SystemExit(f"bench.py: LOCAL_RANK {local} but only {ndev} GPUs visible")
+        device = local % ndev
+        torch.cuda.set_device(device)
     if world > 1:
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            dist.init_process_group("nccl", device_id=torch.device("cuda", device))
         else:
-            dist.init_process_group(backend)
-            COLL_DEVICE = "cpu"
-    return rank, world, local
+            dist.init_process_group("gloo")
+        COLL_DEVICE = "cuda" if backend == "nccl" else "cpu"
+    return rank, world, local, device, backend
+
+
+def barrier(world):
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+
+
+def max_over_ranks(x, world):
+    if world == 1:
+        return float(x)
+    import torch.distributed as dist
+    t = torch.tensor([float(x)], dtype=torch.float64, device=COLL_DEVICE)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def gather_objects(obj, world):
+    if world == 1:
+        return [obj]
+    import torch.distributed as dist
+    out = [None] * world
+    dist.all_gather_object(out, obj)
+    return out
+
+
+def device_info(rank, local, device):
+    d = {"rank": rank, "local_rank": local, "host": socket.gethostname(), "device": device}
+    if device is not None:
+        p = torch.cuda.get_device_properties(device)
+        d.update(name=p.name, uuid=str(getattr(p, "uuid", "")),
+                 pci=f"{getattr(p, 'pci_domain_id', 0):04x}:{getattr(p, 'pci_bus_id', 0):02x}:"
+                     f"{getattr(p, 'pci_device_id', 0):02x}")
+    return d
 
 
 def timed_steps(fn, steps, warmup, world):
@@ -94,7 +210,88 @@ def cpu_model():
     return platform.processor() or "unknown"
 
 
-CPU_SHARE = 16      # host cores a one-GPU box grants a job (the box's CPU share)
+# --------------------------------------------------------------------------- cpu_baseline leg
+# The host reference md5.c (oracle/_ref, built in place from /root/reference;
+# else the oracle restatement).  Timed on the C1 sample for the baseline, and
+# used -- outside every timed region -- as the CHECKER of a sample of the
+# batch the GPU hashed.  Nothing here is on the measured path.
+class _HostRef:
+    def __init__(self):
+        ref = os.path.join(REPO, "oracle", "_ref", "libmd5_ref.so")
+        port = os.path.join(REPO, "oracle", "_build", "libmd5_oracle.so")
+        if os.path.exists(ref):
+            self.lib, self.kind = ctypes.CDLL(ref), "reference md5.c (oracle/_ref)"
+            vp = ctypes.c_void_p
+            self.lib.MD5Init.argtypes = [vp]
+            self.lib.MD5Update.argtypes = [vp, vp, ctypes.c_uint]
+            self.lib.MD5Final.argtypes = [vp, vp]
+        elif os.path.exists(port):
+            self.lib, self.kind = ctypes.CDLL(port), "oracle restatement (oracle/_build)"
+            self.lib.oracle_md5.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p]
+        else:
+            self.lib = None
+            self.kind = "absent"
+
+    def digest(self, buf, off, n):
+        """MD5 of buf[off:off+n] (buf: contiguous numpy uint8)."""
+        out = (ctypes.c_ubyte * 16)()
+        p = buf.ctypes.data + off
+        if self.kind.startswith("reference"):
+            ctx = (ctypes.c_ubyte * 88)()
+            self.lib.MD5Init(ctx)
+            done = 0
+            while True:                          # md5.h:47 takes an unsigned length
+                part = min(n - done, 1 << 30)
+                self.lib.MD5Update(ctx, p + done, part)
+                done += part
+                if done >= n:
+                    break
+            self.lib.MD5Final(out, ctx)
+        else:
+            self.lib.oracle_md5(p, n, out)
+        return bytes(out)
+
+
+def check_sample(buf, offs, lens, got, threads=8):
+    """parity of a sample: host reference digests of (buf, offs, lens) vs the
+    GPU's digests `got` (uint8 [k, 16])."""
+    import numpy as np
+    ref = _HostRef()
+    if ref.lib is None:
+        return {"checked": 0, "ok": None, "checker": "absent"}
+    k = len(lens)
+    with ThreadPoolExecutor(max_workers=threads) as ex:     # ctypes releases the GIL
+        exp = list(ex.map(lambda j: ref.digest(buf, int(offs[j]), int(lens[j])), range(k)))
+    exp = np.frombuffer(b"".join(exp), dtype=np.uint8).reshape(k, 16)
+    bad = int((exp != got).any(axis=1).sum())
+    return {"checked": k, "mismatches": bad, "ok": bad == 0, "checker": ref.kind,
+            "sample_bytes": int(np.sum(np.asarray(lens, dtype=np.int64)))}
+
+
+def sample_fixed(data, out, n, L, k, seed):
+    """(parity dict) for k sampled chunks (first and last included) of a
+    fixed-length device batch; chunk rows gathered on the device, one D2H."""
+    import numpy as np
+    if k <= 0:
+        return None
+    rng = np.random.default_rng(seed)
+    idx = np.unique(np.concatenate([[0, n - 1], rng.integers(0, n, size=max(0, min(k, n) - 2))]))
+    it = torch.from_numpy(idx.astype(np.int64)).to(data.device)
+    rows = data[: n * L].view(n, L).index_select(0, it).cpu().numpy().reshape(-1)
+    got = out.index_select(0, it).cpu().numpy()
+    return check_sample(rows, np.arange(idx.size, dtype=np.int64) * L, np.full(idx.size, L), got)
+
+
+def sample_desc(data, offs, lens, out, idx):
+    """(parity dict) for the chunks `idx` of a descriptor batch in device `data`."""
+    import numpy as np
+    idx = np.unique(np.asarray(idx, dtype=np.int64))
+    parts = [data[int(offs[j]): int(offs[j]) + int(lens[j])] for j in idx]
+    flat = torch.cat(parts).cpu().numpy() if parts else np.empty(0, np.uint8)
+    l_s = lens[idx].astype(np.int64)
+    o_s = np.concatenate([[0], np.cumsum(l_s)[:-1]]) if idx.size else l_s
+    got = out.index_select(0, torch.from_numpy(idx).to(out.device)).cpu().numpy()
+    return check_sample(flat, o_s, l_s, got)
 
 
 def cpu_baseline(reps=10, threads=1):
@@ -134,106 +331,223 @@ def cpu_baseline_crc(reps=7):
             "fold_ok": r["fold"] == "ad5b15d5"}
 
 
-def load_traffic(path, variant):
-    """HBM bytes per launch from a committed rocprofv3 PMC summary (profiles/)."""
+# --------------------------------------------------------------------------- traffic evidence
+def load_traffic(path, kernel, workload):
+    """HBM bytes per launch of `kernel` on `workload` from the committed
+    rocprofv3 PMC summary (profiles/traffic.json, scripts/traffic_json.py),
+    keyed by the SHA-256 of libmd5hip.so's device code object: a summary taken
+    from other kernel code, or another workload, reads as null."""
     if not path or not os.path.exists(path):
-        return None
+        return None, "no traffic summary"
     try:
         d = json.load(open(path))
-        return d.get(variant, d.get("default"))
-    except Exception:
-        return None
+    except Exception as e:  # pragma: no cover
+        return None, f"unreadable: {e}"
+    h = m.code_object_hash()
+    ent = d.get("by_code_object", {}).get(h)
+    if ent is None:
+        return None, f"stale: no PMC summary for code object {h[:16]}"
+    v = ent.get("kernels", {}).get(f"{kernel}@{workload}")
+    if v is None:
+        return None, f"no PMC entry for {kernel}@{workload} (code object {h[:16]})"
+    return v["bytes"], f"rocprofv3 PMC FETCH_SIZE/WRITE_SIZE, code object {h[:16]}, {v.get('source', '')}"
 
 
-def run_c2(a, rank, world):
+# --------------------------------------------------------------------------- configs
+def per_rank_line(res, rank, world, local, device, backend, rank_bytes, rank_wall, parity):
+    """Gather every rank's own rate, device and parity into the line."""
+    mine = {"gib_s": round(rank_bytes / rank_wall / GIB, 2) if rank_wall else 0.0,
+            "dev": device_info(rank, local, device), "parity": parity}
+    allr = gather_objects(mine, world)
+    res["per_gpu"] = [r["gib_s"] for r in allr]
+    devs = [r["dev"] for r in allr]
+    res["ranks_seen"] = {"world": world, "backend": backend if world > 1 else None,
+                         "distinct_devices": len({(d["host"], d.get("uuid") or d["device"]) for d in devs
+                                                  if d["device"] is not None}),
+                         "ranks": devs}
+    ps = [r["parity"] for r in allr if r["parity"] is not None]
+    if ps:
+        res["parity"] = {"ok": all(p["ok"] for p in ps), "checked": sum(p["checked"] for p in ps),
+                         "mismatches": sum(p.get("mismatches", 0) for p in ps),
+                         "checker": ps[0]["checker"],
+                         "sample": "first + last + seeded-random chunks of every rank's batch, "
+                                   "re-digested on the host after the timed region"}
+    return res
+
+
+def run_dry(a, rank, world, local, device, backend):
+    """CPU dry run: the launch, rank and aggregation path with no GPU -- each
+    rank hashes a small host batch with the product's host MD5 (md5_stream.c)."""
+    import numpy as np
+    n, L = (a.chunks or 64), a.len
+    buf = np.random.default_rng(0x5EED0000 + rank).integers(0, 256, n * L, dtype=np.uint8)
+    out = np.empty((n, 16), dtype=np.uint8)
+
+    def step():
+        for i in range(n):
+            out[i] = np.frombuffer(m.md5(buf[i * L:(i + 1) * L]), dtype=np.uint8)
+
+    for _ in range(a.warmup):
+        step()
+    barrier(world)
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step()
+    wall = time.perf_counter() - t0
+    barrier(world)
+    wall_max = max_over_ranks(wall, world)
+    par = None
+    if a.parity_sample:
+        k = min(n, a.parity_sample)
+        par = check_sample(buf, np.arange(k) * L, np.full(k, L), out[:k])
+    res = {"metric": METRIC + " [CPU dry run]", "value": round(n * L * world * a.steps / wall_max / GIB, 4),
+           "unit": "GiB/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+           "ms_per_step": round(wall_max / a.steps * 1e3, 4), "higher_is_better": True,
+           "scaling": "weak", "vs_baseline": None, "dtype": "u32", "dry_run": True,
+           "data": "synthetic host buffers (CPU dry run: product host MD5, no GPU)",
+           "config": {"workload": f"dry run: {n} x {L} B host chunks per rank",
+                      "chunks_per_gpu": n, "chunk_bytes": L,
+                      "parallelism": f"dp{world} (independent chunk shards, no collective)"}}
+    return per_rank_line(res, rank, world, local, device, backend, n * L * a.steps, wall, par)
+
+
+def c2_shape(a, rank, world):
+    if a.total_chunks:       # strong form: one global batch split into contiguous shards
+        lo = a.total_chunks * rank // world
+        hi = a.total_chunks * (rank + 1) // world
+        return hi - lo, a.total_chunks
+    n = a.chunks or ((1 << 20) if world == 1 else (1 << 21))
+    return n, n * world
+
+
+def c2_workload(n, n_all, L, world, strong):
+    if (n, L, world, strong) == (1 << 20, 16384, 1, False):
+        return "C2: 1,048,576 x 16 KiB chunks per GPU, device-resident"
+    if n == (1 << 21) and L == 16384 and not strong:
+        return (f"C4 shard: 2,097,152 x 16 KiB chunks per GPU, {n_all:,} on {world} GPU(s) "
+                f"(C4 = 16,777,216 on 8), device-resident")
+    return f"{n_all} x {L} B chunks total, {n} per GPU, device-resident"
+
+
+def run_c2(a, rank, world, local, device, backend):
     L = a.len
-    if a.total_chunks:       # strong / C4 form: one global batch split into contiguous shards
-        lo, hi = shard_range(a.total_chunks, rank, world)
-        n = hi - lo
-    else:                    # weak scaling: a fixed per-GPU batch (C2 shape on every GPU)
-        n = a.chunks
+    n, n_all = c2_shape(a, rank, world)
     data = torch.empty(n * L, dtype=torch.uint8, device="cuda")
     m.fill_synthetic(data, seed=0x5EED0000 + rank)
     out = torch.empty((n, 16), dtype=torch.uint8, device="cuda")
     variant = m.VARIANTS[a.variant]
     fn = lambda: m.digest_fixed(data, n, L, out=out, variant=variant)  # noqa: E731
     wall, dev_ms = timed_steps(fn, a.steps, a.warmup, world)
-    wall_max = max_over_ranks(wall, world, COLL_DEVICE)
-    dev_ms_max = max_over_ranks(dev_ms, world, COLL_DEVICE)
-    n_all = a.total_chunks if a.total_chunks else n * world
-    total_bytes = float(n_all) * L * a.steps
-    value = total_bytes / wall_max / GIB
+    wall_max = max_over_ranks(wall, world)
+    dev_ms_max = max_over_ranks(dev_ms, world)
+    value = float(n_all) * L * a.steps / wall_max / GIB
     alg_bytes = float(n) * (L + 16)            # read every chunk once + 16-B digest write
     achieved = alg_bytes / (dev_ms_max * 1e-3) / 1e9
     vname = m.variant_name(m.resolve_variant(variant))
+    kname = "md5_fixed_" + vname
+    traffic, tnote = load_traffic(a.traffic, kname, f"c2@{n}x{L}")
     res = {
         "metric": METRIC, "value": round(value, 2), "unit": "GiB/s", "n_gpus": world,
         "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(wall_max / a.steps * 1e3, 4),
         "higher_is_better": True, "scaling": "strong" if a.total_chunks else "weak",
         "vs_baseline": None, "dtype": "u32",
         "data": "synthetic (device-generated splitmix words, per-rank seed)",
-        "config": {"workload": ("C2: 1,048,576 x 16 KiB chunks per GPU, device-resident"
-                                if (n, L) == (1 << 20, 16384) and not a.total_chunks else
-                                f"{n_all} x {L} B chunks total, {n} on rank 0, device-resident"),
+        "config": {"workload": c2_workload(n, n_all, L, world, bool(a.total_chunks)),
                    "chunks_per_gpu": n, "chunk_bytes": L, "kernel_variant": vname,
                    "parallelism": f"dp{world} (independent chunk shards, no collective)"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                     "traffic": load_traffic(a.traffic, vname),
-                     "kernel": "md5hip " + vname, "avg_launch_ms": round(dev_ms_max, 4),
+                     "traffic": traffic, "traffic_source": tnote,
+                     "kernel": "md5hip::" + kname, "avg_launch_ms": round(dev_ms_max, 4),
                      "alg_bytes_per_launch": int(alg_bytes)},
     }
-    return res
+    par = sample_fixed(data, out, n, L, a.parity_sample, seed=77 + rank)
+    return per_rank_line(res, rank, world, local, device, backend, float(n) * L * a.steps, wall, par)
 
 
-def run_crc(a, rank, world):
+def run_crc(a, rank, world, local, device, backend):
     """§8f row 2: netcache's own block checksum (CRC-32, crc32.c) over the C2
-    shape, device-resident; the same step/timing rules as C2."""
-    L, n = a.len, a.chunks
+    shape, device-resident; the same step/timing rules as C2.  --fastcrc F:
+    blk_make_crc's head^tail window (blk_io.c:408-424), F bytes at each end."""
+    L = a.len
+    n = a.chunks or (1 << 20)
+    F = a.fastcrc
     data = torch.empty(n * L, dtype=torch.uint8, device="cuda")
     m.fill_synthetic(data, seed=0x5EED0000 + rank)
     out = torch.empty(n, dtype=torch.int32, device="cuda")
-    fn = lambda: m.crc32_fixed(data, n, L, out=out)  # noqa: E731
+    fn = lambda: m.crc32_fixed(data, n, L, fastcrc=F, out=out)  # noqa: E731
     wall, dev_ms = timed_steps(fn, a.steps, a.warmup, world)
-    wall_max = max_over_ranks(wall, world, COLL_DEVICE)
-    dev_ms_max = max_over_ranks(dev_ms, world, COLL_DEVICE)
-    value = float(n) * L * world * a.steps / wall_max / GIB
-    alg_bytes = float(n) * (L + 4)
-    vname = "crc32 " + m.crc_variant_name(0)
+    wall_max = max_over_ranks(wall, world)
+    dev_ms_max = max_over_ranks(dev_ms, world)
+    fast = 0 < F < L
+    read = 2 * F if fast else L                 # bytes blk_make_crc reads per block
+    alg_bytes = float(n) * (read + 4)
+    kname = m.crc_kernel_name(L, F)
     achieved = alg_bytes / (dev_ms_max * 1e-3) / 1e9
-    return {"metric": "device-resident CRC-32 (netcache blk_make_crc) GiB/s on batched 16 KiB chunks",
-            "value": round(value, 2), "unit": "GiB/s", "n_gpus": world, "steps": a.steps,
-            "warmup": a.warmup, "ms_per_step": round(wall_max / a.steps * 1e3, 4),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32",
-            "data": "synthetic (device-generated splitmix words, per-rank seed)",
-            "config": {"workload": f"{n} x {L} B chunks per GPU, device-resident, fastcrc 0",
-                       "chunks_per_gpu": n, "chunk_bytes": L, "kernel_variant": vname},
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "traffic": load_traffic(a.traffic, vname), "kernel": vname,
-                         "avg_launch_ms": round(dev_ms_max, 4), "alg_bytes_per_launch": int(alg_bytes)}}
+    traffic, tnote = load_traffic(a.traffic, kname, f"crc@{n}x{L}f{F}")
+    res = {"metric": ("device-resident CRC-32 (netcache blk_make_crc) GiB/s on batched 16 KiB chunks"
+                      if not fast else
+                      f"device-resident fastcrc={F} CRC-32 (netcache blk_make_crc) blocks/s"),
+           "value": (round(float(n) * L * world * a.steps / wall_max / GIB, 2) if not fast else
+                     round(float(n) * world * a.steps / wall_max, 1)),
+           "unit": "GiB/s" if not fast else "blocks/s", "n_gpus": world, "steps": a.steps,
+           "warmup": a.warmup, "ms_per_step": round(wall_max / a.steps * 1e3, 4),
+           "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32",
+           "data": "synthetic (device-generated splitmix words, per-rank seed)",
+           "config": {"workload": f"{n} x {L} B chunks per GPU, device-resident, fastcrc {F}",
+                      "chunks_per_gpu": n, "chunk_bytes": L, "kernel": kname,
+                      "block_payload_gib_s": round(float(n) * L * world * a.steps / wall_max / GIB, 2)},
+           "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                        "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                        "traffic": traffic, "traffic_source": tnote, "kernel": "md5hip::" + kname,
+                        "avg_launch_ms": round(dev_ms_max, 4), "alg_bytes_per_launch": int(alg_bytes),
+                        "alg_bytes_note": f"{read} B read per block (+4 B CRC written)"}}
+    return per_rank_line(res, rank, world, local, device, backend, float(n) * L * a.steps, wall, None)
 
 
-def run_c3(a, rank, world):
+def c3_lens(total_bytes, seed):
+    """C3 lengths: classes 4 KiB..1 MiB, 1 in 8 a ragged
+    tail in [1, class) (blk_io.c:377), until `total_bytes` of payload."""
+    import numpy as np
+    rng = np.random.default_rng(seed)
+    classes = np.array([4096 << k for k in range(9)], dtype=np.int64)
+    out, tot = [], 0
+    while tot < total_bytes:
+        c = int(classes[rng.integers(0, 9)])
+        if rng.integers(0, 8) == 0:
+            c = int(rng.integers(1, c))
+        out.append(c)
+        tot += c
+    return np.array(out, dtype=np.int64)
+
+
+def c3_offsets(lens):
+    import numpy as np
+    offs = np.concatenate([[0], np.cumsum((lens + 15) // 16 * 16)[:-1]])
+    return offs, int(offs[-1] + lens[-1] + 16)
+
+
+def c3_sample(lens, order, k, seed):
+    """C3 parity sample: seeded-random chunks, the first and last in lane
+    order, every length class and 64 of each ragged residue len % 64 in
+    {1, 55, 56, 63, 0}."""
+    import numpy as np
+    rng = np.random.default_rng(seed)
+    pick = [rng.integers(0, lens.size, size=max(0, k - 2)), [order[0], order[-1]]]
+    for c in [4096 << j for j in range(9)]:
+        pick.append(np.flatnonzero(lens == c)[:8])
+    rag = ~np.isin(lens, [4096 << j for j in range(9)])
+    for r in (1, 55, 56, 63, 0):
+        pick.append(np.flatnonzero(rag & (lens % 64 == r))[:64])
+    return np.unique(np.concatenate([np.asarray(p, dtype=np.int64) for p in pick]))
+
+
+def run_c3(a, rank, world, local, device, backend):
     """Mixed lengths 4 KiB..1 MiB (netcache chunk_size range, httpd.c:7968) with
     1-in-8 ragged tails, packed 16-B aligned, lanes packed longest-first."""
     import numpy as np
-
-    def c3_lens(seed):
-        rng = np.random.default_rng(seed)
-        classes = np.array([4096 << k for k in range(9)], dtype=np.int64)
-        out, tot = [], 0
-        while tot < a.c3_bytes:
-            c = int(classes[rng.integers(0, 9)])
-            if rng.integers(0, 8) == 0:
-                c = int(rng.integers(1, c))
-            out.append(c)
-            tot += c
-        return np.array(out, dtype=np.int64)
-
-    lens = c3_lens(1000 + rank)
-    offs = np.concatenate([[0], np.cumsum((lens + 15) // 16 * 16)[:-1]])
-    total = int(offs[-1] + lens[-1] + 16)
+    lens = c3_lens(a.c3_bytes, 1000 + rank)
+    offs, total = c3_offsets(lens)
     # the batch lives in an arena (md5hip_arena_alloc: 1 GiB-aligned virtual
     # range, large page-table fragments), where HYBRID's lane-direct chains
     # run ~7 % faster than in a 2 MiB-aligned hipMalloc buffer
@@ -250,15 +564,23 @@ def run_c3(a, rank, world):
     out = torch.empty((lens.size, 16), dtype=torch.uint8, device="cuda")
     fn = lambda: m.digest_desc(data, d_off, d_len, d_ord, out=out, variant=dvar)  # noqa: E731
     wall, dev_ms = timed_steps(fn, a.steps, a.warmup, world)
-    wall_max = max_over_ranks(wall, world, COLL_DEVICE)
+    wall_max = max_over_ranks(wall, world)
     payload = float(lens.sum())
     value = payload * world * a.steps / wall_max / GIB
+    par = sample_desc(data, offs, lens, out, c3_sample(lens, order, a.parity_sample // 2, 91 + rank)) \
+        if a.parity_sample else None
     # the longest chunk bounds the step: a 1 MiB chunk is 16,385 dependent
     # compressions on one lane.  A batched engine keeps several batches in
-    # flight (the batcher's slots), so batch k+1's short chunks run beside
-    # batch k's long chains: the same K batches issued round-robin on
-    # `c3_streams` streams (each batch complete, own digest array) give the
-    # streamed rate, reported beside the single-batch one.
+    # flight, so batch k+1's short chunks run beside batch k's long chains:
+    # the same K batches issued round-robin on `c3_streams` streams (each
+    # batch complete, own digest array) give the streamed rate.
+    if a.c3_legs == "main":
+        kname = "md5_desc_" + dvar
+        return per_rank_line({"metric": "C3 main launches only (profiling run)", "value": round(value, 2),
+                              "unit": "GiB/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+                              "config": {"workload": "C3 mixed lengths", "kernel": kname},
+                              "roofline": {"avg_launch_ms": round(dev_ms, 4)}},
+                             rank, world, local, device, backend, payload * a.steps, wall, par)
     ns = max(1, a.c3_streams)
     streams = [torch.cuda.Stream() for _ in range(ns)]
     outs = [torch.empty_like(out) for _ in range(ns)]
@@ -279,19 +601,18 @@ def run_c3(a, rank, world):
     t0 = time.perf_counter()
     streamed(a.steps)
     torch.cuda.synchronize()
-    s_wall = max_over_ranks(time.perf_counter() - t0, world, COLL_DEVICE)
+    s_wall = max_over_ranks(time.perf_counter() - t0, world)
     barrier(world)
     ok = all(torch.equal(o, out) for o in outs[:min(ns, a.steps)])
     del outs
     # coalesced: K such batches (own lengths, own bytes) planned and launched
-    # as one descriptor batch -- what a batcher holding K submissions does;
-    # the long chains of all K then overlap inside one launch
+    # as one descriptor batch by hand (what md5hip_queue does, --config c3q)
     coal = None
     K = a.c3_coalesce
     if K > 1:
-        lk = [lens] + [c3_lens(2000 + 17 * j + rank) for j in range(1, K)]
-        ok_ = [np.concatenate([[0], np.cumsum((x + 15) // 16 * 16)[:-1]]) for x in lk]
-        spans = [int((o[-1] + x[-1] + 16 + 15) // 16 * 16) for o, x in zip(ok_, lk)]
+        lk = [lens] + [c3_lens(a.c3_bytes, 2000 + 17 * j + rank) for j in range(1, K)]
+        ok_ = [c3_offsets(x)[0] for x in lk]
+        spans = [(c3_offsets(x)[1] + 15) // 16 * 16 for x in lk]
         starts = np.concatenate([[0], np.cumsum(spans)[:-1]])
         big = m.arena_empty(int(sum(spans)))
         m.fill_synthetic(big, seed=0xC3C + rank)
@@ -319,8 +640,7 @@ def run_c3(a, rank, world):
     # the bound of one mixed batch: each chunk is one serial chain on one lane
     # (md5.c:204-210, 64 dependent steps per block), so the batch ends no
     # earlier than its longest chunks -- timed alone (every chunk of the
-    # maximum length, same kernel variant as the batch; one lone chunk would
-    # understate the chip's clock, which drops when a single wave is active)
+    # maximum length, same kernel variant as the batch)
     il = np.flatnonzero(lens == lens.max())
     d_off1 = torch.from_numpy(offs[il]).cuda()
     d_len1 = torch.from_numpy(lens[il].astype(np.int32)).cuda()
@@ -328,37 +648,108 @@ def run_c3(a, rank, world):
     _, chain_ms = timed_steps(lambda: m.digest_desc(data, d_off1, d_len1, out=dig1, variant=dvar),
                               5, 2, world)
     del dig1
-    return {"metric": "device-resident MD5 GiB/s, mixed 4 KiB-1 MiB chunks (C3)",
-            "value": round(value, 2), "unit": "GiB/s", "n_gpus": world, "steps": a.steps,
-            "warmup": a.warmup, "ms_per_step": round(wall_max / a.steps * 1e3, 4),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32",
-            "data": "synthetic", "config": {"workload": "C3 mixed lengths", "chunks": int(lens.size),
-                                            "payload_bytes": int(payload),
-                                            "longest": int(lens.max()), "plan_ms": round(plan_ms, 3),
-                                            "kernel": "md5hip desc " + dvar,
-                                            "uniform_16k_ms": round(u_ms, 4),
-                                            "imbalance_vs_uniform": round(dev_ms / u_ms, 3)},
-            "roofline": {"bound": "hbm", "achieved": round(payload / (dev_ms * 1e-3) / 1e9, 1),
-                         "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(payload / (dev_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-                         "traffic": None,
-                         "longest_alone_ms": round(chain_ms, 4),
-                         "n_longest": int(il.size),
-                         "frac_of_longest_alone": round(chain_ms / dev_ms, 4),
-                         "note": "one batch ends with its longest chunks' serial chains "
-                                 "(longest_alone_ms: those chunks hashed alone); see streamed"},
-            "streamed": {"streams": ns, "value": round(payload * world * a.steps / s_wall / GIB, 2),
-                         "unit": "GiB/s", "ms_per_batch": round(s_wall / a.steps * 1e3, 4),
-                         "digests_equal_single": ok,
-                         "note": "the same K batches, round-robin over streams, "
-                                 "batch k+1 overlapping batch k's long chains"},
-            "coalesced": coal}
+    kname = "md5_desc_" + dvar
+    traffic, tnote = load_traffic(a.traffic, kname, f"c3@{a.c3_bytes}s{1000 + rank}")
+    achieved = payload / (dev_ms * 1e-3) / 1e9
+    res = {"metric": "device-resident MD5 GiB/s, mixed 4 KiB-1 MiB chunks (C3)",
+           "value": round(value, 2), "unit": "GiB/s", "n_gpus": world, "steps": a.steps,
+           "warmup": a.warmup, "ms_per_step": round(wall_max / a.steps * 1e3, 4),
+           "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32",
+           "data": "synthetic", "config": {"workload": "C3 mixed lengths", "chunks": int(lens.size),
+                                           "payload_bytes": int(payload),
+                                           "longest": int(lens.max()), "plan_ms": round(plan_ms, 3),
+                                           "kernel": "md5hip desc " + dvar,
+                                           "uniform_16k_ms": round(u_ms, 4),
+                                           "imbalance_vs_uniform": round(dev_ms / u_ms, 3)},
+           "roofline": {"bound": "hbm", "achieved": round(achieved, 1),
+                        "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": round(achieved / HBM_PEAK_GBS, 4),
+                        "traffic": traffic, "traffic_source": tnote, "kernel": "md5hip::" + kname,
+                        "avg_launch_ms": round(dev_ms, 4),
+                        "alg_bytes_per_launch": int(payload + 16 * lens.size),
+                        "chain_bound": {"longest_alone_ms": round(chain_ms, 4), "n_longest": int(il.size),
+                                        "frac": round(chain_ms / dev_ms, 4),
+                                        "note": "second roofline: the batch's longest chunks hashed "
+                                                "alone (serial chains, md5.c:204-210) / the batch"}},
+           "streamed": {"streams": ns, "value": round(payload * world * a.steps / s_wall / GIB, 2),
+                        "unit": "GiB/s", "ms_per_batch": round(s_wall / a.steps * 1e3, 4),
+                        "digests_equal_single": ok,
+                        "note": "the same K batches, round-robin over streams, "
+                                "batch k+1 overlapping batch k's long chains"},
+           "coalesced": coal}
+    return per_rank_line(res, rank, world, local, device, backend, payload * a.steps, wall, par)
 
 
-def run_c5(a, rank, world):
+def run_c3q(a, rank, world, local, device, backend):
+    """C3 through the product's device-input queue (md5hip_queue, include/
+    md5hip.h): `c3q_batches` distinct C3 batches (own lengths, own bytes)
+    submitted back to back, as netcache's ASIO threads would submit vectors;
+    the queue coalesces whatever is pending into one planned launch per slot
+    and completes each ticket on its own.  A step = submit all + wait all."""
+    import numpy as np
+    K = max(1, a.c3q_batches)
+    lk = [c3_lens(a.c3_bytes, 3000 + 31 * j + rank) for j in range(K)]
+    ok_ = [c3_offsets(x)[0] for x in lk]
+    spans = [(c3_offsets(x)[1] + 15) // 16 * 16 for x in lk]
+    starts = np.concatenate([[0], np.cumsum(spans)[:-1]]).astype(np.int64)
+    big = m.arena_empty(int(sum(spans)))
+    m.fill_synthetic(big, seed=0xC3D + rank)
+    base = big.data_ptr()
+    subs = []
+    for j in range(K):
+        ptrs = (base + starts[j] + ok_[j]).astype(np.uint64)
+        subs.append((ptrs, lk[j].astype(np.uint32),
+                     torch.empty((lk[j].size, 16), dtype=torch.uint8, device="cuda")))
+    q = m.Queue(device=torch.cuda.current_device())
+
+    def step():
+        ts = [q.submit_device(p, L_, o) for p, L_, o in subs]
+        for t in reversed(ts):             # any order: tickets complete independently
+            q.wait(t)
+
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize()
+    barrier(world)
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step()
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    barrier(world)
+    wall_max = max_over_ranks(wall, world)
+    stats = q.stats()
+    q.close()
+    payload = float(sum(x.sum() for x in lk))
+    value = payload * world * a.steps / wall_max / GIB
+    par = None
+    if a.parity_sample:
+        ps = []
+        for j in range(K):
+            idx = c3_sample(lk[j], np.argsort(-lk[j], kind="stable"), a.parity_sample // (2 * K), 5 + j)
+            ps.append(sample_desc(big, starts[j] + ok_[j], lk[j], subs[j][2], idx))
+        par = {"checked": sum(p["checked"] for p in ps), "mismatches": sum(p.get("mismatches", 0) for p in ps),
+               "ok": all(p["ok"] for p in ps), "checker": ps[0]["checker"]}
+    res = {"metric": "device-resident MD5 GiB/s, mixed 4 KiB-1 MiB chunks (C3) through md5hip_queue",
+           "value": round(value, 2), "unit": "GiB/s", "n_gpus": world, "steps": a.steps,
+           "warmup": a.warmup, "ms_per_step": round(wall_max / a.steps * 1e3, 4),
+           "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32",
+           "data": "synthetic", "tb_s": round(value * GIB / 1e12, 3),
+           "config": {"workload": f"C3 stream: {K} submissions of 16 GiB mixed 4 KiB-1 MiB chunks "
+                                  f"per step, device-resident, through md5hip_queue",
+                      "submissions": K, "chunks": int(sum(x.size for x in lk)),
+                      "payload_bytes": int(payload), "queue": stats},
+           "roofline": {"bound": "hbm", "achieved": round(payload / (wall_max / a.steps) / 1e9, 1),
+                        "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": round(payload / (wall_max / a.steps) / 1e9 / HBM_PEAK_GBS, 4),
+                        "traffic": None, "kernel": "md5hip::md5_desc_* (queue launches)",
+                        "note": "wall-clock per step (submit + wait), several launches per step"}}
+    return per_rank_line(res, rank, world, local, device, backend, payload * a.steps, wall, par)
+
+
+def run_c5(a, rank, world, local, device, backend):
     """End to end from pinned host memory: H2D -> MD5 -> D2H over pipelined
     batcher slots (md5hip_batch_host_fixed)."""
-    import numpy as np
     n, L = a.c5_chunks, a.len
     host = torch.empty(n * L, dtype=torch.uint8, pin_memory=True)
     host.view(torch.int64).random_(generator=torch.Generator().manual_seed(5))
@@ -386,62 +777,58 @@ def run_c5(a, rank, world):
             b.host_fixed(arr, n, L)
         t0 = time.perf_counter()
         for _ in range(a.steps):
-            b.host_fixed(arr, n, L)
+            dig = b.host_fixed(arr, n, L)
         wall = time.perf_counter() - t0
     gbs = n * L * a.steps / wall / 1e9
-    return {"metric": "end-to-end MD5 GiB/s from pinned host memory (C5)",
-            "value": round(n * L * a.steps / wall / GIB, 2), "unit": "GiB/s", "n_gpus": 1,
-            "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(wall / a.steps * 1e3, 3),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32",
-            "data": "synthetic (host random)", "config": {"workload": "C5", "chunks": n,
-                                                          "chunk_bytes": L, "slice_bytes": a.c5_slice,
-                                                          "slots": 3},
-            "roofline": {"bound": "pcie", "achieved": round(gbs, 2), "peak": round(h2d_gbs, 2),
-                         "unit": "GB/s", "frac": round(gbs / h2d_gbs, 4),
-                         "peak_note": (f"measured pinned H2D copy alone, best of 1 and {nsl} "
-                                       f"streams; spec {PCIE_PEAK_GBS} GB/s"),
-                         "traffic": None}}
+    import numpy as np
+    k = min(n, a.parity_sample)
+    par = check_sample(arr, np.arange(k) * L, np.full(k, L), dig[:k]) if k else None
+    res = {"metric": "end-to-end MD5 GiB/s from pinned host memory (C5)",
+           "value": round(n * L * a.steps / wall / GIB, 2), "unit": "GiB/s", "n_gpus": world,
+           "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(wall / a.steps * 1e3, 3),
+           "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32",
+           "data": "synthetic (host random)", "config": {"workload": "C5", "chunks": n,
+                                                         "chunk_bytes": L, "slice_bytes": a.c5_slice,
+                                                         "slots": 3},
+           "roofline": {"bound": "pcie", "achieved": round(gbs, 2), "peak": round(h2d_gbs, 2),
+                        "unit": "GB/s", "frac": round(gbs / h2d_gbs, 4),
+                        "peak_note": (f"measured pinned H2D copy alone, best of 1 and {nsl} "
+                                      f"streams; spec {PCIE_PEAK_GBS} GB/s"),
+                        "traffic": None}}
+    return per_rank_line(res, rank, world, local, device, backend, n * L * a.steps, wall, par)
 
 
-def main():
-    p = argparse.ArgumentParser()
-    p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=50)
-    p.add_argument("--warmup", type=int, default=20,
-                   help="untimed launches first: the board settles its clock over the first ~15 "
-                        "launches of a 3 ms kernel (slow start, profiles/r01_bench_kernel_trace_startup.json)")
-    p.add_argument("--config", default="c2", choices=["c2", "c3", "c5", "crc"])
-    p.add_argument("--chunks", type=int, default=1 << 20, help="chunks per GPU (C2, weak scaling)")
-    p.add_argument("--total-chunks", type=int, default=0,
-                   help="one global batch split across ranks (C4: 16777216 on 8 GPUs)")
-    p.add_argument("--len", type=int, default=16384)
-    p.add_argument("--variant", default="auto", choices=sorted(m.VARIANTS))
-    p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
-                   help="control-plane backend for N > 1 (barrier + scalar MAX only)")
-    p.add_argument("--traffic", default=os.path.join(REPO, "profiles", "traffic.json"))
-    p.add_argument("--c3-bytes", type=int, default=16 << 30)
-    p.add_argument("--c3-variant", default="plan", choices=["plan"] + sorted(m.DESC_VARIANTS),
-                   help="descriptor kernel for C3 (plan = md5hip_plan_desc's choice)")
-    p.add_argument("--c3-coalesce", type=int, default=3,
-                   help="C3 batches planned and launched together for the coalesced rate (0/1 = off)")
-    p.add_argument("--c3-streams", type=int, default=3,
-                   help="streams for C3's streamed rate (batches in flight)")
-    p.add_argument("--c5-chunks", type=int, default=1 << 18)
-    p.add_argument("--c5-slice", type=int, default=64 << 20)
-    a = p.parse_args()
-    rank, world, _ = dist_setup(a.gpus, a.dist_backend)
-    res = {"c2": run_c2, "c3": run_c3, "c5": run_c5, "crc": run_crc}[a.config](a, rank, world)
-    if rank == 0 and world == 1 and a.config == "c2" and not a.no_cpu_baseline:
-        res["cpu_baseline"] = cpu_baseline()
-        # labelled separately: the same reference md5.c on the box's CPU share
-        res["cpu_baseline_all_cores"] = cpu_baseline(reps=10, threads=CPU_SHARE)
-    if rank == 0 and world == 1 and a.config == "crc" and not a.no_cpu_baseline:
-        res["cpu_baseline"] = cpu_baseline_crc()
+def main(argv=None):
+    global torch, m
+    argv = sys.argv[1:] if argv is None else list(argv)
+    a = parse_args(argv)
+    if a.gpus < 1:
+        raise SystemExit("bench.py: --gpus must be >= 1")
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(a, argv))           # before anything touches the GPU
+    import torch as _torch
+    torch = _torch
+    sys.path.insert(0, REPO)
+    from sproxy_amd import md5 as _m
+    m = _m
+    rank, world, local, device, backend = dist_setup(a)
+    if a.dry_run:
+        res = run_dry(a, rank, world, local, device, backend)
+    else:
+        res = {"c2": run_c2, "c3": run_c3, "c3q": run_c3q, "c5": run_c5,
+               "crc": run_crc}[a.config](a, rank, world, local, device, backend)
+    if rank == 0 and world == 1 and not a.dry_run and not a.no_cpu_baseline:
+        if a.config == "c2":
+            res["cpu_baseline"] = cpu_baseline()
+            # labelled separately: the same reference md5.c on the box's CPU share
+            res["cpu_baseline_all_cores"] = cpu_baseline(reps=10, threads=CPU_SHARE)
+        elif a.config == "crc":
+            res["cpu_baseline"] = cpu_baseline_crc()
     if rank == 0:
         print(json.dumps(res), flush=True)
     if world > 1:
         import torch.distributed as dist
+        dist.barrier()
         dist.destroy_process_group()
 
 

@@ -30,27 +30,24 @@
 extern "C" {
 #endif
 
-#define MD5HIP_ABI_VERSION 1
+#define MD5HIP_ABI_VERSION 2
 
-/* Kernel variants for md5hip_digest_fixed_variant (tuning / A-B benches). */
+/* Fixed-length kernels for md5hip_digest_fixed_variant.  ABI 2: the round-1
+ * A/B variants (values 2-9) moved to the diagnostic library (md5_diag.hip);
+ * the library ships the default and one fallback, and no environment
+ * variable re-routes a launch. */
 enum md5hip_variant {
-    MD5HIP_AUTO = 0,        /* library's choice (measured best on MI355X) */
-    MD5HIP_DIRECT2 = 1,     /* lane-direct dwordx4 loads, 2-block register ring */
-    MD5HIP_DIRECT4 = 2,     /* lane-direct dwordx4 loads, 4-block register ring */
-    MD5HIP_LDS64 = 3,       /* wave LDS-DMA staging, 64 B per chunk per stage */
-    MD5HIP_LDS128 = 4,      /* wave LDS-DMA staging, 128 B per chunk per stage */
-    MD5HIP_XPOSE1 = 5,      /* coalesced buffer loads, LDS transpose, 1 stage ahead */
-    MD5HIP_XPOSE2 = 6,      /* same, 2 stages ahead */
-    MD5HIP_XPOSE1NT = 7,    /* xpose1 with non-temporal loads */
-    MD5HIP_XPOSE2NT = 8,    /* xpose2 with non-temporal loads */
-    MD5HIP_LDS128NT = 9,    /* lds128 with non-temporal loads */
-    MD5HIP_XDMA1NT = 10,    /* xpose image filled by LDS-DMA (no VGPR staging), non-temporal */
+    MD5HIP_AUTO = 0,        /* the default: XDMA1NT */
+    MD5HIP_DIRECT2 = 1,     /* lane-direct dwordx4 loads, 2-block register ring (used for
+                               strides >= 2^31/64, where XDMA1NT's 32-bit offsets end) */
+    MD5HIP_XDMA1NT = 10,    /* 8 chunks x 128 B per wave-instruction by LDS-DMA into a per-wave
+                               transpose image, non-temporal; DESIGN.md §4 */
     MD5HIP_NUM_VARIANTS = 11
 };
 
 int md5hip_abi_version(void);
 const char *md5hip_variant_name(int variant);
-/* The concrete variant MD5HIP_AUTO resolves to (env MD5HIP_VARIANT overrides). */
+/* The concrete variant MD5HIP_AUTO resolves to. */
 int md5hip_resolve_variant(int variant);
 
 /*
@@ -75,16 +72,16 @@ int md5hip_digest_fixed_variant(const void *d_base, uint64_t n, uint32_t len, ui
 int md5hip_digest_desc(const void *d_base, const uint64_t *d_offsets, const uint32_t *d_lens,
                        const uint32_t *d_order, uint64_t n, unsigned char *d_digests,
                        void *stream);
-/* Descriptor-batch kernels for md5hip_digest_desc_variant (A-B benches). */
+/* Descriptor-batch kernels for md5hip_digest_desc_variant. */
 enum md5hip_desc_variant {
-    MD5HIP_DESC_AUTO = 0,   /* library's choice (env MD5HIP_DESC_VARIANT overrides) */
+    MD5HIP_DESC_AUTO = 0,   /* the default: XDMA */
     MD5HIP_DESC_LANE = 1,   /* each lane streams its own chunk (8-block register ring) */
-    MD5HIP_DESC_XPOSE = 2,  /* whole-line loads of 8 chunks x 128 B + LDS transpose;
-                               waves with an unaligned chunk fall back to LANE */
-    MD5HIP_DESC_HYBRID = 3, /* XDMA, but the first waves (one per CU, env MD5HIP_DESC_NLONG)
-                               go lane-direct when they hold a chunk >= 256 KiB */
-    MD5HIP_DESC_XDMA = 4,   /* XPOSE with the image filled by LDS-DMA (no VGPR staging);
-                               the default */
+    /* 2: the register-staged XPOSE loader, moved to the diagnostic library */
+    MD5HIP_DESC_HYBRID = 3, /* XDMA, but the first waves (one per CU) go lane-direct when
+                               they hold a chunk >= 256 KiB (md5hip_plan_desc's choice for
+                               batches whose longest chunks bound the launch) */
+    MD5HIP_DESC_XDMA = 4,   /* whole-line loads of 8 chunks x 128 B by LDS-DMA into a
+                               transpose image; waves holding an unaligned chunk go LANE */
     MD5HIP_DESC_NUM_VARIANTS = 5
 };
 int md5hip_digest_desc_variant(const void *d_base, const uint64_t *d_offsets,
@@ -103,15 +100,12 @@ int md5hip_digest_desc_variant(const void *d_base, const uint64_t *d_offsets,
  */
 int crc32hip_fixed(const void *d_base, uint64_t n, uint32_t len, uint64_t stride,
                    uint32_t fastcrc, uint32_t *d_crcs, void *stream);
-/* CRC-32 kernel variants for crc32hip_fixed_variant (A-B benches). */
+/* CRC-32 kernels for crc32hip_fixed_variant (ABI 2: values 1-5, the round-1
+ * A/B variants, moved to the diagnostic library). */
 enum crc32hip_variant {
-    CRC32HIP_AUTO = 0,      /* library's choice (env CRC32HIP_VARIANT overrides) */
-    CRC32HIP_SHARED8 = 1,   /* slicing-by-8, one shared 8 KiB LDS table set, xpose loads */
-    CRC32HIP_LANE32 = 2,    /* slicing-by-4, 32 lane-private table copies (128 KiB LDS) */
-    CRC32HIP_LANE16 = 3,    /* slicing-by-4, 16 table copies (64 KiB LDS) */
-    CRC32HIP_XLANE16 = 4,   /* slicing-by-4, 16 table copies + whole-line xpose loads */
-    CRC32HIP_XPERM16 = 5,   /* as XLANE16, copies laid out for one-v_perm addressing */
-    CRC32HIP_XDMA16 = 6,    /* XPERM16 tables, full images filled by LDS-DMA, 12 waves/CU */
+    CRC32HIP_AUTO = 0,      /* the default: XDMA16 */
+    CRC32HIP_XDMA16 = 6,    /* slicing-by-4 over 16 v_perm-addressed LDS table copies, 8 KiB
+                               images filled by LDS-DMA, 12 waves/CU */
     CRC32HIP_NUM_VARIANTS = 7
 };
 int crc32hip_fixed_variant(const void *d_base, uint64_t n, uint32_t len, uint64_t stride,

@@ -1,0 +1,70 @@
+#!/usr/bin/env python3
+"""Merge rocprofv3 PMC passes into profiles/traffic.json, keyed by the SHA-256
+of libmd5hip.so's device code object (sproxy_amd._lib.code_object_hash), so
+bench.py reports counter bytes only for the kernel code that was measured.
+
+usage: traffic_json.py FETCH_DIR WRITE_DIR WORKLOAD [--out profiles/traffic.json]
+  FETCH_DIR / WRITE_DIR: `rocprofv3 --pmc FETCH_SIZE` / `--pmc WRITE_SIZE`
+  output dirs (csv) of the same bench command; WORKLOAD: the bench line's
+  config tag the bytes belong to (e.g. c2@1048576x16384).
+HBM bytes per launch (MI355X_MICROARCH.md HBM section, gfx950): read =
+2 x 1024 x FETCH_SIZE, write = 1024 x WRITE_SIZE, mean over the kernel's
+dispatches."""
+import argparse
+import csv
+import glob
+import json
+import os
+import sys
+from collections import defaultdict
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+
+
+def short(name):
+    return name.split("(")[0].replace("void ", "").replace("md5hip::", "").strip()
+
+
+def per_kernel(d, counter):
+    vals = defaultdict(list)
+    for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+        per = defaultdict(float)
+        for r in csv.DictReader(open(f)):
+            if r["Counter_Name"] == counter:
+                per[(short(r["Kernel_Name"]), r["Dispatch_Id"])] += float(r["Counter_Value"])
+        for (k, _), v in per.items():
+            vals[k].append(v)
+    return {k: sum(v) / len(v) for k, v in vals.items()}, {k: len(v) for k, v in vals.items()}
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("fetch")
+    p.add_argument("write")
+    p.add_argument("workload")
+    p.add_argument("--out", default=os.path.join(REPO, "profiles", "traffic.json"))
+    p.add_argument("--source", default="")
+    a = p.parse_args()
+    from sproxy_amd._lib import code_object_hash
+    h = code_object_hash()
+    fs, nf = per_kernel(a.fetch, "FETCH_SIZE")
+    ws, _ = per_kernel(a.write, "WRITE_SIZE")
+    d = json.load(open(a.out)) if os.path.exists(a.out) else {}
+    d.setdefault("_note", "HBM bytes per launch from rocprofv3 PMC (read = 2*1024*FETCH_SIZE, "
+                          "write = 1024*WRITE_SIZE; MI355X_MICROARCH.md HBM section), keyed by the "
+                          "SHA-256 of libmd5hip.so's .hip_fatbin and the bench workload")
+    ent = d.setdefault("by_code_object", {}).setdefault(h, {"kernels": {}})
+    for k, v in fs.items():
+        if not k.startswith(("md5_", "crc32_")):
+            continue
+        ent["kernels"][f"{k}@{a.workload}"] = {
+            "bytes": int(2 * 1024 * v + 1024 * ws.get(k, 0.0)),
+            "read_bytes": int(2 * 1024 * v), "write_bytes": int(1024 * ws.get(k, 0.0)),
+            "dispatches": nf[k], "source": a.source}
+    json.dump(d, open(a.out, "w"), indent=1, sort_keys=True)
+    print(json.dumps(ent, indent=1))
+
+
+if __name__ == "__main__":
+    main()

@@ -141,3 +141,24 @@ EXPORTS = ["MD5Init", "MD5Update", "MD5Final", "nc_MD5Init", "nc_MD5Update", "nc
 def check(fn, rc):
     if rc != 0:
         raise MD5HipError(fn, rc)
+
+
+def code_object_hash(path: str = LIB_PATH) -> str:
+    """SHA-256 of the library's device code (its .hip_fatbin ELF section):
+    counter evidence (profiles/traffic.json) is keyed by it, so numbers taken
+    from other kernel code never read as current."""
+    import hashlib
+    import struct
+    with open(path, "rb") as f:
+        elf = f.read()
+    if elf[:4] != b"\x7fELF" or elf[4] != 2:
+        raise ValueError(f"{path}: not an ELF64 object")
+    shoff, = struct.unpack_from("<Q", elf, 0x28)
+    shentsize, shnum, shstrndx = struct.unpack_from("<HHH", elf, 0x3A)
+    secs = [struct.unpack_from("<IIQQQQIIQQ", elf, shoff + k * shentsize) for k in range(shnum)]
+    stroff = secs[shstrndx][4]
+    for name, _, _, _, off, size, *_ in secs:
+        end = elf.index(b"\0", stroff + name)
+        if elf[stroff + name:end] == b".hip_fatbin":
+            return hashlib.sha256(elf[off:off + size]).hexdigest()
+    raise ValueError(f"{path}: no .hip_fatbin section")

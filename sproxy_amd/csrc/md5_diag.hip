@@ -34,6 +34,7 @@
 #include <errno.h>
 
 #include "md5_kernels.h"
+#include "md5_kernels_ab.h"
 
 namespace md5hip {
 
@@ -871,5 +872,121 @@ extern "C" int md5diag_desc_xpose_lds(const void* base, const uint64_t* offs, co
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)extra);
   hipLaunchKernelGGL(md5_desc_xpose, dim3((uint32_t)((n + 63) / 64)), dim3(64), extra,
                      (hipStream_t)stream, (const uint8_t*)base, offs, lens, order, n, (uint4*)out);
+  return hipGetLastError() == hipSuccess ? 0 : -EIO;
+}
+
+// ---------------------------------------------------------------------------
+// The round-1 A/B variants that left libmd5hip.so (md5_kernels_ab.h), by their
+// former enum values (md5hip.h ABI 1), for A/B benches and parity tests:
+//   fixed  2 direct4, 3 lds64, 4 lds128, 5 xpose1, 6 xpose2, 7 xpose1nt,
+//          8 xpose2nt, 9 lds128nt  (1 direct2 and 10 xdma1nt: also the product's)
+//   desc   2 xpose
+//   crc    1 shared8, 2 lane32, 3 lane16, 4 xlane16, 5 xperm16; descriptor
+//          batches: 5 = crc32_desc_xperm16
+// ---------------------------------------------------------------------------
+namespace {
+int diag_cus() {
+  int dev = 0, cus = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+    return 256;
+  return cus;
+}
+template <int BB, bool NT>
+int diag_launch_lds(const uint8_t* base, uint64_t n, uint32_t len, uint64_t stride, uint4* out,
+                    hipStream_t s) {
+  const size_t lds = (size_t)4 * 2 * 64 * BB;
+  auto fn = BB == 64 ? md5_fixed_lds64 : NT ? md5_fixed_lds128nt : md5_fixed_lds128;
+  if (hipFuncSetAttribute(reinterpret_cast<const void*>(fn),
+                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+    return -ENODEV;
+  hipLaunchKernelGGL(fn, dim3((uint32_t)((n + 255) / 256)), dim3(256), lds, s, base, n, len, stride, out);
+  return hipGetLastError() == hipSuccess ? 0 : -EIO;
+}
+}  // namespace
+
+namespace md5hip {
+template __global__ void md5_fixed_direct<4, Md5Hasher<false>>(const uint8_t*, uint64_t, uint32_t, uint64_t, uint4*);
+}
+
+extern "C" int md5diag_variant_fixed(int v, const void* d_base, uint64_t n, uint32_t len,
+                                     uint64_t stride, void* d_out, void* stream) {
+  if (n == 0) return 0;
+  if (!d_base || !d_out || len > stride || ((uintptr_t)d_base & 15u) || (stride & 15u)) return -EINVAL;
+  if (stride >= (1ull << 31) / 64) return -EINVAL;
+  hipStream_t s = (hipStream_t)stream;
+  const uint8_t* b = (const uint8_t*)d_base;
+  uint4* o = (uint4*)d_out;
+  const dim3 grid((uint32_t)((n + 255) / 256)), blk(256);
+  typedef void (*K)(const uint8_t*, uint64_t, uint32_t, uint64_t, uint4*);
+  K k = nullptr;
+  switch (v) {
+    case 1: k = md5_fixed_direct<2, Md5Hasher<false>>; break;
+    case 2: k = md5_fixed_direct<4, Md5Hasher<false>>; break;
+    case 3: return diag_launch_lds<64, false>(b, n, len, stride, o, s);
+    case 4: return diag_launch_lds<128, false>(b, n, len, stride, o, s);
+    case 9: return diag_launch_lds<128, true>(b, n, len, stride, o, s);
+    case 5: k = md5_fixed_xpose1; break;
+    case 6: k = md5_fixed_xpose2; break;
+    case 7: k = md5_fixed_xpose1nt; break;
+    case 8: k = md5_fixed_xpose2nt; break;
+    case 10: k = md5_fixed_xdma1nt; break;
+    default: return -EINVAL;
+  }
+  hipLaunchKernelGGL(k, grid, blk, 0, s, b, n, len, stride, o);
+  return hipGetLastError() == hipSuccess ? 0 : -EIO;
+}
+
+extern "C" int md5diag_variant_desc(int v, const void* d_base, const uint64_t* offs,
+                                    const uint32_t* lens, const uint32_t* order, uint64_t n,
+                                    void* d_out, void* stream) {
+  if (n == 0) return 0;
+  if (v != 2) return -EINVAL;
+  hipLaunchKernelGGL(md5_desc_xpose, dim3((uint32_t)((n + 63) / 64)), dim3(64), 0, (hipStream_t)stream,
+                     (const uint8_t*)d_base, offs, lens, order, n, (uint4*)d_out);
+  return hipGetLastError() == hipSuccess ? 0 : -EIO;
+}
+
+extern "C" int md5diag_variant_crc(int v, const void* d_base, uint64_t n, uint32_t len,
+                                   uint64_t stride, uint32_t* d_out, void* stream) {
+  if (n == 0) return 0;
+  if (!d_base || !d_out || len > stride || ((uintptr_t)d_base & 15u) || (stride & 15u)) return -EINVAL;
+  if (stride >= (1ull << 31) / 64) return -EINVAL;
+  hipStream_t s = (hipStream_t)stream;
+  const uint8_t* b = (const uint8_t*)d_base;
+  const uint64_t groups = (n + 63) / 64;
+  const uint32_t percu = (uint32_t)(groups < (uint64_t)diag_cus() ? groups : (uint64_t)diag_cus());
+  switch (v) {
+    case 1:
+      hipLaunchKernelGGL(crc32_fixed_xpose, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s, b, n,
+                         len, stride, d_out);
+      break;
+    case 2: case 3: {
+      const uint64_t need = (n + 1023) / 1024, cap = (uint64_t)diag_cus() * (v == 2 ? 1 : 2);
+      hipLaunchKernelGGL(v == 2 ? crc32_fixed_lane32 : crc32_fixed_lane16,
+                         dim3((uint32_t)(need < cap ? need : cap)), dim3(1024), 0, s, b, n, len, stride, d_out);
+      break;
+    }
+    case 4:
+      hipLaunchKernelGGL(crc32_fixed_xlane16, dim3(percu), dim3(1024), 0, s, b, n, len, stride, d_out);
+      break;
+    case 5:
+      hipLaunchKernelGGL(crc32_fixed_xperm16, dim3(percu), dim3(1024), 0, s, b, n, len, stride, d_out);
+      break;
+    default:
+      return -EINVAL;
+  }
+  return hipGetLastError() == hipSuccess ? 0 : -EIO;
+}
+
+extern "C" int md5diag_variant_crc_desc(int v, const void* d_base, const uint64_t* offs,
+                                        const uint32_t* lens, const uint32_t* order, uint64_t n,
+                                        uint32_t* d_out, void* stream) {
+  if (n == 0) return 0;
+  if (v != 5) return -EINVAL;
+  const uint64_t groups = (n + 63) / 64;
+  const uint32_t percu = (uint32_t)(groups < (uint64_t)diag_cus() ? groups : (uint64_t)diag_cus());
+  hipLaunchKernelGGL(crc32_desc_xperm16, dim3(percu), dim3(1024), 0, (hipStream_t)stream,
+                     (const uint8_t*)d_base, offs, lens, order, n, d_out);
   return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }

@@ -6,14 +6,10 @@ namespace md5hip {
 // Explicit instantiations: kernels referenced only from host templates are
 // otherwise not emitted by hipcc (host stub and device code both missing).
 template __global__ void md5_fixed_direct<2, Md5Hasher<false>>(const uint8_t*, uint64_t, uint32_t, uint64_t, uint4*);
-template __global__ void md5_fixed_direct<4, Md5Hasher<false>>(const uint8_t*, uint64_t, uint32_t, uint64_t, uint4*);
 template __global__ void md5_desc<false>(const uint8_t*, const uint64_t*, const uint32_t*,
                                          const uint32_t*, uint64_t, uint64_t, uint32_t, uint4*);
 template __global__ void md5_desc<true>(const uint8_t*, const uint64_t*, const uint32_t*,
                                         const uint32_t*, uint64_t, uint64_t, uint32_t, uint4*);
-template __global__ void crc32_desc<false>(const uint8_t*, const uint64_t*, const uint32_t*,
-                                           const uint32_t*, uint64_t, uint64_t, uint32_t,
-                                           uint32_t*);
 template __global__ void crc32_desc<true>(const uint8_t*, const uint64_t*, const uint32_t*,
                                           const uint32_t*, uint64_t, uint64_t, uint32_t,
                                           uint32_t*);
@@ -53,22 +49,8 @@ int launched() {
   return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }
 
-// Environment knob read once; C++ magic statics make the first call
-// thread-safe (the pool calls the launchers from one host thread per GPU).
-int env_int(const char* name, int lo, int hi, int dflt) {
-  const char* e = getenv(name);
-  const int x = e ? atoi(e) : 0;
-  return (x >= lo && x < hi) ? x : dflt;
-}
-
-int default_variant() {
-  static const int v = env_int("MD5HIP_VARIANT", 1, MD5HIP_NUM_VARIANTS,
-                               MD5HIP_XDMA1NT);   // measured best, DESIGN.md §4
-  return v;
-}
-
 // Compute units of the current device (grid sizing of one-workgroup-per-CU
-// kernels).
+// kernels and HYBRID's long-wave count).
 int cu_count() {
   int dev = 0, cus = 0;
   if (hipGetDevice(&dev) != hipSuccess ||
@@ -78,40 +60,11 @@ int cu_count() {
   return cus;
 }
 
-int default_crc_variant() {
-  static const int v = env_int("CRC32HIP_VARIANT", 1, CRC32HIP_NUM_VARIANTS,
-                               CRC32HIP_XDMA16);   // measured best, DESIGN.md §5
-  return v;
-}
-
-// Lane-private-table kernels: kLaneBlock threads, `per_cu` workgroups per CU
-// resident (LDS-limited), grid-stride over the batch.
-constexpr int kLaneBlock = 1024;
-
-template <int K>
-int launch_crc_lane(const uint8_t* base, uint64_t n, uint32_t len, uint64_t stride, uint32_t* out,
-                    hipStream_t s) {
-  const int per_cu = K == 32 ? 1 : 2;
-  const uint64_t need = (n + kLaneBlock - 1) / kLaneBlock;
-  const uint64_t cap = (uint64_t)cu_count() * per_cu;
-  const uint64_t grid = need < cap ? need : cap;
-  hipLaunchKernelGGL(K == 32 ? crc32_fixed_lane32 : crc32_fixed_lane16, dim3((uint32_t)grid),
-                     dim3(kLaneBlock), 0, s, base, n, len, stride, out);
-  return launched();
-}
-
-template <int BB, bool NT = false>
-int launch_lds(const uint8_t* base, uint64_t n, uint32_t len, uint64_t stride, uint4* out,
-               hipStream_t s) {
-  const size_t lds = (size_t)(kBlock / 64) * 2 * 64 * BB;
-  auto fn = BB == 64 ? md5_fixed_lds64 : NT ? md5_fixed_lds128nt : md5_fixed_lds128;
-  static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(fn),
-                                               hipFuncAttributeMaxDynamicSharedMemorySize,
-                                               (int)lds) == hipSuccess;
-  if (!attr) return -ENODEV;
-  const uint64_t grid = (n + kBlock - 1) / kBlock;
-  hipLaunchKernelGGL(fn, dim3((uint32_t)grid), dim3(kBlock), lds, s, base, n, len, stride, out);
-  return launched();
+// One workgroup of `threads` per CU, grid-stride over 64-chunk groups.
+uint32_t per_cu_grid(uint64_t n) {
+  const uint64_t need = (n + 63) / 64;
+  const uint64_t cap = (uint64_t)cu_count();
+  return (uint32_t)(need < cap ? need : cap);
 }
 
 }  // namespace
@@ -120,39 +73,19 @@ extern "C" {
 
 int md5hip_abi_version(void) { return MD5HIP_ABI_VERSION; }
 
-int md5hip_resolve_variant(int v) { return v == MD5HIP_AUTO ? default_variant() : v; }
-int crc32hip_resolve_variant(int v) { return v == CRC32HIP_AUTO ? default_crc_variant() : v; }
+// The shipped kernels are fixed: the round-1 A/B variants live in the
+// diagnostic library (md5_diag.hip, md5_kernels_ab.h), and no environment
+// variable re-routes a product launch.
+int md5hip_resolve_variant(int v) { return v == MD5HIP_AUTO ? MD5HIP_XDMA1NT : v; }
+int crc32hip_resolve_variant(int v) { return v == CRC32HIP_AUTO ? CRC32HIP_XDMA16 : v; }
 
 const char* md5hip_variant_name(int v) {
   switch (v) {
     case MD5HIP_AUTO: return "auto";
     case MD5HIP_DIRECT2: return "direct2";
-    case MD5HIP_DIRECT4: return "direct4";
-    case MD5HIP_LDS64: return "lds64";
-    case MD5HIP_LDS128: return "lds128";
-    case MD5HIP_XPOSE1: return "xpose1";
-    case MD5HIP_XPOSE2: return "xpose2";
-    case MD5HIP_XPOSE1NT: return "xpose1nt";
     case MD5HIP_XDMA1NT: return "xdma1nt";
-    case MD5HIP_XPOSE2NT: return "xpose2nt";
-    case MD5HIP_LDS128NT: return "lds128nt";
     default: return "?";
   }
-}
-
-int default_desc_variant() {
-  static const int v = env_int("MD5HIP_DESC_VARIANT", 1, MD5HIP_DESC_NUM_VARIANTS,
-                               MD5HIP_DESC_XDMA);    // DESIGN.md §5 (profiles/r01_desc_xdma_ab.json)
-  return v;
-}
-
-// Waves (in longest-first order) that may take the lane-direct path in the
-// HYBRID descriptor kernel: one per CU (env MD5HIP_DESC_NLONG overrides, A/B).
-uint32_t desc_nlong() {
-  const char* e = getenv("MD5HIP_DESC_NLONG");
-  if (!e) return (uint32_t)cu_count();      // per call: the pool drives several devices
-  const unsigned long long v = strtoull(e, nullptr, 10);
-  return v > 0xffffffffull ? 0xffffffffu : (uint32_t)v;
 }
 
 int md5hip_digest_desc(const void* d_base, const uint64_t* d_offsets, const uint32_t* d_lens,
@@ -168,33 +101,32 @@ int md5hip_digest_desc_variant(const void* d_base, const uint64_t* d_offsets,
   if (n == 0) return 0;
   if (!d_base || !d_offsets || !d_lens || !d_digests) return -EINVAL;
   if (((uintptr_t)d_digests & 15u) != 0) return -EINVAL;
-  if (variant < 0 || variant >= MD5HIP_DESC_NUM_VARIANTS) return -EINVAL;
+  if (variant != MD5HIP_DESC_AUTO && variant != MD5HIP_DESC_LANE && variant != MD5HIP_DESC_HYBRID &&
+      variant != MD5HIP_DESC_XDMA)
+    return -EINVAL;
   if (int e = device_ok()) return e;
-  if (variant == MD5HIP_DESC_AUTO) variant = default_desc_variant();
+  const uint64_t g = (n + 63) / 64;
+  if (g > 0x7fffffffull) return -EINVAL;
+  hipStream_t s = (hipStream_t)stream;
+  const uint8_t* base = (const uint8_t*)d_base;
   if (variant == MD5HIP_DESC_HYBRID) {
-    const uint64_t g = (n + 63) / 64;
-    if (g > 0x7fffffffull) return -EINVAL;
-    hipLaunchKernelGGL(md5_desc_hybrid, dim3((uint32_t)g), dim3(64), 0, (hipStream_t)stream,
-                       (const uint8_t*)d_base, d_offsets, d_lens, d_order, n, (uint4*)d_digests,
-                       desc_nlong());
+    // the first waves (one per CU: the longest chunks in longest-first order)
+    // run their chains lane-direct (md5hip_plan_desc picks HYBRID)
+    hipLaunchKernelGGL(md5_desc_hybrid, dim3((uint32_t)g), dim3(64), 0, s, base, d_offsets, d_lens,
+                       d_order, n, (uint4*)d_digests, (uint32_t)cu_count());
     return launched();
   }
-  if (variant == MD5HIP_DESC_XPOSE || variant == MD5HIP_DESC_XDMA) {
-    const uint64_t g = (n + 63) / 64;
-    if (g > 0x7fffffffull) return -EINVAL;
-    hipLaunchKernelGGL(variant == MD5HIP_DESC_XDMA ? md5_desc_xdma : md5_desc_xpose, dim3((uint32_t)g), dim3(64), 0, (hipStream_t)stream,
-                       (const uint8_t*)d_base, d_offsets, d_lens, d_order, n, (uint4*)d_digests);
+  if (variant == MD5HIP_DESC_AUTO || variant == MD5HIP_DESC_XDMA) {
+    hipLaunchKernelGGL(md5_desc_xdma, dim3((uint32_t)g), dim3(64), 0, s, base, d_offsets, d_lens,
+                       d_order, n, (uint4*)d_digests);
     return launched();
   }
-  // One wave per workgroup: a mixed batch has few waves, and the dispatcher
-  // then spreads them one per CU instead of packing 4 onto one CU where the
-  // long chunks' lane-direct loads contend for the CU's address unit
+  // LANE.  One wave per workgroup: a mixed batch has few waves, and the
+  // dispatcher then spreads them one per CU instead of packing 4 onto one CU
+  // where the long chunks' lane-direct loads contend for the CU's address unit
   // (scripts/c3_trace.py: 28.7 -> 13.2 ms on the C3 batch).
-  const uint64_t grid = (n + kDescBlock - 1) / kDescBlock;
-  if (grid > 0x7fffffffull) return -EINVAL;
-  hipLaunchKernelGGL(md5_desc<false>, dim3((uint32_t)grid), dim3(kDescBlock), 0, (hipStream_t)stream,
-                     (const uint8_t*)d_base, d_offsets, d_lens, d_order, n, (uint64_t)0, 0u,
-                     (uint4*)d_digests);
+  hipLaunchKernelGGL(md5_desc<false>, dim3((uint32_t)g), dim3(kDescBlock), 0, s, base, d_offsets,
+                     d_lens, d_order, n, (uint64_t)0, 0u, (uint4*)d_digests);
   return launched();
 }
 
@@ -203,7 +135,8 @@ int md5hip_digest_fixed_variant(const void* d_base, uint64_t n, uint32_t len, ui
   if (n == 0) return 0;
   if (!d_base || !d_digests || len > stride) return -EINVAL;
   if (((uintptr_t)d_digests & 15u) != 0) return -EINVAL;
-  if (variant < 0 || variant >= MD5HIP_NUM_VARIANTS) return -EINVAL;
+  if (variant != MD5HIP_AUTO && variant != MD5HIP_DIRECT2 && variant != MD5HIP_XDMA1NT)
+    return -EINVAL;
   if (int e = device_ok()) return e;
   const uint64_t grid = (n + kBlock - 1) / kBlock;
   if (grid > 0x7fffffffull) return -EINVAL;
@@ -218,38 +151,15 @@ int md5hip_digest_fixed_variant(const void* d_base, uint64_t n, uint32_t len, ui
                        (const uint32_t*)nullptr, n, stride, len, out);
     return launched();
   }
-  if (variant == MD5HIP_AUTO) variant = default_variant();
-  switch (variant) {
-    case MD5HIP_DIRECT2:
-      hipLaunchKernelGGL((md5_fixed_direct<2, Md5Hasher<false>>), dim3((uint32_t)grid), dim3(kBlock), 0, s, base, n,
-                         len, stride, out);
-      return launched();
-    case MD5HIP_DIRECT4:
-      hipLaunchKernelGGL((md5_fixed_direct<4, Md5Hasher<false>>), dim3((uint32_t)grid), dim3(kBlock), 0, s, base, n,
-                         len, stride, out);
-      return launched();
-    case MD5HIP_LDS64:
-      return launch_lds<64>(base, n, len, stride, out, s);
-    case MD5HIP_LDS128:
-      return launch_lds<128>(base, n, len, stride, out, s);
-    case MD5HIP_LDS128NT:
-      return launch_lds<128, true>(base, n, len, stride, out, s);
-    case MD5HIP_XPOSE1:
-    case MD5HIP_XPOSE2:
-    case MD5HIP_XPOSE1NT:
-    case MD5HIP_XDMA1NT:
-    case MD5HIP_XPOSE2NT: {
-      typedef void (*K)(const uint8_t*, uint64_t, uint32_t, uint64_t, uint4*);
-      K k = variant == MD5HIP_XPOSE1 ? md5_fixed_xpose1
-          : variant == MD5HIP_XPOSE2 ? md5_fixed_xpose2
-          : variant == MD5HIP_XPOSE1NT ? md5_fixed_xpose1nt
-          : variant == MD5HIP_XDMA1NT ? md5_fixed_xdma1nt : md5_fixed_xpose2nt;
-      if (stride >= (1ull << 31) / 64) k = md5_fixed_direct<2, Md5Hasher<false>>;  // 32-bit buffer offsets
-      hipLaunchKernelGGL(k, dim3((uint32_t)grid), dim3(kBlock), 0, s, base, n, len, stride, out);
-      return launched();
-    }
+  // xdma1nt addresses a 64-chunk group with 32-bit buffer offsets
+  if (variant == MD5HIP_DIRECT2 || stride >= (1ull << 31) / 64) {
+    hipLaunchKernelGGL((md5_fixed_direct<2, Md5Hasher<false>>), dim3((uint32_t)grid), dim3(kBlock),
+                       0, s, base, n, len, stride, out);
+    return launched();
   }
-  return -EINVAL;
+  hipLaunchKernelGGL(md5_fixed_xdma1nt, dim3((uint32_t)grid), dim3(kBlock), 0, s, base, n, len,
+                     stride, out);
+  return launched();
 }
 
 int md5hip_digest_fixed(const void* d_base, uint64_t n, uint32_t len, uint64_t stride,
@@ -262,50 +172,25 @@ int crc32hip_fixed_variant(const void* d_base, uint64_t n, uint32_t len, uint64_
   if (n == 0) return 0;
   if (!d_base || !d_crcs || len > stride || (fastcrc & 3u)) return -EINVAL;
   if (((uintptr_t)d_crcs & 3u) != 0) return -EINVAL;
-  if (variant < 0 || variant >= CRC32HIP_NUM_VARIANTS) return -EINVAL;
+  if (variant != CRC32HIP_AUTO && variant != CRC32HIP_XDMA16) return -EINVAL;
   if (int e = device_ok()) return e;
-  if (variant == CRC32HIP_AUTO) variant = default_crc_variant();
   hipStream_t s = (hipStream_t)stream;
   const uint8_t* base = (const uint8_t*)d_base;
+  const uint64_t g = (n + kDescBlock - 1) / kDescBlock;
+  if (g > 0x7fffffffull) return -EINVAL;
   if (fastcrc && len > fastcrc) {
-    const uint64_t g = (n + kDescBlock - 1) / kDescBlock;
-    if (g > 0x7fffffffull) return -EINVAL;
     hipLaunchKernelGGL(crc32_fast<true>, dim3((uint32_t)g), dim3(kDescBlock), 0, s, base,
                        (const uint64_t*)nullptr, (const uint32_t*)nullptr, n, stride, len,
                        fastcrc, d_crcs);
     return launched();
   }
   const bool aligned = ((uintptr_t)base & 15u) == 0 && (stride & 15u) == 0;
-  if (aligned && variant == CRC32HIP_LANE32) return launch_crc_lane<32>(base, n, len, stride, d_crcs, s);
-  if (aligned && variant == CRC32HIP_LANE16) return launch_crc_lane<16>(base, n, len, stride, d_crcs, s);
-  if (aligned && stride < (1ull << 31) / 64 &&
-      (variant == CRC32HIP_XLANE16 || variant == CRC32HIP_XPERM16)) {
-    // one 1024-thread workgroup per CU (128 KiB LDS), grid-stride over 64-chunk
-    // groups, wave-major (every CU gets work once there is a group per CU)
-    const uint64_t need = (n + 63) / 64;
-    const uint64_t cap = (uint64_t)cu_count();
-    hipLaunchKernelGGL(variant == CRC32HIP_XLANE16 ? crc32_fixed_xlane16 : crc32_fixed_xperm16,
-                       dim3((uint32_t)(need < cap ? need : cap)), dim3(kLaneBlock), 0, s, base,
-                       n, len, stride, d_crcs);
-    return launched();
-  }
-  if (aligned && stride < (1ull << 31) / 64 && variant == CRC32HIP_XDMA16) {
-    // one 768-thread workgroup per CU (160 KiB LDS), grid-stride, wave-major
-    const uint64_t need = (n + 63) / 64;
-    const uint64_t cap = (uint64_t)cu_count();
-    hipLaunchKernelGGL(crc32_fixed_xdma16, dim3((uint32_t)(need < cap ? need : cap)), dim3(768), 0,
-                       s, base, n, len, stride, d_crcs);
-    return launched();
-  }
   if (aligned && stride < (1ull << 31) / 64) {
-    const uint64_t g = (n + kBlock - 1) / kBlock;
-    if (g > 0x7fffffffull) return -EINVAL;
-    hipLaunchKernelGGL(crc32_fixed_xpose, dim3((uint32_t)g), dim3(kBlock), 0, s, base, n, len,
+    // one 768-thread workgroup per CU (160 KiB LDS), grid-stride, wave-major
+    hipLaunchKernelGGL(crc32_fixed_xdma16, dim3(per_cu_grid(n)), dim3(768), 0, s, base, n, len,
                        stride, d_crcs);
     return launched();
   }
-  const uint64_t g = (n + kDescBlock - 1) / kDescBlock;
-  if (g > 0x7fffffffull) return -EINVAL;
   hipLaunchKernelGGL(crc32_desc<true>, dim3((uint32_t)g), dim3(kDescBlock), 0, s, base,
                      (const uint64_t*)nullptr, (const uint32_t*)nullptr,
                      (const uint32_t*)nullptr, n, stride, len, d_crcs);
@@ -331,24 +216,11 @@ int crc32hip_desc(const void* d_base, const uint64_t* d_offsets, const uint32_t*
     hipLaunchKernelGGL(crc32_fast<false>, dim3((uint32_t)g), dim3(kDescBlock), 0, s,
                        (const uint8_t*)d_base, d_offsets, d_lens, n, (uint64_t)0, 0u, fastcrc,
                        d_crcs);
-  } else if (default_crc_variant() == CRC32HIP_XDMA16) {
-    // XDMA16: one 768-thread workgroup per CU, LDS-DMA images
-    const uint64_t need = (n + 63) / 64;
-    const uint64_t cap = (uint64_t)cu_count();
-    hipLaunchKernelGGL(crc32_desc_xdma16, dim3((uint32_t)(need < cap ? need : cap)), dim3(768), 0,
-                       s, (const uint8_t*)d_base, d_offsets, d_lens, d_order, n, d_crcs);
-  } else if (default_crc_variant() == CRC32HIP_XPERM16) {
-    // XPERM16 tables + descriptor xpose loads: one 1024-thread workgroup per CU
-    const uint64_t need = (n + 63) / 64;
-    const uint64_t cap = (uint64_t)cu_count();
-    hipLaunchKernelGGL(crc32_desc_xperm16, dim3((uint32_t)(need < cap ? need : cap)),
-                       dim3(kLaneBlock), 0, s, (const uint8_t*)d_base, d_offsets, d_lens, d_order,
-                       n, d_crcs);
-  } else {
-    hipLaunchKernelGGL(crc32_desc<false>, dim3((uint32_t)g), dim3(kDescBlock), 0, s,
-                       (const uint8_t*)d_base, d_offsets, d_lens, d_order, n, (uint64_t)0, 0u,
-                       d_crcs);
+    return launched();
   }
+  // XDMA16: one 768-thread workgroup per CU, LDS-DMA images
+  hipLaunchKernelGGL(crc32_desc_xdma16, dim3(per_cu_grid(n)), dim3(768), 0, s,
+                     (const uint8_t*)d_base, d_offsets, d_lens, d_order, n, d_crcs);
   return launched();
 }
 
@@ -357,9 +229,7 @@ int md5hip_gather_launch(const struct md5hip_seg* d_segs, uint64_t nseg, unsigne
   static_assert(sizeof(md5hip_seg) == sizeof(GatherSeg), "segment layout");
   if (nseg == 0) return 0;
   const uint64_t g = nseg < 65536 ? nseg : 65536;
-  static const int unroll = env_int("MD5HIP_GATHER_UNROLL", 1, 5, 4);   // A/B knob
-  auto fn = unroll == 1 ? gather_segments<1> : unroll == 2 ? gather_segments<2> : gather_segments<4>;
-  hipLaunchKernelGGL(fn, dim3((uint32_t)g), dim3(256), 0, (hipStream_t)stream,
+  hipLaunchKernelGGL(gather_segments<4>, dim3((uint32_t)g), dim3(256), 0, (hipStream_t)stream,
                      reinterpret_cast<const GatherSeg*>(d_segs), nseg, d_dst);
   return launched();
 }

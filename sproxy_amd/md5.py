@@ -28,10 +28,8 @@ except Exception:  # pragma: no cover
 
 MD5_DIGEST_SIZE = 16
 
-AUTO, DIRECT2, DIRECT4, LDS64, LDS128, XPOSE1, XPOSE2, XPOSE1NT, XPOSE2NT, LDS128NT, XDMA1NT = range(11)
-VARIANTS = {"auto": AUTO, "direct2": DIRECT2, "direct4": DIRECT4, "lds64": LDS64, "lds128": LDS128,
-            "xpose1": XPOSE1, "xpose2": XPOSE2, "xpose1nt": XPOSE1NT, "xpose2nt": XPOSE2NT,
-            "lds128nt": LDS128NT, "xdma1nt": XDMA1NT}
+AUTO, DIRECT2, XDMA1NT = 0, 1, 10            # enum md5hip_variant (ABI 2: the shipped kernels)
+VARIANTS = {"auto": AUTO, "direct2": DIRECT2, "xdma1nt": XDMA1NT}
 
 
 # ---------------------------------------------------------------- per message
@@ -129,7 +127,7 @@ def digest_fixed(data, n: int = None, length: int = None, stride: int = None, ou
     return out
 
 
-DESC_VARIANTS = {"auto": 0, "lane": 1, "xpose": 2, "hybrid": 3, "xdma": 4}   # enum md5hip_desc_variant
+DESC_VARIANTS = {"auto": 0, "lane": 1, "hybrid": 3, "xdma": 4}   # enum md5hip_desc_variant
 
 
 def digest_desc(base, offsets, lens, order=None, out=None, stream=None, variant=0):
@@ -157,8 +155,7 @@ def digest_desc(base, offsets, lens, order=None, out=None, stream=None, variant=
     return out
 
 
-CRC_VARIANTS = {"auto": 0, "shared8": 1, "lane32": 2, "lane16": 3, "xlane16": 4, "xperm16": 5,
-                "xdma16": 6}   # enum crc32hip_variant
+CRC_VARIANTS = {"auto": 0, "xdma16": 6}   # enum crc32hip_variant
 
 
 def crc32_fixed(data, n: int = None, length: int = None, stride: int = None, fastcrc: int = 0,
@@ -260,6 +257,20 @@ def crc_variant_name(v=0) -> str:
     """Name (CRC_VARIANTS key) of the CRC-32 kernel variant v resolves to."""
     r = lib().crc32hip_resolve_variant(CRC_VARIANTS[v] if isinstance(v, str) else v)
     return {k: x for x, k in CRC_VARIANTS.items()}[r]
+
+
+def crc_kernel_name(length: int, fastcrc: int = 0) -> str:
+    """The kernel crc32hip_fixed launches for 16-B aligned chunks of `length`
+    bytes (bench.py's roofline names it)."""
+    if 0 < fastcrc < length:
+        return "crc32_fast"
+    return "crc32_fixed_" + crc_variant_name(0)
+
+
+def code_object_hash() -> str:
+    """SHA-256 of libmd5hip.so's device code (keys profiles/traffic.json)."""
+    from ._lib import code_object_hash as h
+    return h()
 
 
 def resolve_variant(v=AUTO) -> int:

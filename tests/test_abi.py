@@ -44,8 +44,8 @@ def test_exports_every_declared_symbol():
 
 def test_abi_version_and_names():
     L = _lib.lib()
-    assert L.md5hip_abi_version() == 1
-    assert [m.variant_name(v) for v in range(len(m.VARIANTS))] == list(m.VARIANTS)
+    assert L.md5hip_abi_version() == 2
+    assert [m.variant_name(v) for v in m.VARIANTS.values()] == list(m.VARIANTS)
 
 
 def test_header_compiles_as_c_and_layout():
