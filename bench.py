@@ -83,6 +83,9 @@ def parse_args(argv):
                    help="main: only the single-batch launches (PMC passes count one kernel)")
     p.add_argument("--c3q-batches", type=int, default=6,
                    help="--config c3q: C3 submissions streamed through one md5hip_queue")
+    p.add_argument("--c3q-inflight", type=int, default=2,
+                   help="--config c3q: launches in flight before the queue coalesces")
+    p.add_argument("--c3q-slots", type=int, default=4, help="--config c3q: queue slots")
     p.add_argument("--c5-chunks", type=int, default=1 << 18)
     p.add_argument("--c5-slice", type=int, default=64 << 20)
     return p.parse_args(argv)
@@ -700,7 +703,7 @@ def run_c3q(a, rank, world, local, device, backend):
         ptrs = (base + starts[j] + ok_[j]).astype(np.uint64)
         subs.append((ptrs, lk[j].astype(np.uint32),
                      torch.empty((lk[j].size, 16), dtype=torch.uint8, device="cuda")))
-    q = m.Queue(device=torch.cuda.current_device())
+    q = m.Queue(device=torch.cuda.current_device(), nslots=a.c3q_slots, inflight=a.c3q_inflight)
 
     def step():
         ts = [q.submit_device(p, L_, o) for p, L_, o in subs]

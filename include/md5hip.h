@@ -128,7 +128,9 @@ int md5hip_plan_order(const uint32_t *lens, uint64_t n, uint32_t *order);
  * the GPU page tables can use large fragments for the whole range.  Chunks
  * hashed by lane-direct chains (HYBRID's long waves) touch 64 pages per load;
  * they run faster from an arena than from a 2 MiB-aligned hipMalloc buffer.
- * 0 / -EINVAL / -ENODEV / -ENOMEM / -EIO; free with md5hip_arena_free.
+ * 0 / -EINVAL / -ENODEV / -ENOMEM / -EIO; free with md5hip_arena_free, which
+ * first synchronizes the arena's device (a kernel still queued on any stream
+ * may read it), so it may be called right after an asynchronous launch.
  */
 int md5hip_arena_alloc(int device, uint64_t bytes, void **d_ptr);
 int md5hip_arena_free(void *d_ptr);
@@ -149,15 +151,22 @@ int md5hip_plan_desc(const uint32_t *lens, uint64_t n, uint32_t *order);
 int md5hip_fill_synthetic(void *d_dst, uint64_t nbytes, uint64_t seed, void *stream);
 
 /*
- * Host-memory batches (the blk_make_crc call site, blk_io.c:354; config C5).
- * A batcher owns `nslots` pipeline slots (HIP stream + pinned staging of
- * `slice_bytes` + device buffers); slices of the batch flow
- * host gather -> H2D -> kernel -> D2H with slot k+1 overlapping slot k.
+ * The batcher: a thread-safe, coalescing submission queue (md5_submit.c) for
+ * the blk_make_crc call site (blk_io.c:354; configs C3 and C5).  It owns
+ * `nslots` pipeline slots (HIP stream + pinned staging of `slice_bytes` +
+ * device buffers + descriptors).  Submissions from any number of threads
+ * append their chunks to the one OPEN slot -- host chunks are gathered into
+ * its pinned staging, device-resident chunks add only a descriptor -- and
+ * the slot is launched as ONE planned descriptor batch when it is full, when
+ * fewer than `inflight target` slots are running (an idle device takes work
+ * at once), or when a caller waits on, polls or flushes a ticket in it.
+ * While the device is busy, everything submitted meanwhile is therefore
+ * coalesced into the next launch.  A progress thread per batcher retires
+ * finished slots, delivers digests and launches the open slot.
  * slice_bytes = 0 / nslots = 0 select the defaults, 128 MiB x 4: MD5 is one
  * serial chain per chunk, so the bytes in flight must cover the PCIe rate
  * times one chunk's hashing time.
- * Calls are synchronous: they return once every digest is in `digests`.
- * A batcher is not thread-safe; use one per submitting thread.
+ * Every entry saves and restores the calling thread's HIP device.
  */
 typedef struct md5hip_batcher md5hip_batcher;
 
@@ -168,12 +177,36 @@ enum md5hip_digest_kind { MD5HIP_DIGEST_MD5 = 0, MD5HIP_DIGEST_CRC32 = 1 };
 
 int md5hip_batcher_create(int device, uint64_t slice_bytes, uint32_t nslots,
                           md5hip_batcher **out);
+/* A batcher sized for device-resident chunks (md5_batch_submit_device*):
+ * `max_chunks` descriptors per launch (0 = 1,048,576), 16 MiB of staging per
+ * slot for the odd host-memory submission. */
+int md5hip_queue_create(int device, uint64_t max_chunks, uint32_t nslots, md5hip_batcher **out);
+/* Launches what is still open, waits for everything in flight, frees. */
 void md5hip_batcher_destroy(md5hip_batcher *b);
+/* Waits until nothing is queued, then switches (concurrent submitters see
+ * the new kind on their next call; md5hip_batch_verify_iov returns -EAGAIN
+ * if the kind changed between its read and its submit). */
 int md5hip_batcher_set_digest(md5hip_batcher *b, int kind, uint32_t fastcrc);
 int md5hip_batcher_get_digest(const md5hip_batcher *b, int *kind, uint32_t *fastcrc);
+/* The open slot is launched at once while fewer than `target` slots are in
+ * flight (1..nslots; default 2, or 1 with fewer than 3 slots).  1 coalesces
+ * hardest; nslots never waits to coalesce. */
+int md5hip_batcher_set_inflight(md5hip_batcher *b, uint32_t target);
+
+struct md5hip_batcher_stats {
+    uint64_t submissions;             /* tickets issued */
+    uint64_t launches;                /* slots launched */
+    uint64_t coalesced_launches;      /* launches holding chunks of > 1 ticket */
+    uint64_t chunks;                  /* chunks launched */
+    uint64_t bytes_staged;            /* host bytes moved through staging */
+    uint64_t max_chunks_per_launch;
+    uint64_t max_tickets_per_launch;
+    uint64_t inflight_target, nslots, max_chunks_per_slot;
+};
+int md5hip_batcher_get_stats(md5hip_batcher *b, struct md5hip_batcher_stats *out);
 
 /* digests[i] = MD5(ptrs[i], lens[i]); any host memory.  -E2BIG if one chunk
- * exceeds slice_bytes. */
+ * exceeds slice_bytes.  Synchronous. */
 int md5_batch_submit(md5hip_batcher *b, const void *const *ptrs, const uint32_t *lens,
                      uint64_t n, unsigned char *digests);
 
@@ -192,26 +225,36 @@ int md5_batch_submit_iov(md5hip_batcher *b, const struct md5hip_iov *segs,
                          const uint64_t *seg_first, uint64_t n, unsigned char *digests);
 
 /* Asynchronous forms: the
- * call returns once the chunks have been gathered into the batcher's pinned
- * staging -- the caller's buffers may be reused, except in the zero-copy
- * gather modes (registered memory is read by the device until the work is
- * done) -- and *ticket names the submission.  `digests` must stay valid until
- * md5_batch_wait(b, ticket) returns 0 or md5_batch_poll(b, ticket) returns 1;
- * both complete every earlier submission of the batcher too.  A later submit
- * on the same batcher may deliver an earlier submission's digests while it
- * reuses that work's pipeline slot.  Submissions larger than the pipeline
- * (nslots x slice_bytes) block inside the call until slots free up. */
+ * call returns once the chunks are staged -- the caller's buffers may be
+ * reused, except in the zero-copy gather modes (registered memory is read
+ * by the device until the work is done) -- and *ticket names the
+ * submission (0 for an empty one).  `digests` must stay valid until
+ * md5_batch_wait(b, ticket) returns or md5_batch_poll(b, ticket) returns 1.
+ * Tickets complete independently and out of order: a ticket is done when
+ * the slots holding ITS chunks are, whatever earlier tickets still run.
+ * Submissions larger than the free pipeline block inside the call until
+ * slots free up. */
 int md5_batch_submit_async(md5hip_batcher *b, const void *const *ptrs, const uint32_t *lens,
                            uint64_t n, unsigned char *digests, uint64_t *ticket);
 int md5_batch_submit_iov_async(md5hip_batcher *b, const struct md5hip_iov *segs,
                                const uint64_t *seg_first, uint64_t n, unsigned char *digests,
                                uint64_t *ticket);
-/* Block until submission `ticket` (and every earlier one) has delivered its
- * digests: 0 or -errno. */
+/* Device-resident chunks: d_ptrs[i] (a HOST array of device addresses on the
+ * batcher's device, any alignment) and lens[i]; no bytes are copied.  The
+ * digests go to `digests`, device memory of the batcher's device when
+ * digests_on_device != 0, else host memory.  Same ticket semantics. */
+int md5_batch_submit_device_async(md5hip_batcher *b, const uint64_t *d_ptrs, const uint32_t *lens,
+                                  uint64_t n, unsigned char *digests, int digests_on_device,
+                                  uint64_t *ticket);
+int md5_batch_submit_device(md5hip_batcher *b, const uint64_t *d_ptrs, const uint32_t *lens,
+                            uint64_t n, unsigned char *digests, int digests_on_device);
+/* Block until submission `ticket` has delivered its digests: 0 or -errno. */
 int md5_batch_wait(md5hip_batcher *b, uint64_t ticket);
-/* Non-blocking: 1 = `ticket` (and every earlier one) delivered, 0 = still
- * running, <0 = error. */
+/* Non-blocking: 1 = `ticket` delivered, 0 = still running (its slot is
+ * launched if it was waiting to coalesce), <0 = error. */
 int md5_batch_poll(md5hip_batcher *b, uint64_t ticket);
+/* Launch the open slot now, whatever the in-flight count. */
+int md5_batch_flush(md5hip_batcher *b);
 
 /* Batched verify (cache read / write verify sites, blk_io.c:665-704,
  * bc_mgr.c:1464-1492): ok[i] = (digest of chunk i == expected[i]), expected

@@ -38,6 +38,14 @@ class MD5HipIov(ctypes.Structure):
     _fields_ = [("base", ctypes.c_void_p), ("len", ctypes.c_uint32)]
 
 
+class MD5HipBatcherStats(ctypes.Structure):
+    """struct md5hip_batcher_stats (include/md5hip.h)."""
+    _fields_ = [(n, ctypes.c_uint64) for n in (
+        "submissions", "launches", "coalesced_launches", "chunks", "bytes_staged",
+        "max_chunks_per_launch", "max_tickets_per_launch", "inflight_target", "nslots",
+        "max_chunks_per_slot")]
+
+
 class MD5HipError(RuntimeError):
     def __init__(self, fn, rc):
         name = errno.errorcode.get(-rc, str(rc))
@@ -74,6 +82,12 @@ def lib():
         "crc32hip_fixed_variant": (i, [vp, u64, u32, u64, u32, vp, vp, i]),
         "md5hip_fill_synthetic": (i, [vp, u64, u64, vp]),
         "md5hip_batcher_create": (i, [i, u64, u32, ctypes.POINTER(vp)]),
+        "md5hip_queue_create": (i, [i, u64, u32, ctypes.POINTER(vp)]),
+        "md5hip_batcher_set_inflight": (i, [vp, u32]),
+        "md5hip_batcher_get_stats": (i, [vp, ctypes.POINTER(MD5HipBatcherStats)]),
+        "md5_batch_submit_device_async": (i, [vp, vp, vp, u64, vp, i, vp]),
+        "md5_batch_submit_device": (i, [vp, vp, vp, u64, vp, i]),
+        "md5_batch_flush": (i, [vp]),
         "md5hip_batcher_destroy": (None, [vp]),
         "md5_batch_submit": (i, [vp, vp, vp, u64, vp]),
         "md5_batch_submit_iov": (i, [vp, vp, vp, u64, vp]),
@@ -135,7 +149,9 @@ EXPORTS = ["MD5Init", "MD5Update", "MD5Final", "nc_MD5Init", "nc_MD5Update", "nc
            "nc_digest_update", "nc_digest_verify", "nc_digest_scatter", "nc_digest_compare",
            "nc_crc32", "nc_header_crc", "nc_header_seal", "nc_header_verify",
            "md5hip_batch_verify_headers", "md5hip_host_register", "md5hip_host_unregister",
-           "md5hip_batcher_set_gather", "md5hip_pool_set_gather"]
+           "md5hip_batcher_set_gather", "md5hip_pool_set_gather", "md5hip_queue_create",
+           "md5hip_batcher_set_inflight", "md5hip_batcher_get_stats", "md5_batch_submit_device_async",
+           "md5_batch_submit_device", "md5_batch_flush"]
 
 
 def check(fn, rc):

@@ -23,6 +23,15 @@ __attribute__((visibility("hidden")))
 int md5hip_gather_launch(const struct md5hip_seg *d_segs, uint64_t nseg, unsigned char *d_dst,
                          void *stream);
 
+/* Batched verify with a digest kind of its own (md5_submit.c): the
+ * batcher's setting is not touched, so concurrent submitters keep theirs. */
+struct md5hip_batcher;
+struct md5hip_iov;
+__attribute__((visibility("hidden")))
+int md5hip_verify_iov_as(struct md5hip_batcher *b, int kind, uint32_t fastcrc,
+                         const struct md5hip_iov *segs, const uint64_t *seg_first, uint64_t n,
+                         const void *expected, unsigned char *ok);
+
 #ifdef __cplusplus
 }
 #endif

@@ -301,6 +301,7 @@ struct Arena {
   void* base;      // the reservation (the runtime ignores a reservation's
   size_t rsize;    // alignment argument, so it is over-reserved by kArenaAlign)
   hipMemGenericAllocationHandle_t h;
+  int device;
 };
 std::mutex g_arena_mu;
 std::vector<Arena> g_arenas;
@@ -345,7 +346,7 @@ int md5hip_arena_alloc(int device, uint64_t bytes, void** out) {
   }
   {
     std::lock_guard<std::mutex> lk(g_arena_mu);
-    g_arenas.push_back(Arena{ptr, size, base, rsize, h});
+    g_arenas.push_back(Arena{ptr, size, base, rsize, h, device});
   }
   *out = ptr;
   return 0;
@@ -362,10 +363,16 @@ int md5hip_arena_free(void* ptr) {
     a = g_arenas[k];
     g_arenas.erase(g_arenas.begin() + (long)k);
   }
-  int rc = 0;
+  // Not stream-ordered like torch's allocator: a kernel still queued on any
+  // stream of the device may read the arena, so drain the device before the
+  // pages go (md5hip.h: freeing an arena synchronizes its device).
+  int rc = 0, prev = -1;
+  const bool had = hipGetDevice(&prev) == hipSuccess;
+  if (hipSetDevice(a.device) != hipSuccess || hipDeviceSynchronize() != hipSuccess) rc = -EIO;
   if (hipMemUnmap(a.ptr, a.size) != hipSuccess) rc = -EIO;
   if (hipMemRelease(a.h) != hipSuccess) rc = -EIO;
   if (hipMemAddressFree(a.base, a.rsize) != hipSuccess) rc = -EIO;
+  if (had) (void)hipSetDevice(prev);
   return rc;
 }
 

@@ -198,12 +198,10 @@ int md5hip_pool_submit(md5hip_pool *p, const void *const *ptrs, const uint32_t *
     return rc;
 }
 
-int md5hip_pool_submit_iov(md5hip_pool *p, const struct md5hip_iov *segs, const uint64_t *seg_first,
-                           uint64_t n, unsigned char *digests)
+/* (p->lock held) */
+static int pool_submit_iov_locked(md5hip_pool *p, const struct md5hip_iov *segs,
+                                  const uint64_t *seg_first, uint64_t n, unsigned char *digests)
 {
-    if (!p) return -EINVAL;
-    if (n == 0) return 0;
-    if (!segs || !seg_first || !digests || seg_first[0] != 0) return -EINVAL;
     uint32_t *lens = malloc(4 * n);
     uint64_t *rebased = malloc(8 * (n + p->ndev));
     if (!lens || !rebased) { free(lens); free(rebased); return -ENOMEM; }
@@ -220,7 +218,6 @@ int md5hip_pool_submit_iov(md5hip_pool *p, const struct md5hip_iov *segs, const 
     if (rc == 0) {
         uint64_t first[POOL_MAX_DEV + 1];
         struct job jobs[POOL_MAX_DEV];
-        pthread_mutex_lock(&p->lock);
         md5hip_pool_plan(lens, n, p->ndev, first);
         jobs_init(p, jobs, JOB_IOV, first, digests);
         /* each device sees its own seg_first[] re-based to 0 (n+G entries total) */
@@ -233,10 +230,21 @@ int md5hip_pool_submit_iov(md5hip_pool *p, const struct md5hip_iov *segs, const 
                 rebased[at++] = seg_first[i] - seg_first[first[g]];
         }
         rc = run_jobs(jobs, p->ndev);
-        pthread_mutex_unlock(&p->lock);
     }
     free(lens);
     free(rebased);
+    return rc;
+}
+
+int md5hip_pool_submit_iov(md5hip_pool *p, const struct md5hip_iov *segs, const uint64_t *seg_first,
+                           uint64_t n, unsigned char *digests)
+{
+    if (!p) return -EINVAL;
+    if (n == 0) return 0;
+    if (!segs || !seg_first || !digests || seg_first[0] != 0) return -EINVAL;
+    pthread_mutex_lock(&p->lock);
+    const int rc = pool_submit_iov_locked(p, segs, seg_first, n, digests);
+    pthread_mutex_unlock(&p->lock);
     return rc;
 }
 
@@ -266,11 +274,14 @@ int md5hip_pool_verify_iov(md5hip_pool *p, const struct md5hip_iov *segs, const 
 {
     if (!p) return -EINVAL;
     if (n == 0) return 0;
-    if (!expected || !ok) return -EINVAL;
+    if (!expected || !ok || !segs || !seg_first || seg_first[0] != 0) return -EINVAL;
+    /* the digest size is read and used under one hold of the pool lock, so a
+     * concurrent md5hip_pool_set_digest cannot change it in between */
+    pthread_mutex_lock(&p->lock);
     const uint32_t dsz = p->dsz;
     unsigned char *got = malloc((size_t)dsz * n);
-    if (!got) return -ENOMEM;
-    int rc = md5hip_pool_submit_iov(p, segs, seg_first, n, got);
+    int rc = got ? pool_submit_iov_locked(p, segs, seg_first, n, got) : -ENOMEM;
+    pthread_mutex_unlock(&p->lock);
     if (rc == 0) {
         const unsigned char *e = expected;
         for (uint64_t i = 0; i < n; i++) {

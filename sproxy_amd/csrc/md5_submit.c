@@ -1,22 +1,48 @@
 /*
- * md5_submit.c -- host-memory batched submit (include/md5hip.h).
+ * md5_submit.c -- the batcher: a thread-safe, coalescing submission queue in
+ * front of the batched kernels (include/md5hip.h).
  *
  * Serves the netcache block-completion checksum site (blk_make_crc,
- * netcache/common/blk_io.c:354-430): chunks live in host memory (cache pages,
- * socket buffers), so the batch is staged H2D, hashed on the device and the
- * 16-byte digests come back D2H.  A batcher owns `nslots` pipeline slots; slot
- * k has its own HIP stream, pinned staging buffer, device buffer, descriptor
- * arrays and completion event, so the host gather of slice k+1, the H2D copy
- * of slice k and the kernel of slice k-1 overlap.
+ * netcache/common/blk_io.c:354-430, called from ASIO pool threads,
+ * asio_mgr.c:1054-1057): chunks live in host memory (cache pages, socket
+ * buffers) or already in HBM, and each caller wants its own digests back.
  *
- * Errors: 0 / negative errno (include/md5hip.h conventions); -E2BIG when one
- * chunk alone exceeds the slot's staging capacity.
+ * A batcher owns `nslots` pipeline slots.  Slot k has its own HIP stream,
+ * pinned staging, device buffers, descriptor arrays and completion event.
+ * At most one slot is OPEN at a time: submissions (from any thread) append
+ * their chunks to it -- host chunks are gathered into its pinned staging,
+ * device-resident chunks only add a descriptor -- and the slot is launched
+ * as ONE planned descriptor batch (md5hip_plan_desc) when
+ *   - it is full (bytes, descriptors or gather segments), or
+ *   - fewer than `target` slots are in flight (an idle pipeline takes work at
+ *     once: no added latency when the device is not busy), or
+ *   - a caller waits on / polls / flushes a ticket it holds.
+ * So while the device is busy, everything submitted meanwhile is coalesced
+ * into the next launch: a 1 MiB chunk's serial chain (~10 ms) then runs
+ * beside the bytes of many later submissions instead of ending its launch
+ * alone.
+ *
+ * Completion is per ticket and out of order: a ticket completes when every
+ * slot holding its chunks has finished, whatever earlier tickets are doing.
+ * A progress thread per batcher polls the in-flight slots' events, delivers
+ * host digests (D2H staging -> the caller's array), retires slots and
+ * launches the open slot when the pipeline drains below `target`.
+ *
+ * Locking: b->mu guards all batcher state; HIP enqueue calls are made under
+ * it (they are asynchronous); host gathers (memcpy) run outside it, the slot
+ * held open by a writer count.  Lock order: b->mu, then g_reg_lock.
+ *
+ * Every entry saves and restores the calling thread's HIP device.
+ * Errors: 0 / negative errno (include/md5hip.h); -E2BIG when one chunk
+ * exceeds the slot's staging; -EFAULT when registered memory vanished
+ * under a zero-copy submission.
  */
 #include <errno.h>
 #include <pthread.h>
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
 #include <hip/hip_runtime_api.h>
 
@@ -52,13 +78,32 @@ static long reg_find(uintptr_t p, uint64_t len)
     return -1;
 }
 
+/* The caller's HIP device, restored on every exit from an entry. */
+struct dev_guard { int prev; int ok; };
+static int dev_enter(struct dev_guard *g, int device)
+{
+    g->ok = hipGetDevice(&g->prev) == hipSuccess;
+    if (hipSetDevice(device) != hipSuccess) {
+        if (g->ok) (void)hipSetDevice(g->prev);
+        return -ENODEV;
+    }
+    return 0;
+}
+static void dev_leave(const struct dev_guard *g)
+{
+    if (g->ok) (void)hipSetDevice(g->prev);
+}
+
 int md5hip_host_register(void *base, uint64_t bytes)
 {
     if (!base || bytes == 0) return -EINVAL;
     const uintptr_t lo = (uintptr_t)base, hi = lo + bytes;
-    int ndev = 0, cur = 0;
+    int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return -ENODEV;
     if (ndev > REG_MAXDEV) ndev = REG_MAXDEV;
+    struct dev_guard g;
+    (void)hipGetDevice(&g.prev);
+    g.ok = 1;
     pthread_rwlock_wrlock(&g_reg_lock);
     int rc = 0;
     size_t at = 0;
@@ -72,8 +117,8 @@ int md5hip_host_register(void *base, uint64_t bytes)
         g_capreg = cap;
     }
     /* coarse-grained: the batcher reads a range only between the caller's
-     * writes (calls are synchronous), and DMA from coarse-grained pages runs
-     * 44 vs 34 GB/s; MD5HIP_REGISTER_COARSE=0 turns it off */
+     * writes, and DMA from coarse-grained pages runs 44 vs 34 GB/s
+     * (DESIGN.md §5); MD5HIP_REGISTER_COARSE=0 turns it off */
     unsigned flags = hipHostRegisterPortable | hipHostRegisterMapped;
     const char *coarse = getenv("MD5HIP_REGISTER_COARSE");
     if (!coarse || atoi(coarse)) flags |= hipExtHostRegisterCoarseGrained;
@@ -82,18 +127,17 @@ int md5hip_host_register(void *base, uint64_t bytes)
         goto out;
     }
     struct reg_range r = {lo, hi, {0}};
-    (void)hipGetDevice(&cur);
     for (int d = 0; d < ndev; d++) {
         void *dp = NULL;
         if (hipSetDevice(d) == hipSuccess && hipHostGetDevicePointer(&dp, base, 0) == hipSuccess)
             r.delta[d] = (intptr_t)((uintptr_t)dp - lo);
     }
-    (void)hipSetDevice(cur);
     memmove(&g_reg[at + 1], &g_reg[at], (g_nreg - at) * sizeof *g_reg);
     g_reg[at] = r;
     g_nreg++;
 out:
     pthread_rwlock_unlock(&g_reg_lock);
+    dev_leave(&g);
     return rc;
 }
 
@@ -114,6 +158,20 @@ int md5hip_host_unregister(void *base)
     return rc;
 }
 
+/* ------------------------------------------------------------------------
+ * Slots and tickets
+ * ------------------------------------------------------------------------ */
+enum slot_state { SLOT_FREE = 0, SLOT_OPEN, SLOT_INFLIGHT };
+enum slot_mode { MODE_NONE = 0, MODE_STAGED, MODE_ZEROCOPY, MODE_FIXED };
+
+/* One ticket's chunks in one slot: slot chunks [first, first+count) deliver
+ * into `user` (host array, or device memory when on_device). */
+struct seg {
+    uint64_t ticket, first, count;
+    unsigned char *user;
+    int on_device;
+};
+
 struct slot {
     hipStream_t stream;
     hipEvent_t done;
@@ -125,11 +183,18 @@ struct slot {
     struct md5hip_seg *h_seg, *d_seg; /* zero-copy gather table, `segcap` entries */
     void **b_dst, **b_src;            /* DMA-batch gather arrays (plain host memory) */
     size_t *b_len;
-    unsigned char *user_dig;          /* where this slot's digests go (NULL = idle) */
-    uint64_t ticket;                  /* submission the in-flight work belongs to */
-    uint64_t ndig;
-    uint32_t dsz;
-    int busy;
+    long *b_reg;                      /* registration each DMA entry lies in */
+    struct md5hip_seg *h_dsc, *d_dsc; /* device-digest scatter table, `segcap` entries */
+    struct seg *segs;                 /* ticket segments */
+    uint32_t nsegs, capsegs;
+    int state, mode, writers, full, flush, err;
+    uint64_t n, used, nseg, ndma, ndsc;
+    uint32_t kind, fastcrc, dsz;
+    /* MODE_FIXED (md5hip_batch_host_fixed): one contiguous host range */
+    const unsigned char *fx_src;
+    uint64_t fx_bytes, fx_stride;
+    uint32_t fx_len;
+    uint64_t tickets_in;              /* distinct tickets (stats) */
 };
 
 struct md5hip_batcher {
@@ -142,30 +207,321 @@ struct md5hip_batcher {
     uint64_t maxn;     /* chunks per slot */
     uint64_t segcap;   /* gather segments per slot (zero-copy modes) */
     int gather;        /* enum md5hip_gather_mode */
-    uint32_t next;     /* slot the next slice goes to (round robin across calls) */
-    uint64_t ticket;   /* last submission ticket issued (md5_batch_wait) */
+    uint32_t target;   /* launch the open slot at once while fewer slots are in flight */
     struct slot *s;
+    int open;          /* index of the OPEN slot new chunks go to, -1 = none */
+    uint32_t inflight;
+    /* tickets: ring of ids [tk_lo, tk_hi); id t at tk[t & (tkcap - 1)] */
+    uint64_t tk_lo, tk_hi;
+    uint32_t *tk_pending;
+    int *tk_err;
+    uint64_t tkcap;
+    int broken;        /* sticky first error of a ticket that has left the ring */
+    struct md5hip_batcher_stats st;
+    pthread_mutex_t mu;
+    pthread_cond_t done_cv;   /* a slot retired / a ticket completed */
+    pthread_cond_t work_cv;   /* a slot went in flight / stop */
+    pthread_t progress;
+    int progress_started, stop;
 };
 
 #define CK(x) do { if ((x) != hipSuccess) { rc = -ENODEV; goto fail; } } while (0)
 
-static int slot_retire(struct slot *sl)
+static int tk_grow(md5hip_batcher *b)
 {
-    if (!sl->busy) return 0;
-    if (hipEventSynchronize(sl->done) != hipSuccess) return -EIO;
-    if (sl->user_dig) memcpy(sl->user_dig, sl->h_dig, (size_t)sl->dsz * sl->ndig);
-    sl->busy = 0;
-    sl->user_dig = NULL;
+    const uint64_t nc = b->tkcap ? 2 * b->tkcap : 1024;
+    uint32_t *p = malloc(nc * sizeof *p);
+    int *e = malloc(nc * sizeof *e);
+    if (!p || !e) { free(p); free(e); return -ENOMEM; }
+    for (uint64_t t = b->tk_lo; t < b->tk_hi; t++) {
+        p[t & (nc - 1)] = b->tk_pending[t & (b->tkcap - 1)];
+        e[t & (nc - 1)] = b->tk_err[t & (b->tkcap - 1)];
+    }
+    free(b->tk_pending);
+    free(b->tk_err);
+    b->tk_pending = p;
+    b->tk_err = e;
+    b->tkcap = nc;
     return 0;
 }
 
-void md5hip_batcher_destroy(md5hip_batcher *b)
+/* a new ticket holding one "submission in progress" reference (mu held) */
+static int tk_new(md5hip_batcher *b, uint64_t *t)
 {
-    if (!b) return;
-    hipSetDevice(b->device);
+    if (b->tk_hi - b->tk_lo == b->tkcap) {
+        const int rc = tk_grow(b);
+        if (rc) return rc;
+    }
+    const uint64_t id = b->tk_hi++;
+    b->tk_pending[id & (b->tkcap - 1)] = 1;
+    b->tk_err[id & (b->tkcap - 1)] = 0;
+    *t = id;
+    return 0;
+}
+
+/* 1 = complete, 0 = pending; *err = its error (mu held) */
+static int tk_done(const md5hip_batcher *b, uint64_t t, int *err)
+{
+    if (t < b->tk_lo) { *err = b->broken; return 1; }
+    *err = b->tk_err[t & (b->tkcap - 1)];
+    return b->tk_pending[t & (b->tkcap - 1)] == 0;
+}
+
+static void tk_put(md5hip_batcher *b, uint64_t t, int err)
+{
+    if (t < b->tk_lo) return;
+    const uint64_t k = t & (b->tkcap - 1);
+    if (err && !b->tk_err[k]) b->tk_err[k] = err;
+    if (b->tk_pending[k]) b->tk_pending[k]--;
+    while (b->tk_lo < b->tk_hi && b->tk_pending[b->tk_lo & (b->tkcap - 1)] == 0) {
+        const int e = b->tk_err[b->tk_lo & (b->tkcap - 1)];
+        if (e && !b->broken) b->broken = e;
+        b->tk_lo++;
+    }
+}
+
+/* One segment per (ticket, slot): a submission fills a slot until it is full
+ * before it moves on, so its chunks in one slot are one contiguous run. */
+static int seg_push(struct slot *sl, struct seg sg)
+{
+    if (sl->nsegs == sl->capsegs) {
+        const uint32_t nc = sl->capsegs ? 2 * sl->capsegs : 64;
+        struct seg *p = realloc(sl->segs, nc * sizeof *p);
+        if (!p) return -ENOMEM;
+        sl->segs = p;
+        sl->capsegs = nc;
+    }
+    sl->segs[sl->nsegs++] = sg;
+    sl->tickets_in++;
+    return 0;
+}
+
+static int seg_has(const struct slot *sl, uint64_t t)
+{
+    for (uint32_t k = 0; k < sl->nsegs; k++)
+        if (sl->segs[k].ticket == t) return 1;
+    return 0;
+}
+
+/* Enqueue slot `sl` (mu held, writers == 0): bytes in, kernel, digests out. */
+static int slot_enqueue(md5hip_batcher *b, struct slot *sl)
+{
+    int rc = 0;
+    const uint64_t n = sl->n;
+    if (sl->mode == MODE_FIXED) {
+        if (hipMemcpyAsync(sl->d_data, sl->fx_src, sl->fx_bytes, hipMemcpyHostToDevice, sl->stream))
+            return -EIO;
+        rc = sl->kind == MD5HIP_DIGEST_CRC32
+                 ? crc32hip_fixed(sl->d_data, n, sl->fx_len, sl->fx_stride, sl->fastcrc,
+                                  (uint32_t *)sl->d_dig, sl->stream)
+                 : md5hip_digest_fixed(sl->d_data, n, sl->fx_len, sl->fx_stride, sl->d_dig, sl->stream);
+        if (rc) return rc;
+    } else {
+        const int dvar = md5hip_plan_desc(sl->h_len, n, sl->h_ord);
+        if (dvar < 0) return dvar;
+        if (hipMemcpyAsync(sl->d_off, sl->h_off, 8 * n, hipMemcpyHostToDevice, sl->stream) ||
+            hipMemcpyAsync(sl->d_len, sl->h_len, 4 * n, hipMemcpyHostToDevice, sl->stream) ||
+            hipMemcpyAsync(sl->d_ord, sl->h_ord, 4 * n, hipMemcpyHostToDevice, sl->stream))
+            return -EIO;
+        if (sl->mode == MODE_STAGED && sl->used) {
+            if (hipMemcpyAsync(sl->d_data, sl->h_data, sl->used, hipMemcpyHostToDevice, sl->stream))
+                return -EIO;
+        } else if (sl->mode == MODE_ZEROCOPY && sl->nseg) {
+            int mode = b->gather;
+            if (mode == MD5HIP_GATHER_AUTO)
+                /* measured: per-copy DMA beats the PCIe-reading
+                 * gather kernel once copies average more than ~192 KiB */
+                mode = sl->ndma * (256u << 10) <= sl->used ? MD5HIP_GATHER_DMA : MD5HIP_GATHER_DEVICE;
+            if (mode == MD5HIP_GATHER_DEVICE) {
+                if (hipMemcpyAsync(sl->d_seg, sl->h_seg, sizeof(struct md5hip_seg) * sl->nseg,
+                                   hipMemcpyHostToDevice, sl->stream))
+                    return -EIO;
+                if ((rc = md5hip_gather_launch(sl->d_seg, sl->nseg, sl->d_data, sl->stream))) return rc;
+            } else {
+                /* one async copy per run (hipMemcpyBatchAsync is newer than the
+                 * HIP runtime torch ships, which this library shares) */
+                for (uint64_t q = 0; q < sl->ndma; q++)
+                    if (hipMemcpyAsync(sl->b_dst[q], sl->b_src[q], sl->b_len[q], hipMemcpyHostToDevice,
+                                       sl->stream) != hipSuccess)
+                        return -EIO;
+            }
+        }
+        rc = sl->kind == MD5HIP_DIGEST_CRC32
+                 ? crc32hip_desc(sl->d_data, sl->d_off, sl->d_len, sl->d_ord, n, sl->fastcrc,
+                                 (uint32_t *)sl->d_dig, sl->stream)
+                 : md5hip_digest_desc_variant(sl->d_data, sl->d_off, sl->d_len, sl->d_ord, n,
+                                              sl->d_dig, sl->stream, dvar);
+        if (rc) return rc;
+    }
+    /* digests out: one D2H for the host segments, one scatter for the device ones */
+    int any_host = 0;
+    sl->ndsc = 0;
+    for (uint32_t k = 0; k < sl->nsegs; k++) {
+        const struct seg *g = &sl->segs[k];
+        if (!g->on_device) { any_host = 1; continue; }
+        sl->h_dsc[sl->ndsc++] = (struct md5hip_seg){
+            (uint64_t)(uintptr_t)(sl->d_dig + (size_t)sl->dsz * g->first),
+            (uint64_t)((uintptr_t)g->user - (uintptr_t)sl->d_dig),     /* relative to d_dig (mod 2^64) */
+            (uint32_t)(sl->dsz * g->count), 0};
+    }
+    if (sl->ndsc) {
+        if (hipMemcpyAsync(sl->d_dsc, sl->h_dsc, sizeof(struct md5hip_seg) * sl->ndsc,
+                           hipMemcpyHostToDevice, sl->stream))
+            return -EIO;
+        if ((rc = md5hip_gather_launch(sl->d_dsc, sl->ndsc, sl->d_dig, sl->stream))) return rc;
+    }
+    if (any_host &&
+        hipMemcpyAsync(sl->h_dig, sl->d_dig, (size_t)sl->dsz * n, hipMemcpyDeviceToHost, sl->stream))
+        return -EIO;
+    if (hipEventRecord(sl->done, sl->stream)) return -EIO;
+    return 0;
+}
+
+static void slot_reset(struct slot *sl)
+{
+    sl->state = SLOT_FREE;
+    sl->mode = MODE_NONE;
+    sl->writers = sl->full = sl->flush = sl->err = 0;
+    sl->n = sl->used = sl->nseg = sl->ndma = sl->ndsc = 0;
+    sl->nsegs = 0;
+    sl->tickets_in = 0;
+}
+
+/* Deliver a finished (or failed) slot to its tickets and free it (mu held). */
+static void slot_retire(md5hip_batcher *b, struct slot *sl, int err)
+{
+    for (uint32_t k = 0; k < sl->nsegs; k++) {
+        const struct seg *g = &sl->segs[k];
+        if (!err && !g->on_device)
+            memcpy(g->user, sl->h_dig + (size_t)sl->dsz * g->first, (size_t)sl->dsz * g->count);
+        tk_put(b, g->ticket, err);
+    }
+    if (sl->state == SLOT_INFLIGHT) b->inflight--;
+    slot_reset(sl);
+    pthread_cond_broadcast(&b->done_cv);
+}
+
+/* Launch slot `sl` if it may go now (mu held). */
+static void slot_try_launch(md5hip_batcher *b, struct slot *sl)
+{
+    if (sl->state != SLOT_OPEN || sl->writers) return;
+    if (sl->n == 0) {                 /* nothing reserved (all chunks failed) */
+        if (b->open == (int)(sl - b->s)) b->open = -1;
+        slot_retire(b, sl, sl->err);
+        return;
+    }
+    if (!(sl->full || sl->flush || b->inflight < b->target)) return;
+    if (b->open == (int)(sl - b->s)) b->open = -1;
+    const int rc = sl->err ? sl->err : slot_enqueue(b, sl);
+    if (rc) {
+        slot_retire(b, sl, rc);
+        return;
+    }
+    sl->state = SLOT_INFLIGHT;
+    b->inflight++;
+    b->st.launches++;
+    b->st.chunks += sl->n;
+    b->st.bytes_staged += sl->used;
+    if (sl->n > b->st.max_chunks_per_launch) b->st.max_chunks_per_launch = sl->n;
+    if (sl->tickets_in > 1) b->st.coalesced_launches++;
+    if (sl->tickets_in > b->st.max_tickets_per_launch) b->st.max_tickets_per_launch = sl->tickets_in;
+    pthread_cond_broadcast(&b->work_cv);
+}
+
+/* A FREE slot made OPEN in `mode` for digests of `kind` (mu held; waits
+ * for one to retire). */
+static struct slot *slot_take(md5hip_batcher *b, int mode, int kind, uint32_t fastcrc)
+{
+    for (;;) {
+        for (uint32_t k = 0; k < b->nslots; k++) {
+            struct slot *sl = &b->s[k];
+            if (sl->state != SLOT_FREE) continue;
+            slot_reset(sl);
+            sl->state = SLOT_OPEN;
+            sl->mode = mode;
+            sl->kind = (uint32_t)kind;
+            sl->fastcrc = fastcrc;
+            sl->dsz = kind == MD5HIP_DIGEST_CRC32 ? 4 : 16;
+            return sl;
+        }
+        /* all busy: make sure the open slot can go, then wait for a retire */
+        if (b->open >= 0) {
+            struct slot *o = &b->s[b->open];
+            o->full = 1;
+            slot_try_launch(b, o);
+        }
+        pthread_cond_wait(&b->done_cv, &b->mu);
+    }
+}
+
+/* The OPEN slot that accepts chunks of `mode` and digest `kind` (mu held). */
+static struct slot *slot_open(md5hip_batcher *b, int mode, int kind, uint32_t fastcrc)
+{
+    if (b->open >= 0) {
+        struct slot *o = &b->s[b->open];
+        const int compatible = (o->mode == mode || mode == MODE_NONE || o->mode == MODE_NONE) &&
+                               o->kind == (uint32_t)kind && o->fastcrc == fastcrc;
+        if (!o->full && compatible && o->nsegs < b->segcap) {
+            if (o->mode == MODE_NONE) o->mode = mode;
+            return o;
+        }
+        o->full = 1;                 /* closes: launched once its writers are done */
+        b->open = -1;
+        slot_try_launch(b, o);
+    }
+    struct slot *sl = slot_take(b, mode, kind, fastcrc);
+    b->open = (int)(sl - b->s);
+    return sl;
+}
+
+/* ------------------------------------------------------------------------
+ * Progress thread: retire finished slots, launch coalesced work.
+ * ------------------------------------------------------------------------ */
+static void *progress_main(void *arg)
+{
+    md5hip_batcher *b = arg;
+    (void)hipSetDevice(b->device);
+    pthread_mutex_lock(&b->mu);
+    unsigned idle_us = 20;
+    while (!b->stop) {
+        int any = 0;
+        for (uint32_t k = 0; k < b->nslots; k++) {
+            struct slot *sl = &b->s[k];
+            if (sl->state != SLOT_INFLIGHT) continue;
+            const hipError_t e = hipEventQuery(sl->done);
+            if (e == hipErrorNotReady) continue;
+            slot_retire(b, sl, e == hipSuccess ? 0 : -EIO);
+            any = 1;
+        }
+        if (any) {
+            if (b->open >= 0) slot_try_launch(b, &b->s[b->open]);
+            idle_us = 20;
+            continue;
+        }
+        if (b->inflight == 0) {
+            pthread_cond_wait(&b->work_cv, &b->mu);
+            idle_us = 20;
+        } else {
+            struct timespec ts;
+            clock_gettime(CLOCK_REALTIME, &ts);
+            ts.tv_nsec += (long)idle_us * 1000;
+            if (ts.tv_nsec >= 1000000000L) { ts.tv_sec++; ts.tv_nsec -= 1000000000L; }
+            pthread_cond_timedwait(&b->work_cv, &b->mu, &ts);
+            if (idle_us < 200) idle_us += 20;
+        }
+    }
+    pthread_mutex_unlock(&b->mu);
+    return NULL;
+}
+
+/* ------------------------------------------------------------------------
+ * Create / destroy / settings
+ * ------------------------------------------------------------------------ */
+static void batcher_free(md5hip_batcher *b)
+{
     for (uint32_t k = 0; b->s && k < b->nslots; k++) {
         struct slot *sl = &b->s[k];
-        if (sl->busy) hipEventSynchronize(sl->done);
+        if (sl->state == SLOT_INFLIGHT) hipEventSynchronize(sl->done);
         if (sl->stream) hipStreamDestroy(sl->stream);
         if (sl->done) hipEventDestroy(sl->done);
         hipHostFree(sl->h_data); hipHostFree(sl->h_off); hipHostFree(sl->h_len);
@@ -173,39 +529,72 @@ void md5hip_batcher_destroy(md5hip_batcher *b)
         hipFree(sl->d_data); hipFree(sl->d_off); hipFree(sl->d_len);
         hipFree(sl->d_ord); hipFree(sl->d_dig);
         hipHostFree(sl->h_seg); hipFree(sl->d_seg);
-        free(sl->b_dst); free(sl->b_src); free(sl->b_len);
+        hipHostFree(sl->h_dsc); hipFree(sl->d_dsc);
+        free(sl->b_dst); free(sl->b_src); free(sl->b_len); free(sl->b_reg);
+        free(sl->segs);
     }
     free(b->s);
+    free(b->tk_pending);
+    free(b->tk_err);
+    pthread_mutex_destroy(&b->mu);
+    pthread_cond_destroy(&b->done_cv);
+    pthread_cond_destroy(&b->work_cv);
     free(b);
 }
 
-int md5hip_batcher_create(int device, uint64_t slice_bytes, uint32_t nslots, md5hip_batcher **out)
+void md5hip_batcher_destroy(md5hip_batcher *b)
+{
+    if (!b) return;
+    struct dev_guard g;
+    if (dev_enter(&g, b->device)) g.ok = 0;
+    if (b->progress_started) {
+        pthread_mutex_lock(&b->mu);
+        /* launch what is still open so every ticket completes, then drain */
+        if (b->open >= 0) {
+            struct slot *o = &b->s[b->open];
+            o->flush = 1;
+            slot_try_launch(b, o);
+        }
+        while (b->inflight) pthread_cond_wait(&b->done_cv, &b->mu);
+        b->stop = 1;
+        pthread_cond_broadcast(&b->work_cv);
+        pthread_mutex_unlock(&b->mu);
+        pthread_join(b->progress, NULL);
+    }
+    batcher_free(b);
+    dev_leave(&g);
+}
+
+static int batcher_new(int device, uint64_t slice_bytes, uint32_t nslots, uint64_t maxn,
+                       md5hip_batcher **out)
 {
     int rc = 0;
     if (!out) return -EINVAL;
     *out = NULL;
-    /* defaults sized for MD5's serial chains: a slice of B-byte chunks keeps
-     * slice/B lanes busy for B/110 MB/s (one chain), so the bytes in flight
-     * must cover PCIe rate x chain time -- 4 x 128 MiB reaches the H2D rate
-     * for 256 KiB blocks where 3 x 64 MiB stalls at ~34 GB/s (DESIGN.md §5) */
     if (nslots == 0) nslots = 4;
     if (nslots > 16) return -EINVAL;
-    if (slice_bytes == 0) slice_bytes = 128ull << 20;
     slice_bytes = (slice_bytes + 4095) & ~4095ull;
-    if (hipSetDevice(device) != hipSuccess) return -ENODEV;
+    if (slice_bytes == 0) slice_bytes = 4096;
+    struct dev_guard g;
+    if (dev_enter(&g, device)) return -ENODEV;
     md5hip_batcher *b = calloc(1, sizeof *b);
-    if (!b) return -ENOMEM;
+    if (!b) { dev_leave(&g); return -ENOMEM; }
+    pthread_mutex_init(&b->mu, NULL);
+    pthread_cond_init(&b->done_cv, NULL);
+    pthread_cond_init(&b->work_cv, NULL);
     b->device = device;
     b->kind = MD5HIP_DIGEST_MD5;
     b->dsz = 16;
     b->nslots = nslots;
     b->cap = slice_bytes;
-    b->maxn = slice_bytes / 64 < 4096 ? 4096 : slice_bytes / 64;
-    if (b->maxn > (1u << 20)) b->maxn = 1u << 20;      /* descriptors: 32 B per chunk */
+    b->maxn = maxn;
     b->segcap = slice_bytes / 1024 < 4096 ? 4096 : slice_bytes / 1024;
     b->gather = MD5HIP_GATHER_AUTO;
+    b->target = nslots > 2 ? 2 : 1;
+    b->open = -1;
+    b->tk_lo = b->tk_hi = 1;              /* ticket 0 = "nothing": complete at once */
     b->s = calloc(nslots, sizeof *b->s);
-    if (!b->s) { free(b); return -ENOMEM; }
+    if (!b->s || tk_grow(b)) { rc = -ENOMEM; goto fail; }
     for (uint32_t k = 0; k < nslots; k++) {
         struct slot *sl = &b->s[k];
         CK(hipStreamCreateWithFlags(&sl->stream, hipStreamNonBlocking));
@@ -222,120 +611,140 @@ int md5hip_batcher_create(int device, uint64_t slice_bytes, uint32_t nslots, md5
         CK(hipMalloc((void **)&sl->d_dig, 16 * b->maxn));
         CK(hipHostMalloc((void **)&sl->h_seg, sizeof(struct md5hip_seg) * b->segcap, hipHostMallocDefault));
         CK(hipMalloc((void **)&sl->d_seg, sizeof(struct md5hip_seg) * b->segcap));
+        CK(hipHostMalloc((void **)&sl->h_dsc, sizeof(struct md5hip_seg) * b->segcap, hipHostMallocDefault));
+        CK(hipMalloc((void **)&sl->d_dsc, sizeof(struct md5hip_seg) * b->segcap));
         sl->b_dst = malloc(sizeof(void *) * b->segcap);
         sl->b_src = malloc(sizeof(void *) * b->segcap);
         sl->b_len = malloc(sizeof(size_t) * b->segcap);
-        if (!sl->b_dst || !sl->b_src || !sl->b_len) { rc = -ENOMEM; goto fail; }
+        sl->b_reg = malloc(sizeof(long) * b->segcap);
+        if (!sl->b_dst || !sl->b_src || !sl->b_len || !sl->b_reg) { rc = -ENOMEM; goto fail; }
     }
+    if (pthread_create(&b->progress, NULL, progress_main, b) != 0) { rc = -EAGAIN; goto fail; }
+    b->progress_started = 1;
     *out = b;
+    dev_leave(&g);
     return 0;
 fail:
-    md5hip_batcher_destroy(b);
+    batcher_free(b);
+    dev_leave(&g);
     return rc;
+}
+
+int md5hip_batcher_create(int device, uint64_t slice_bytes, uint32_t nslots, md5hip_batcher **out)
+{
+    /* defaults sized for MD5's serial chains: a slice of B-byte chunks keeps
+     * slice/B lanes busy for B/110 MB/s (one chain), so the bytes in flight
+     * must cover PCIe rate x chain time -- 4 x 128 MiB reaches the H2D rate
+     * for 256 KiB blocks where 3 x 64 MiB stalls at ~34 GB/s (DESIGN.md §5) */
+    if (slice_bytes == 0) slice_bytes = 128ull << 20;
+    uint64_t maxn = slice_bytes / 64 < 4096 ? 4096 : slice_bytes / 64;
+    if (maxn > (1u << 20)) maxn = 1u << 20;      /* descriptors: 32 B per chunk */
+    return batcher_new(device, slice_bytes, nslots, maxn, out);
+}
+
+int md5hip_queue_create(int device, uint64_t max_chunks, uint32_t nslots, md5hip_batcher **out)
+{
+    if (max_chunks == 0) max_chunks = 1u << 20;
+    if (max_chunks > (1ull << 26)) return -EINVAL;
+    /* a small staging slice keeps host-memory submissions possible */
+    return batcher_new(device, 16ull << 20, nslots, max_chunks, out);
+}
+
+/* Wait until nothing is open or in flight (mu held). */
+static void drain(md5hip_batcher *b)
+{
+    for (;;) {
+        if (b->open >= 0) {
+            struct slot *o = &b->s[b->open];
+            o->flush = 1;
+            slot_try_launch(b, o);
+        }
+        int busy = 0;
+        for (uint32_t k = 0; k < b->nslots; k++) busy |= b->s[k].state != SLOT_FREE;
+        if (!busy) return;
+        pthread_cond_wait(&b->done_cv, &b->mu);
+    }
 }
 
 int md5hip_batcher_set_digest(md5hip_batcher *b, int kind, uint32_t fastcrc)
 {
     if (!b) return -EINVAL;
+    uint32_t dsz;
     if (kind == MD5HIP_DIGEST_MD5) {
         if (fastcrc) return -EINVAL;
-        b->dsz = 16;
+        dsz = 16;
     } else if (kind == MD5HIP_DIGEST_CRC32) {
         if (fastcrc & 3u) return -EINVAL;       /* cfs_apix.c:2222-2236 */
-        b->dsz = 4;
+        dsz = 4;
     } else {
         return -EINVAL;
     }
-    for (uint32_t k = 0; k < b->nslots; k++) {  /* never change kind under in-flight work */
-        int rc = 0;
-        struct slot *sl = &b->s[k];
-        if (sl->busy && hipEventSynchronize(sl->done) != hipSuccess) rc = -EIO;
-        if (rc) return rc;
-    }
+    pthread_mutex_lock(&b->mu);
+    drain(b);                                    /* never change kind under queued work */
     b->kind = kind;
     b->fastcrc = fastcrc;
+    b->dsz = dsz;
+    pthread_mutex_unlock(&b->mu);
     return 0;
 }
 
 int md5hip_batcher_get_digest(const md5hip_batcher *b, int *kind, uint32_t *fastcrc)
 {
     if (!b || !kind || !fastcrc) return -EINVAL;
+    pthread_mutex_lock((pthread_mutex_t *)&b->mu);
     *kind = b->kind;
     *fastcrc = b->fastcrc;
+    pthread_mutex_unlock((pthread_mutex_t *)&b->mu);
     return 0;
 }
 
 int md5hip_batcher_set_gather(md5hip_batcher *b, int mode)
 {
     if (!b || mode < MD5HIP_GATHER_HOST || mode > MD5HIP_GATHER_AUTO) return -EINVAL;
+    pthread_mutex_lock(&b->mu);
     b->gather = mode;
+    pthread_mutex_unlock(&b->mu);
     return 0;
 }
 
-/* Enqueue slot `sl` holding `n` chunks, `bytes` packed bytes.  nseg == 0: the
- * bytes are in the pinned staging buffer (one H2D copy); nseg > 0: they are
- * pulled from registered host memory by the gather table (zero-copy modes). */
-static int slot_launch(const md5hip_batcher *b, struct slot *sl, uint64_t n, uint64_t bytes,
-                       uint64_t nseg, uint64_t ndma, unsigned char *user_dig)
+int md5hip_batcher_set_inflight(md5hip_batcher *b, uint32_t target)
 {
-    sl->ticket = b->ticket;
-    int rc;
-    const int dvar = md5hip_plan_desc(sl->h_len, n, sl->h_ord);
-    if (dvar < 0) return -EINVAL;
-    if (hipMemcpyAsync(sl->d_off, sl->h_off, 8 * n, hipMemcpyHostToDevice, sl->stream) ||
-        hipMemcpyAsync(sl->d_len, sl->h_len, 4 * n, hipMemcpyHostToDevice, sl->stream) ||
-        hipMemcpyAsync(sl->d_ord, sl->h_ord, 4 * n, hipMemcpyHostToDevice, sl->stream))
-        return -EIO;
-    int mode = b->gather;
-    if (mode == MD5HIP_GATHER_AUTO)
-        /* measured: per-copy DMA beats the PCIe-reading gather
-         * kernel (~32 GB/s) once copies average more than ~192 KiB */
-        mode = ndma * (256u << 10) <= bytes ? MD5HIP_GATHER_DMA : MD5HIP_GATHER_DEVICE;
-    if (nseg == 0) {
-        if (hipMemcpyAsync(sl->d_data, sl->h_data, bytes, hipMemcpyHostToDevice, sl->stream))
-            return -EIO;
-    } else if (mode == MD5HIP_GATHER_DEVICE) {
-        if (hipMemcpyAsync(sl->d_seg, sl->h_seg, sizeof(struct md5hip_seg) * nseg,
-                           hipMemcpyHostToDevice, sl->stream))
-            return -EIO;
-        if ((rc = md5hip_gather_launch(sl->d_seg, nseg, sl->d_data, sl->stream))) return rc;
-    } else {
-        /* one async copy per segment (hipMemcpyBatchAsync is newer than the
-         * HIP runtime torch ships, which this library shares) */
-        for (uint64_t q = 0; q < ndma; q++)
-            if (hipMemcpyAsync(sl->b_dst[q], sl->b_src[q], sl->b_len[q], hipMemcpyHostToDevice,
-                               sl->stream) != hipSuccess)
-                return -EIO;
-    }
-    if (b->kind == MD5HIP_DIGEST_CRC32)
-        rc = crc32hip_desc(sl->d_data, sl->d_off, sl->d_len, sl->d_ord, n, b->fastcrc,
-                           (uint32_t *)sl->d_dig, sl->stream);
-    else
-        rc = md5hip_digest_desc_variant(sl->d_data, sl->d_off, sl->d_len, sl->d_ord, n, sl->d_dig,
-                                        sl->stream, dvar);
-    if (rc) return rc;
-    if (hipMemcpyAsync(sl->h_dig, sl->d_dig, (size_t)b->dsz * n, hipMemcpyDeviceToHost, sl->stream) ||
-        hipEventRecord(sl->done, sl->stream))
-        return -EIO;
-    sl->busy = 1;
-    sl->user_dig = user_dig;
-    sl->ndig = n;
-    sl->dsz = b->dsz;
+    if (!b || target == 0 || target > b->nslots) return -EINVAL;
+    pthread_mutex_lock(&b->mu);
+    b->target = target;
+    if (b->open >= 0) slot_try_launch(b, &b->s[b->open]);
+    pthread_mutex_unlock(&b->mu);
     return 0;
 }
 
-/* Chunk sources for the generic gather loop: a flat (ptr, len) list or an
- * iovec list with per-chunk segment ranges. */
+int md5hip_batcher_get_stats(md5hip_batcher *b, struct md5hip_batcher_stats *out)
+{
+    if (!b || !out) return -EINVAL;
+    pthread_mutex_lock(&b->mu);
+    *out = b->st;
+    out->inflight_target = b->target;
+    out->nslots = b->nslots;
+    out->max_chunks_per_slot = b->maxn;
+    pthread_mutex_unlock(&b->mu);
+    return 0;
+}
+
+/* ------------------------------------------------------------------------
+ * Chunk sources
+ * ------------------------------------------------------------------------ */
+/* a flat (ptr, len) list, an iovec list with per-chunk segment ranges, or
+ * device addresses (no bytes to move) */
 struct chunk_src {
     const void *const *ptrs;
     const uint32_t *lens;
     const struct md5hip_iov *segs;
     const uint64_t *seg_first;
+    const uint64_t *dptrs;
 };
 
 static uint64_t src_len(const struct chunk_src *s, uint64_t i)
 {
-    if (s->ptrs) return s->lens[i];
+    if (s->ptrs || s->dptrs) return s->lens[i];
     uint64_t L = 0;
     for (uint64_t j = s->seg_first[i]; j < s->seg_first[i + 1]; j++) L += s->segs[j].len;
     return L;
@@ -382,13 +791,11 @@ static void src_copy(const struct chunk_src *s, uint64_t i, unsigned char *dst)
     }
 }
 
-/* Host gather of one slice: chunks [first, first + m) into the pinned
- * staging at sl->h_off[].  One thread's memcpy from pageable memory into
- * pinned staging runs ~15 GB/s (zero-copy table), well below
- * the PCIe H2D rate, so a large slice is cut by bytes into parts copied by
- * MD5HIP_GATHER_THREADS threads (default 4; the calling thread copies the
- * first part).  Threads are started per slice: a slice worth splitting
- * (>= 8 MiB) takes milliseconds to copy, a pthread_create microseconds. */
+/* Host gather of chunks [first, first + m) to dst + off[j].  One thread's
+ * memcpy from pageable memory into pinned staging runs ~15 GB/s (DESIGN.md
+ * §5), well below PCIe, so a large range is cut by bytes into parts copied
+ * by MD5HIP_GATHER_THREADS threads (default 4; the calling thread copies the
+ * first part). */
 struct gather_part {
     const struct chunk_src *src;
     uint64_t first, jlo, jhi;
@@ -415,23 +822,24 @@ static void gather_threads_init(void)
     }
 }
 
-#define GATHER_SPLIT_MIN (8ull << 20)   /* bytes per slice before it is split */
+#define GATHER_SPLIT_MIN (8ull << 20)   /* bytes per range before it is split */
 #define GATHER_PART_MIN (2ull << 20)    /* and at least this many bytes per part */
 
-static void gather_slice(const struct chunk_src *src, uint64_t first, uint64_t m,
-                         const uint64_t *off, unsigned char *dst, uint64_t used)
+static void gather_range(const struct chunk_src *src, uint64_t first, uint64_t m,
+                         const uint64_t *off, unsigned char *dst, uint64_t lo, uint64_t used)
 {
     pthread_once(&g_gather_once, gather_threads_init);
+    const uint64_t bytes = used - lo;
     uint64_t T = (uint64_t)g_gather_threads;
-    if (used < GATHER_SPLIT_MIN) T = 1;
-    if (T > used / GATHER_PART_MIN) T = used / GATHER_PART_MIN ? used / GATHER_PART_MIN : 1;
+    if (bytes < GATHER_SPLIT_MIN) T = 1;
+    if (T > bytes / GATHER_PART_MIN) T = bytes / GATHER_PART_MIN ? bytes / GATHER_PART_MIN : 1;
     if (T > m) T = m ? m : 1;
     struct gather_part part[32];
     pthread_t tid[32];
     int started[32] = {0};
     uint64_t j = 0;
-    for (uint64_t t = 0; t < T; t++) {      /* part t: chunks whose offset < (t+1) * used / T */
-        const uint64_t lim = t + 1 == T ? UINT64_MAX : (t + 1) * used / T;
+    for (uint64_t t = 0; t < T; t++) {      /* part t: chunks whose offset < lo + (t+1) * bytes / T */
+        const uint64_t lim = t + 1 == T ? UINT64_MAX : lo + (t + 1) * bytes / T;
         part[t] = (struct gather_part){src, first, j, j, off, dst};
         while (j < m && off[j] < lim) j++;
         part[t].jhi = j;
@@ -445,115 +853,241 @@ static void gather_slice(const struct chunk_src *src, uint64_t first, uint64_t m
     }
 }
 
-/* async == 0: returns once every digest is in `digests`.  async != 0:
- * returns once the host gather is done (the caller's buffers are free again,
- * except in the zero-copy modes); *ticket names the submission for
- * md5_batch_wait / md5_batch_poll, which deliver its digests. */
-static int submit_gather(md5hip_batcher *b, const struct chunk_src *src, uint64_t n,
-                         unsigned char *digests, int async, uint64_t *ticket)
+/* ------------------------------------------------------------------------
+ * Submission
+ * ------------------------------------------------------------------------ */
+/* Reserve chunks [i, n) of `src` into the open slot (mu held): descriptors,
+ * staging offsets, zero-copy tables.  Returns the number reserved (the slot
+ * is marked full when a chunk did not fit) or -errno. */
+static long reserve(md5hip_batcher *b, struct slot *sl, const struct chunk_src *src, uint64_t i,
+                    uint64_t n, int zc)
 {
-    for (uint64_t i = 0; i < n; i++) {
-        const uint64_t L = src_len(src, i);
-        if (L > 0xffffffffull) return -E2BIG;
-        if ((L + 15) / 16 * 16 > b->cap) return -E2BIG;
-    }
-    if (hipSetDevice(b->device) != hipSuccess) return -ENODEV;
-    int zc = b->gather != MD5HIP_GATHER_HOST && src_registered(src, n);
-    if (zc)
-        for (uint64_t i = 0; i < n; i++)
-            if (src_nseg(src, i) > b->segcap) zc = 0;   /* a chunk too fragmented for one table */
-    const int dev = b->device < REG_MAXDEV ? b->device : 0;
-    int rc = 0;
-    uint32_t k = b->next;
-    uint64_t i = 0;
-    const uint64_t t = ++b->ticket;
-    if (ticket) *ticket = t;
-    while (i < n) {
-        struct slot *sl = &b->s[k];
-        if ((rc = slot_retire(sl))) return rc;
-        uint64_t used = 0, m = 0, first = i, nseg = 0, ndma = 0;
-        if (zc) pthread_rwlock_rdlock(&g_reg_lock);
-        while (i < n && m < b->maxn) {
-            const uint64_t L = src_len(src, i);
-            const uint64_t sz = (L + 15) & ~15ull;   /* 16-B aligned packing */
-            if (used + sz > b->cap) break;
+    const int dev = b->device;
+    uint64_t j = i;
+    if (zc) pthread_rwlock_rdlock(&g_reg_lock);
+    while (j < n && sl->n < b->maxn) {
+        const uint64_t L = src_len(src, j);
+        if (src->dptrs) {                                      /* device-resident: no bytes */
+            sl->h_off[sl->n] = src->dptrs[j] - (uint64_t)(uintptr_t)sl->d_data;
+        } else {
+            const uint64_t sz = (L + 15) & ~15ull;             /* 16-B aligned packing */
+            if (sl->used + sz > b->cap) break;
             if (zc) {
-                const uint64_t ns = src_nseg(src, i);
-                if (nseg + ns > b->segcap) break;
-                uint64_t at = used;
+                const uint64_t ns = src_nseg(src, j);
+                if (sl->nseg + ns > b->segcap || sl->ndma + ns > b->segcap) break;
+                uint64_t at = sl->used;
                 for (uint64_t q = 0; q < ns; q++) {
                     const void *p;
                     uint32_t len;
-                    src_seg(src, i, q, &p, &len);
+                    src_seg(src, j, q, &p, &len);
                     if (!len) continue;
                     const long r = reg_find((uintptr_t)p, len);
+                    if (r < 0) {                               /* unregistered under us */
+                        pthread_rwlock_unlock(&g_reg_lock);
+                        return -EFAULT;
+                    }
                     const uint64_t dsrc = (uint64_t)((uintptr_t)p + g_reg[r].delta[dev]);
                     /* device table: contiguous pieces merged up to 64 KiB, so
                      * a slice keeps >= ~1000 workgroups of gather work */
-                    struct md5hip_seg *prev = nseg ? &sl->h_seg[nseg - 1] : NULL;
+                    struct md5hip_seg *prev = sl->nseg ? &sl->h_seg[sl->nseg - 1] : NULL;
                     if (prev && prev->src + prev->len == dsrc && prev->dst + prev->len == at &&
                         (uint64_t)prev->len + len <= (64u << 10)) {
                         prev->len += len;
                     } else {
-                        sl->h_seg[nseg++] = (struct md5hip_seg){dsrc, at, len, 0};
+                        sl->h_seg[sl->nseg++] = (struct md5hip_seg){dsrc, at, len, 0};
                     }
-                    /* DMA list: merged without limit (a copy has a fixed cost) */
-                    if (ndma && (const unsigned char *)sl->b_src[ndma - 1] + sl->b_len[ndma - 1] ==
-                                    (const unsigned char *)p &&
-                        sl->b_dst[ndma - 1] == sl->d_data + at - sl->b_len[ndma - 1]) {
-                        sl->b_len[ndma - 1] += len;
+                    /* DMA list: merged without limit (a copy has a fixed cost),
+                     * but only within one registered range (one pinned allocation) */
+                    const uint64_t q1 = sl->ndma;
+                    if (q1 && sl->b_reg[q1 - 1] == r &&
+                        (const unsigned char *)sl->b_src[q1 - 1] + sl->b_len[q1 - 1] ==
+                            (const unsigned char *)p &&
+                        (unsigned char *)sl->b_dst[q1 - 1] + sl->b_len[q1 - 1] == sl->d_data + at) {
+                        sl->b_len[q1 - 1] += len;
                     } else {
-                        sl->b_dst[ndma] = sl->d_data + at;
-                        sl->b_src[ndma] = (void *)p;
-                        sl->b_len[ndma] = len;
-                        ndma++;
+                        sl->b_dst[q1] = sl->d_data + at;
+                        sl->b_src[q1] = (void *)p;
+                        sl->b_len[q1] = len;
+                        sl->b_reg[q1] = r;
+                        sl->ndma++;
                     }
                     at += len;
                 }
             }
-            sl->h_off[m] = used;
-            sl->h_len[m] = (uint32_t)L;
-            used += sz;
-            m++;
-            i++;
+            sl->h_off[sl->n] = sl->used;
+            sl->used += sz;
         }
-        if (zc) pthread_rwlock_unlock(&g_reg_lock);
-        else gather_slice(src, first, m, sl->h_off, sl->h_data, used);
-        if ((rc = slot_launch(b, sl, m, used ? used : 16, zc ? nseg : 0, ndma,
-                              digests + (size_t)b->dsz * first)))
-            return rc;
-        k = (k + 1) % b->nslots;
-        b->next = k;
+        sl->h_len[sl->n] = (uint32_t)L;
+        sl->n++;
+        j++;
     }
-    return async ? 0 : md5_batch_wait(b, t);
+    if (zc) pthread_rwlock_unlock(&g_reg_lock);
+    if (j < n) sl->full = 1;
+    return (long)(j - i);
+}
+
+/* The submission engine.  kind < 0: the batcher's current digest kind;
+ * else this submission's own (it never changes the batcher's setting). */
+static int submit(md5hip_batcher *b, const struct chunk_src *src, uint64_t n, unsigned char *digests,
+                  int on_device, int async, uint64_t *ticket, int kind, uint32_t fastcrc)
+{
+    for (uint64_t i = 0; i < n; i++) {
+        const uint64_t L = src_len(src, i);
+        if (L > 0xffffffffull) return -E2BIG;
+        if (!src->dptrs && (L + 15) / 16 * 16 > b->cap) return -E2BIG;
+    }
+    struct dev_guard g;
+    if (dev_enter(&g, b->device)) return -ENODEV;
+    int zc = 0;
+    if (!src->dptrs && b->gather != MD5HIP_GATHER_HOST && b->device < REG_MAXDEV &&
+        src_registered(src, n)) {
+        zc = 1;
+        for (uint64_t i = 0; i < n; i++)
+            if (src_nseg(src, i) > b->segcap) zc = 0;   /* a chunk too fragmented for one table */
+    }
+    const int mode = src->dptrs ? MODE_NONE : zc ? MODE_ZEROCOPY : MODE_STAGED;
+    pthread_mutex_lock(&b->mu);
+    int rc = 0;
+    uint64_t t = 0;
+    if (kind < 0) {
+        kind = b->kind;
+        fastcrc = b->fastcrc;
+    }
+    rc = tk_new(b, &t);
+    if (rc) {
+        pthread_mutex_unlock(&b->mu);
+        dev_leave(&g);
+        return rc;
+    }
+    b->st.submissions++;
+    const uint32_t dsz = kind == MD5HIP_DIGEST_CRC32 ? 4 : 16;
+    uint64_t i = 0;
+    while (i < n) {
+        struct slot *sl = slot_open(b, mode, kind, fastcrc);
+        const uint64_t at = sl->n;
+        const uint64_t lo = sl->used;
+        const long got = reserve(b, sl, src, i, n, zc);
+        if (got < 0) { rc = (int)got; break; }
+        if (got == 0) {                      /* nothing fit: close it and take a fresh one */
+            sl->full = 1;
+            b->open = -1;
+            slot_try_launch(b, sl);
+            continue;
+        }
+        const uint64_t m = (uint64_t)got;
+        const uint64_t hi = sl->used;
+        if ((rc = seg_push(sl, (struct seg){t, at, m, digests + (size_t)dsz * i, on_device}))) {
+            sl->err = rc;                    /* its reserved chunks have no segment */
+            break;
+        }
+        b->tk_pending[t & (b->tkcap - 1)]++;
+        if (mode == MODE_STAGED && hi > lo) {
+            /* copy outside the lock: other submitters may reserve behind us */
+            sl->writers++;
+            pthread_mutex_unlock(&b->mu);
+            gather_range(src, i, m, sl->h_off + at, sl->h_data, lo, hi);
+            pthread_mutex_lock(&b->mu);
+            sl->writers--;
+        }
+        i += m;
+        if (!async && i >= n) sl->flush = 1;  /* the caller waits right away */
+        slot_try_launch(b, sl);
+    }
+    tk_put(b, t, rc);                        /* the submission's own reference */
+    if (ticket) *ticket = t;
+    if (!async || rc) {
+        int err = 0;
+        while (!tk_done(b, t, &err)) {
+            for (uint32_t k = 0; k < b->nslots; k++)
+                if (b->s[k].state == SLOT_OPEN && seg_has(&b->s[k], t)) {
+                    b->s[k].flush = 1;
+                    slot_try_launch(b, &b->s[k]);
+                }
+            pthread_cond_wait(&b->done_cv, &b->mu);
+        }
+        if (!rc) rc = err;
+    }
+    pthread_mutex_unlock(&b->mu);
+    dev_leave(&g);
+    return rc;
 }
 
 int md5_batch_wait(md5hip_batcher *b, uint64_t ticket)
 {
     if (!b) return -EINVAL;
-    int rc = 0;
-    for (uint32_t j = 0; j < b->nslots; j++) {
-        struct slot *sl = &b->s[j];
-        if (sl->busy && sl->ticket <= ticket) {
-            const int r = slot_retire(sl);
-            if (r && !rc) rc = r;
+    if (ticket == 0) return 0;               /* "nothing submitted" */
+    pthread_mutex_lock(&b->mu);
+    int rc = 0, err = 0;
+    if (ticket >= b->tk_hi) {
+        rc = -EINVAL;
+    } else {
+        while (!tk_done(b, ticket, &err)) {
+            for (uint32_t k = 0; k < b->nslots; k++)
+                if (b->s[k].state == SLOT_OPEN && seg_has(&b->s[k], ticket)) {
+                    b->s[k].flush = 1;
+                    slot_try_launch(b, &b->s[k]);
+                }
+            pthread_cond_wait(&b->done_cv, &b->mu);
         }
+        rc = err;
     }
+    pthread_mutex_unlock(&b->mu);
     return rc;
 }
 
 int md5_batch_poll(md5hip_batcher *b, uint64_t ticket)
 {
     if (!b) return -EINVAL;
-    for (uint32_t j = 0; j < b->nslots; j++) {
-        const struct slot *sl = &b->s[j];
-        if (!sl->busy || sl->ticket > ticket) continue;
-        const hipError_t e = hipEventQuery(sl->done);
-        if (e == hipErrorNotReady) return 0;
-        if (e != hipSuccess) return -EIO;
+    if (ticket == 0) return 1;
+    pthread_mutex_lock(&b->mu);
+    int rc, err = 0;
+    if (ticket >= b->tk_hi) {
+        rc = -EINVAL;
+    } else if (tk_done(b, ticket, &err)) {
+        rc = err ? err : 1;
+    } else {
+        /* it must make progress without the caller blocking: launch its open slot */
+        for (uint32_t k = 0; k < b->nslots; k++)
+            if (b->s[k].state == SLOT_OPEN && seg_has(&b->s[k], ticket)) {
+                b->s[k].flush = 1;
+                slot_try_launch(b, &b->s[k]);
+            }
+        rc = 0;
     }
-    const int rc = md5_batch_wait(b, ticket);    /* all complete: deliver, no blocking */
-    return rc ? rc : 1;
+    pthread_mutex_unlock(&b->mu);
+    return rc;
+}
+
+int md5_batch_flush(md5hip_batcher *b)
+{
+    if (!b) return -EINVAL;
+    pthread_mutex_lock(&b->mu);
+    if (b->open >= 0) {
+        struct slot *o = &b->s[b->open];
+        o->flush = 1;
+        slot_try_launch(b, o);
+    }
+    pthread_mutex_unlock(&b->mu);
+    return 0;
+}
+
+static int check_ptrs(const void *const *ptrs, const uint32_t *lens, uint64_t n)
+{
+    if (!ptrs || !lens) return -EINVAL;
+    for (uint64_t i = 0; i < n; i++)
+        if (!ptrs[i] && lens[i]) return -EINVAL;
+    return 0;
+}
+
+static int check_iov(const struct md5hip_iov *segs, const uint64_t *seg_first, uint64_t n)
+{
+    if (!segs || !seg_first || seg_first[0] != 0) return -EINVAL;
+    for (uint64_t i = 0; i < n; i++) {
+        if (seg_first[i + 1] < seg_first[i]) return -EINVAL;
+        for (uint64_t j = seg_first[i]; j < seg_first[i + 1]; j++)
+            if (!segs[j].base && segs[j].len) return -EINVAL;
+    }
+    return 0;
 }
 
 int md5_batch_submit(md5hip_batcher *b, const void *const *ptrs, const uint32_t *lens, uint64_t n,
@@ -561,24 +1095,24 @@ int md5_batch_submit(md5hip_batcher *b, const void *const *ptrs, const uint32_t 
 {
     if (!b) return -EINVAL;
     if (n == 0) return 0;
-    if (!ptrs || !lens || !digests) return -EINVAL;
-    for (uint64_t i = 0; i < n; i++)
-        if (!ptrs[i] && lens[i]) return -EINVAL;
-    const struct chunk_src src = {ptrs, lens, NULL, NULL};
-    return submit_gather(b, &src, n, digests, 0, NULL);
+    if (!digests) return -EINVAL;
+    int rc = check_ptrs(ptrs, lens, n);
+    if (rc) return rc;
+    const struct chunk_src src = {ptrs, lens, NULL, NULL, NULL};
+    return submit(b, &src, n, digests, 0, 0, NULL, -1, 0);
 }
 
 int md5_batch_submit_async(md5hip_batcher *b, const void *const *ptrs, const uint32_t *lens,
                            uint64_t n, unsigned char *digests, uint64_t *ticket)
 {
     if (!b || !ticket) return -EINVAL;
-    *ticket = b->ticket;                   /* an empty batch is complete at once */
+    *ticket = 0;                           /* an empty batch is complete at once */
     if (n == 0) return 0;
-    if (!ptrs || !lens || !digests) return -EINVAL;
-    for (uint64_t i = 0; i < n; i++)
-        if (!ptrs[i] && lens[i]) return -EINVAL;
-    const struct chunk_src src = {ptrs, lens, NULL, NULL};
-    return submit_gather(b, &src, n, digests, 1, ticket);
+    if (!digests) return -EINVAL;
+    int rc = check_ptrs(ptrs, lens, n);
+    if (rc) return rc;
+    const struct chunk_src src = {ptrs, lens, NULL, NULL, NULL};
+    return submit(b, &src, n, digests, 0, 1, ticket, -1, 0);
 }
 
 int md5_batch_submit_iov(md5hip_batcher *b, const struct md5hip_iov *segs,
@@ -586,14 +1120,11 @@ int md5_batch_submit_iov(md5hip_batcher *b, const struct md5hip_iov *segs,
 {
     if (!b) return -EINVAL;
     if (n == 0) return 0;
-    if (!segs || !seg_first || !digests || seg_first[0] != 0) return -EINVAL;
-    for (uint64_t i = 0; i < n; i++) {
-        if (seg_first[i + 1] < seg_first[i]) return -EINVAL;
-        for (uint64_t j = seg_first[i]; j < seg_first[i + 1]; j++)
-            if (!segs[j].base && segs[j].len) return -EINVAL;
-    }
-    const struct chunk_src src = {NULL, NULL, segs, seg_first};
-    return submit_gather(b, &src, n, digests, 0, NULL);
+    if (!digests) return -EINVAL;
+    int rc = check_iov(segs, seg_first, n);
+    if (rc) return rc;
+    const struct chunk_src src = {NULL, NULL, segs, seg_first, NULL};
+    return submit(b, &src, n, digests, 0, 0, NULL, -1, 0);
 }
 
 int md5_batch_submit_iov_async(md5hip_batcher *b, const struct md5hip_iov *segs,
@@ -601,16 +1132,39 @@ int md5_batch_submit_iov_async(md5hip_batcher *b, const struct md5hip_iov *segs,
                                uint64_t *ticket)
 {
     if (!b || !ticket) return -EINVAL;
-    *ticket = b->ticket;
+    *ticket = 0;
     if (n == 0) return 0;
-    if (!segs || !seg_first || !digests || seg_first[0] != 0) return -EINVAL;
-    for (uint64_t i = 0; i < n; i++) {
-        if (seg_first[i + 1] < seg_first[i]) return -EINVAL;
-        for (uint64_t j = seg_first[i]; j < seg_first[i + 1]; j++)
-            if (!segs[j].base && segs[j].len) return -EINVAL;
-    }
-    const struct chunk_src src = {NULL, NULL, segs, seg_first};
-    return submit_gather(b, &src, n, digests, 1, ticket);
+    if (!digests) return -EINVAL;
+    int rc = check_iov(segs, seg_first, n);
+    if (rc) return rc;
+    const struct chunk_src src = {NULL, NULL, segs, seg_first, NULL};
+    return submit(b, &src, n, digests, 0, 1, ticket, -1, 0);
+}
+
+int md5_batch_submit_device_async(md5hip_batcher *b, const uint64_t *d_ptrs, const uint32_t *lens,
+                                  uint64_t n, unsigned char *digests, int digests_on_device,
+                                  uint64_t *ticket)
+{
+    if (!b || !ticket) return -EINVAL;
+    *ticket = 0;
+    if (n == 0) return 0;
+    if (!d_ptrs || !lens || !digests) return -EINVAL;
+    for (uint64_t i = 0; i < n; i++)
+        if (!d_ptrs[i] && lens[i]) return -EINVAL;
+    const struct chunk_src src = {NULL, lens, NULL, NULL, d_ptrs};
+    return submit(b, &src, n, digests, digests_on_device != 0, 1, ticket, -1, 0);
+}
+
+int md5_batch_submit_device(md5hip_batcher *b, const uint64_t *d_ptrs, const uint32_t *lens,
+                            uint64_t n, unsigned char *digests, int digests_on_device)
+{
+    if (!b) return -EINVAL;
+    if (n == 0) return 0;
+    if (!d_ptrs || !lens || !digests) return -EINVAL;
+    for (uint64_t i = 0; i < n; i++)
+        if (!d_ptrs[i] && lens[i]) return -EINVAL;
+    const struct chunk_src src = {NULL, lens, NULL, NULL, d_ptrs};
+    return submit(b, &src, n, digests, digests_on_device != 0, 0, NULL, -1, 0);
 }
 
 int md5hip_batch_host_fixed(md5hip_batcher *b, const void *h_base, uint64_t n, uint32_t len,
@@ -620,63 +1174,88 @@ int md5hip_batch_host_fixed(md5hip_batcher *b, const void *h_base, uint64_t n, u
     if (n == 0) return 0;
     if (!h_base || !digests || len > stride) return -EINVAL;
     if (stride > b->cap) return -E2BIG;
-    if (hipSetDevice(b->device) != hipSuccess) return -ENODEV;
+    struct dev_guard g;
+    if (dev_enter(&g, b->device)) return -ENODEV;
     const unsigned char *src = (const unsigned char *)h_base;
     uint64_t per = b->cap / stride;
     if (per > b->maxn) per = b->maxn;
-    int rc = 0;
-    uint32_t k = b->next;
-    const uint64_t t = ++b->ticket;
-    for (uint64_t i = 0; i < n; i += per) {
-        const uint64_t m = n - i < per ? n - i : per;
-        struct slot *sl = &b->s[k];
-        if ((rc = slot_retire(sl))) return rc;
-        const uint64_t bytes = (m - 1) * stride + len;
-        /* straight from the caller's (ideally pinned) buffer: no host gather */
-        if (hipMemcpyAsync(sl->d_data, src + i * stride, bytes, hipMemcpyHostToDevice, sl->stream))
-            return -EIO;
-        if (b->kind == MD5HIP_DIGEST_CRC32)
-            rc = crc32hip_fixed(sl->d_data, m, len, stride, b->fastcrc, (uint32_t *)sl->d_dig,
-                                sl->stream);
-        else
-            rc = md5hip_digest_fixed(sl->d_data, m, len, stride, sl->d_dig, sl->stream);
-        if (rc) return rc;
-        if (hipMemcpyAsync(sl->h_dig, sl->d_dig, (size_t)b->dsz * m, hipMemcpyDeviceToHost, sl->stream) ||
-            hipEventRecord(sl->done, sl->stream))
-            return -EIO;
-        sl->busy = 1;
-        sl->user_dig = digests + (size_t)b->dsz * i;
-        sl->ticket = t;
-        sl->ndig = m;
-        sl->dsz = b->dsz;
-        k = (k + 1) % b->nslots;
-        b->next = k;
+    pthread_mutex_lock(&b->mu);
+    uint64_t t = 0;
+    int rc = tk_new(b, &t);
+    if (rc) {
+        pthread_mutex_unlock(&b->mu);
+        dev_leave(&g);
+        return rc;
     }
-    return md5_batch_wait(b, t);
+    b->st.submissions++;
+    for (uint64_t i = 0; i < n && !rc; i += per) {
+        const uint64_t m = n - i < per ? n - i : per;
+        /* straight from the caller's (ideally pinned) buffer: no host gather,
+         * a slot of its own (the open slot keeps coalescing other work) */
+        struct slot *sl = slot_take(b, MODE_FIXED, b->kind, b->fastcrc);
+        sl->n = m;
+        sl->fx_src = src + i * stride;
+        sl->fx_bytes = (m - 1) * stride + len;
+        sl->fx_len = len;
+        sl->fx_stride = stride;
+        sl->full = 1;
+        if ((rc = seg_push(sl, (struct seg){t, 0, m, digests + (size_t)b->dsz * i, 0}))) {
+            slot_retire(b, sl, rc);
+            break;
+        }
+        b->tk_pending[t & (b->tkcap - 1)]++;
+        slot_try_launch(b, sl);
+    }
+    tk_put(b, t, rc);
+    int err = 0;
+    while (!tk_done(b, t, &err)) pthread_cond_wait(&b->done_cv, &b->mu);
+    if (!rc) rc = err;
+    pthread_mutex_unlock(&b->mu);
+    dev_leave(&g);
+    return rc;
 }
 
 /* Batched verify for the cache-read / write-verify sites (blk_io.c:665-704,
  * bc_mgr.c:1464-1492): ok[i] = digest(chunk i) == expected[i]; returns the
  * number of mismatching chunks (>= 0) or -errno.  A mismatch is what
  * dm_verify_block_crc (diskcache.c:3245-3265) reports per block; the caller
- * applies its own EAGAIN / inode-reset policy per flagged block. */
-int md5hip_batch_verify_iov(md5hip_batcher *b, const struct md5hip_iov *segs,
-                            const uint64_t *seg_first, uint64_t n, const void *expected,
-                            unsigned char *ok)
+ * applies its own EAGAIN / inode-reset policy per flagged block.
+ * md5hip_verify_iov_as: with an explicit digest kind for this call only (the
+ * batcher's setting is untouched, so concurrent users are unaffected). */
+int md5hip_verify_iov_as(md5hip_batcher *b, int kind, uint32_t fastcrc,
+                         const struct md5hip_iov *segs, const uint64_t *seg_first, uint64_t n,
+                         const void *expected, unsigned char *ok)
 {
     if (!b) return -EINVAL;
     if (n == 0) return 0;
     if (!expected || !ok) return -EINVAL;
-    unsigned char *got = malloc((size_t)b->dsz * n);
+    if (kind != MD5HIP_DIGEST_MD5 && kind != MD5HIP_DIGEST_CRC32) return -EINVAL;
+    if (kind == MD5HIP_DIGEST_MD5 ? fastcrc != 0 : (fastcrc & 3u) != 0) return -EINVAL;
+    int rc = check_iov(segs, seg_first, n);
+    if (rc) return rc;
+    const uint32_t dsz = kind == MD5HIP_DIGEST_CRC32 ? 4 : 16;
+    unsigned char *got = malloc((size_t)dsz * n);
     if (!got) return -ENOMEM;
-    int rc = md5_batch_submit_iov(b, segs, seg_first, n, got);
+    const struct chunk_src src = {NULL, NULL, segs, seg_first, NULL};
+    rc = submit(b, &src, n, got, 0, 0, NULL, kind, fastcrc);
     if (rc == 0) {
         const unsigned char *e = (const unsigned char *)expected;
         for (uint64_t i = 0; i < n; i++) {
-            ok[i] = memcmp(got + (size_t)b->dsz * i, e + (size_t)b->dsz * i, b->dsz) == 0;
+            ok[i] = memcmp(got + (size_t)dsz * i, e + (size_t)dsz * i, dsz) == 0;
             rc += !ok[i];
         }
     }
     free(got);
     return rc;
+}
+
+int md5hip_batch_verify_iov(md5hip_batcher *b, const struct md5hip_iov *segs,
+                            const uint64_t *seg_first, uint64_t n, const void *expected,
+                            unsigned char *ok)
+{
+    if (!b) return -EINVAL;
+    int kind;
+    uint32_t fastcrc;
+    md5hip_batcher_get_digest(b, &kind, &fastcrc);
+    return md5hip_verify_iov_as(b, kind, fastcrc, segs, seg_first, n, expected, ok);
 }

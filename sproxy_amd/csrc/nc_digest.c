@@ -9,6 +9,8 @@
 #include <string.h>
 
 #include "../../include/nc_digest.h"
+#include "../../include/md5hip.h"
+#include "md5_internal.h"
 
 uint64_t nc_canned_digest_size(uint32_t bitmaplen, uint32_t dsz)
 {
@@ -166,10 +168,7 @@ int md5hip_batch_verify_headers(md5hip_batcher *b, const void *const *headers, u
     if (!b) return -EINVAL;
     if (n == 0) return 0;
     if (!headers || !ok) return -EINVAL;
-    int kind;
-    uint32_t fastcrc;
-    int rc = md5hip_batcher_get_digest(b, &kind, &fastcrc);
-    if (rc) return rc;
+    int rc = 0;
     struct md5hip_iov *segs = malloc(sizeof *segs * 5 * n);
     uint64_t *first = malloc(sizeof *first * (n + 1));
     uint32_t *want = malloc(4 * n);
@@ -191,11 +190,10 @@ int md5hip_batch_verify_headers(md5hip_batcher *b, const void *const *headers, u
         }
         first[i + 1] = s;
     }
-    if ((rc = md5hip_batcher_set_digest(b, MD5HIP_DIGEST_CRC32, 0))) goto out;
-    rc = md5hip_batch_verify_iov(b, segs, first, n, want, got);
-    int rc2 = md5hip_batcher_set_digest(b, kind, fastcrc);
+    /* CRC-32 for this call only: the batcher's own digest kind (it may be
+     * shared with ASIO threads hashing blocks) is left alone */
+    rc = md5hip_verify_iov_as(b, MD5HIP_DIGEST_CRC32, 0, segs, first, n, want, got);
     if (rc < 0) goto out;
-    if (rc2) { rc = rc2; goto out; }
     rc = 0;
     for (uint64_t i = 0; i < n; i++) {
         ok[i] = got[i] && hdr_plausible(headers[i]);

@@ -19,7 +19,7 @@ import ctypes
 
 import numpy as np
 
-from ._lib import MD5Context, MD5HipError, MD5HipIov, check, lib
+from ._lib import MD5Context, MD5HipBatcherStats, MD5HipError, MD5HipIov, check, lib
 
 try:
     import torch
@@ -282,7 +282,8 @@ def resolve_variant(v=AUTO) -> int:
 
 # ---------------------------------------------------------------- host batches
 class Batcher:
-    """Host-memory batched submit (include/md5hip.h md5hip_batcher_*)."""
+    """The batcher (include/md5hip.h md5hip_batcher_*): a thread-safe,
+    coalescing submission queue; tickets complete out of order."""
 
     MD5, CRC32 = 0, 1
     GATHER_HOST, GATHER_DEVICE, GATHER_DMA, GATHER_AUTO = 0, 1, 2, 3
@@ -291,7 +292,10 @@ class Batcher:
                submit="md5_batch_submit", submit_iov="md5_batch_submit_iov",
                verify_iov="md5hip_batch_verify_iov", host_fixed="md5hip_batch_host_fixed",
                submit_async="md5_batch_submit_async", submit_iov_async="md5_batch_submit_iov_async",
-               wait="md5_batch_wait", poll="md5_batch_poll")
+               wait="md5_batch_wait", poll="md5_batch_poll", flush="md5_batch_flush",
+               submit_device_async="md5_batch_submit_device_async",
+               submit_device="md5_batch_submit_device", set_inflight="md5hip_batcher_set_inflight",
+               stats="md5hip_batcher_get_stats")
 
     def __init__(self, device: int = 0, slice_bytes: int = 0, nslots: int = 0,
                  kind: int = 0, fastcrc: int = 0):
@@ -383,8 +387,9 @@ class Batcher:
         """An asynchronous submission: `ticket`, the output array, and the
         input references the device may still read (zero-copy modes)."""
 
-        def __init__(self, batcher, ticket, out, n, keep):
+        def __init__(self, batcher, ticket, out, n, keep, on_device=False):
             self.batcher, self.ticket, self._out, self.n, self._keep = batcher, ticket, out, n, keep
+            self.on_device = on_device
 
         def poll(self) -> bool:
             name, rc = self.batcher._call("poll", ctypes.c_uint64(self.ticket))
@@ -392,10 +397,10 @@ class Batcher:
                 check(name, rc)
             return rc == 1
 
-        def wait(self) -> np.ndarray:
+        def wait(self):
             check(*self.batcher._call("wait", ctypes.c_uint64(self.ticket)))
             self._keep = None
-            return self.batcher._ret(self._out, self.n)
+            return self._out if self.on_device else self.batcher._ret(self._out, self.n)
 
     def submit_async(self, buffers) -> "Batcher.Pending":
         """md5_batch_submit_async: returns once the chunks are staged; the
@@ -422,6 +427,49 @@ class Batcher:
                           ctypes.byref(t)))
         return Batcher.Pending(self, t.value, out, n, (keep, arr, fa))
 
+    @staticmethod
+    def _dev_args(ptrs, lens, out):
+        P = np.ascontiguousarray(ptrs, dtype=np.uint64)
+        L = np.ascontiguousarray(lens, dtype=np.uint32)
+        if P.size != L.size:
+            raise ValueError("ptrs and lens differ in length")
+        if torch is not None and isinstance(out, torch.Tensor):
+            if not out.is_cuda or not out.is_contiguous() or out.numel() * out.element_size() < P.size * 16:
+                raise ValueError("out must be a contiguous device tensor of >= n x 16 bytes")
+            return P, L, out.data_ptr(), 1
+        if out is None:
+            out = np.empty((max(P.size, 1), 16), dtype=np.uint8)
+        return P, L, out, 0
+
+    def submit_device_async(self, ptrs, lens, out=None) -> "Batcher.Pending":
+        """md5_batch_submit_device_async: chunk i = (device address ptrs[i],
+        lens[i]); digests into `out` -- a device tensor (digests stay on the
+        device) or, by default, a host array returned by .wait()."""
+        P, L, o, on_dev = self._dev_args(ptrs, lens, out)
+        t = ctypes.c_uint64()
+        dst = o if on_dev else o.ctypes.data
+        check(*self._call("submit_device_async", P.ctypes.data, L.ctypes.data, P.size, dst, on_dev,
+                          ctypes.byref(t)))
+        return Batcher.Pending(self, t.value, out if on_dev else o, P.size, (P, L, out), on_dev)
+
+    def submit_device(self, ptrs, lens, out=None):
+        P, L, o, on_dev = self._dev_args(ptrs, lens, out)
+        dst = o if on_dev else o.ctypes.data
+        check(*self._call("submit_device", P.ctypes.data, L.ctypes.data, P.size, dst, on_dev))
+        return out if on_dev else self._ret(o, P.size)
+
+    def flush(self):
+        check(*self._call("flush"))
+
+    def set_inflight(self, target: int):
+        """Launch the open slot at once while fewer than `target` slots run."""
+        check(*self._call("set_inflight", target))
+
+    def stats(self) -> dict:
+        st = MD5HipBatcherStats()
+        check(*self._call("stats", ctypes.byref(st)))
+        return {n: int(getattr(st, n)) for n, _ in MD5HipBatcherStats._fields_}
+
     def verify_iov(self, chunks, expected):
         """(ok[i] bool array, mismatch count): digest(chunks[i]) == expected[i]."""
         arr, fa, keep = self._iov(chunks)
@@ -444,6 +492,23 @@ class Batcher:
         out = self._out(n)
         check(*self._call("host_fixed", a.ctypes.data, n, length, stride, out.ctypes.data))
         return self._ret(out, n)
+
+
+class Queue(Batcher):
+    """A batcher sized for device-resident chunks (md5hip_queue_create):
+    `max_chunks` descriptors per launch, small host staging."""
+
+    def __init__(self, device: int = 0, max_chunks: int = 0, nslots: int = 0, inflight: int = 0):
+        h = ctypes.c_void_p()
+        check("md5hip_queue_create", lib().md5hip_queue_create(device, max_chunks, nslots,
+                                                                ctypes.byref(h)))
+        self._h = h
+        self.kind, self.dsz = self.MD5, 16
+        if inflight:
+            self.set_inflight(inflight)
+
+    def submit(self, *a, **k):           # host-memory chunks work too, through 16 MiB slices
+        return Batcher.submit(self, *a, **k)
 
 
 class Pool(Batcher):
@@ -495,6 +560,6 @@ def pool_plan(lens, nparts: int) -> np.ndarray:
 __all__ = ["MD5Context", "MD5Init", "MD5Update", "MD5Final", "MD5_DIGEST_SIZE", "MD5HipError", "arena_empty",
            "plan_desc",
            "md5", "digest_fixed", "digest_desc", "crc32_fixed", "crc32_desc", "plan_order", "fill_synthetic", "Batcher",
-           "Pool", "pool_plan", "CRC_VARIANTS", "DESC_VARIANTS",
+           "Pool", "Queue", "pool_plan", "CRC_VARIANTS", "DESC_VARIANTS",
            "register_host", "unregister_host",
            "variant_name", "resolve_variant", "VARIANTS", "crc_variant_name"]

@@ -1,0 +1,178 @@
+"""The batcher as a coalescing, out-of-order submission queue (md5_submit.c):
+device-resident chunks (md5_batch_submit_device*), host chunks, several
+submitting threads, tickets completing independently.  Every digest array is
+checked against the oracle (oracle/md5_oracle.c through tests/gen.py)."""
+import threading
+
+import numpy as np
+import pytest
+import torch
+
+import gen
+import sproxy_amd.md5 as m
+
+pytestmark = pytest.mark.gpu
+
+
+def _arena_batch(lens, seed, cuda, align=16):
+    """A device buffer holding chunks of `lens` (packed at `align`), its host
+    copy, the device addresses and the oracle digests."""
+    offs, total = gen.pack_offsets(lens, align=align)
+    host = gen.xorshift_array(total + 64, seed=seed)
+    dev = torch.from_numpy(host.copy()).to(cuda)
+    ptrs = np.asarray(offs, dtype=np.uint64) + np.uint64(dev.data_ptr())
+    return dev, ptrs, np.asarray(lens, dtype=np.uint32), gen.oracle_digests(host, offs, lens)
+
+
+def test_queue_device_chunks_host_and_device_digests(cuda):
+    rng = np.random.default_rng(7)
+    lens = [int(x) for x in rng.integers(0, 300000, 700)] + [0, 1, 55, 56, 63, 64, 65]
+    dev, ptrs, L, want = _arena_batch(lens, 71, cuda, align=1)      # any alignment
+    with m.Queue(device=0) as q:
+        got_h = q.submit_device(ptrs, L)                              # digests to host
+        out = torch.empty((len(lens), 16), dtype=torch.uint8, device=cuda)
+        q.submit_device(ptrs, L, out=out)                             # digests stay on device
+        torch.cuda.synchronize()
+    assert np.array_equal(got_h, want)
+    assert np.array_equal(out.cpu().numpy(), want)
+
+
+def test_queue_tickets_complete_out_of_order(cuda):
+    """A submission of four 64 MiB chunks (each a ~0.6 s serial chain) and a
+    later one of short chunks: the short ticket completes while the long one
+    is still running -- completion does not follow submission order."""
+    long_lens = [64 << 20] * 4
+    dl, pl, Ll, wl = _arena_batch(long_lens, 5, cuda)
+    short_lens = [4096] * 256
+    ds, ps, Ls, ws = _arena_batch(short_lens, 6, cuda)
+    with m.Queue(device=0, nslots=4) as q:
+        q.set_inflight(2)
+        a = q.submit_device_async(pl, Ll)
+        b = q.submit_device_async(ps, Ls)
+        assert np.array_equal(b.wait(), ws)
+        assert not a.poll(), "the long ticket finished before the short one was delivered"
+        assert np.array_equal(a.wait(), wl)
+        assert a.poll() and b.poll()
+
+
+def test_queue_coalesces_pending_submissions(cuda):
+    """With one launch in flight (inflight target 1), everything submitted
+    meanwhile goes out as ONE planned descriptor launch; each ticket still
+    gets exactly its own digests."""
+    dl, pl, Ll, wl = _arena_batch([32 << 20] * 2, 9, cuda)            # keeps the device busy
+    rng = np.random.default_rng(11)
+    small = []
+    for k in range(12):
+        lens = [int(x) for x in rng.integers(0, 70000, int(rng.integers(1, 200)))]
+        small.append(_arena_batch(lens, 100 + k, cuda))
+    with m.Queue(device=0, nslots=4) as q:
+        q.set_inflight(1)
+        pa = q.submit_device_async(pl, Ll)
+        pend = [q.submit_device_async(p, L) for _, p, L, _ in small]
+        outs = [p.wait() for p in reversed(pend)]
+        assert np.array_equal(pa.wait(), wl)
+        st = q.stats()
+    for got, (_, _, _, want) in zip(reversed(outs), small):
+        assert np.array_equal(got, want)
+    assert st["submissions"] == 13
+    assert st["launches"] == 2, st
+    assert st["coalesced_launches"] == 1 and st["max_tickets_per_launch"] == 12, st
+
+
+def test_queue_mixed_host_and_device_chunks(cuda):
+    """Host-memory and device-resident submissions interleaved on one queue,
+    MD5 and (per-call) CRC-32 verify."""
+    rng = np.random.default_rng(13)
+    lens = [int(x) for x in rng.integers(0, 100000, 300)]
+    dev, ptrs, L, want = _arena_batch(lens, 131, cuda)
+    blob = gen.xorshift_bytes(sum(lens) + 1, seed=132)
+    bufs, cur = [], 0
+    for x in lens:
+        bufs.append(blob[cur:cur + x])
+        cur += x
+    want_h = gen.oracle_digests(np.frombuffer(blob, dtype=np.uint8), np.cumsum([0] + lens[:-1]), lens)
+    with m.Queue(device=0, nslots=3) as q:
+        p1 = q.submit_device_async(ptrs, L)
+        p2 = q.submit_async(bufs)
+        p3 = q.submit_device_async(ptrs[::-1].copy(), L[::-1].copy())
+        assert np.array_equal(p2.wait(), want_h)
+        assert np.array_equal(p3.wait(), want[::-1])
+        assert np.array_equal(p1.wait(), want)
+        ok, bad = q.verify_iov([[b] for b in bufs], want_h)
+        assert bad == 0 and ok.all()
+
+
+def test_batcher_shared_by_threads(cuda):
+    """One batcher, four submitting threads (the netcache ASIO pool sharing
+    one instance), async host submissions waited in reverse order."""
+    res = {}
+    errs = []
+
+    with m.Batcher(device=0, slice_bytes=4 << 20, nslots=4) as b:
+        def worker(k):
+            try:
+                rng = np.random.default_rng(500 + k)
+                items = []
+                for j in range(6):
+                    lens = [int(x) for x in rng.integers(0, 200000, 30)]
+                    blob = gen.xorshift_bytes(sum(lens) + 1, seed=10 * k + j)
+                    bufs, cur = [], 0
+                    for x in lens:
+                        bufs.append(blob[cur:cur + x])
+                        cur += x
+                    want = gen.oracle_digests(np.frombuffer(blob, dtype=np.uint8),
+                                              np.cumsum([0] + lens[:-1]), lens)
+                    items.append((b.submit_async(bufs), want))
+                res[k] = all(np.array_equal(p.wait(), w) for p, w in reversed(items))
+            except Exception as e:  # pragma: no cover - surfaced below
+                errs.append(repr(e))
+
+        th = [threading.Thread(target=worker, args=(k,)) for k in range(4)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join(timeout=120)
+        st = b.stats()
+    assert not errs, errs
+    assert res == {0: True, 1: True, 2: True, 3: True}
+    assert st["submissions"] == 24
+
+
+def test_batcher_keeps_its_kind_during_header_verify(cuda):
+    """md5hip_batch_verify_headers hashes CRC-32 for that call only: a
+    concurrent MD5 submission on the same batcher still gets MD5."""
+    import struct
+    from sproxy_amd import nc_digest as ncd
+    hdrs = []
+    for k in range(50):
+        hs = 20 + 977 * k
+        h = bytearray(struct.pack("<IiiII", ncd.NC_MAGIC_V30, 0, hs, 0, 0) + gen.xorshift_bytes(hs - 20, seed=k))
+        ncd.header_seal(h)
+        hdrs.append(h)
+    lens = [70000] * 40
+    blob = gen.xorshift_bytes(sum(lens) + 1, seed=3)
+    bufs = [blob[i * 70000:(i + 1) * 70000] for i in range(40)]
+    want = gen.oracle_digests(np.frombuffer(blob, dtype=np.uint8), np.arange(40) * 70000, lens)
+    with m.Batcher(device=0, slice_bytes=4 << 20, nslots=3) as b:
+        p = b.submit_async(bufs)
+        ok, bad = ncd.verify_headers(b, hdrs)
+        assert bad == 0 and all(ok)
+        assert np.array_equal(p.wait(), want)
+        assert np.array_equal(b.submit(bufs), want)
+
+
+def test_arena_freed_right_after_async_launch(cuda):
+    """md5hip_arena_free synchronizes the device before unmapping: dropping an
+    arena tensor right after an asynchronous launch is safe, and a later batch
+    is still correct."""
+    import gc
+    n, L = 4096, 16384
+    for k in range(3):
+        a = m.arena_empty(n * L)
+        m.fill_synthetic(a, seed=70 + k)
+        out = m.digest_fixed(a, n, L)                # async on the current stream
+        del a
+        gc.collect()                                  # frees the arena while the kernel may run
+        torch.cuda.synchronize()
+        host = gen.synthetic_bytes(n * L, 70 + k)
+        assert np.array_equal(out.cpu().numpy(), gen.oracle_digests_fixed(host, n, L)), k
