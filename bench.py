@@ -706,9 +706,9 @@ def run_c3q(a, rank, world, local, device, backend):
     q = m.Queue(device=torch.cuda.current_device(), nslots=a.c3q_slots, inflight=a.c3q_inflight)
 
     def step():
-        ts = [q.submit_device(p, L_, o) for p, L_, o in subs]
-        for t in reversed(ts):             # any order: tickets complete independently
-            q.wait(t)
+        pend = [q.submit_device_async(p, L_, o) for p, L_, o in subs]
+        for pn in reversed(pend):          # any order: tickets complete independently
+            pn.wait()
 
     for _ in range(a.warmup):
         step()

@@ -89,6 +89,29 @@ int md5hip_digest_desc_variant(const void *d_base, const uint64_t *d_offsets,
                                unsigned char *d_digests, void *stream, int variant);
 
 /*
+ * MD5Init / MD5Update / MD5Final on many caller-owned contexts at once
+ * (md5.c:153-265, batched; the "init/update/final behind the C-ABI shim" of
+ * north_star for concurrent objects).  d_ctxs: n struct MD5Context (md5.h,
+ * 88 bytes each, 4-byte aligned) in device memory.  Every context ends
+ * byte-for-byte as the same sequence of host calls leaves it:
+ *   md5hip_init_ctx    ctx i as MD5Init (md5.c:153-163; in[] untouched);
+ *   md5hip_update_ctx  ctx i as MD5Update(ctx i, d_ptrs[i], d_lens[i]): the
+ *                      bit count with its carry (md5.c:177-182), the pending
+ *                      partial block completed, whole blocks compressed, the
+ *                      tail left in ctx->in (md5.c:184-214); d_ptrs is a DEVICE
+ *                      array of device addresses, any alignment, d_lens a
+ *                      device array (one update per context per call; 0 = none);
+ *   md5hip_final_ctx   digest i (16 B, 16-B aligned array) as MD5Final, ctx i
+ *                      zeroed (md5.c:221-265).
+ * Calls on one stream apply in order, so k updates are k launches.
+ */
+struct MD5Context;
+int md5hip_init_ctx(struct MD5Context *d_ctxs, uint64_t n, void *stream);
+int md5hip_update_ctx(struct MD5Context *d_ctxs, const void *const *d_ptrs, const uint32_t *d_lens,
+                      uint64_t n, void *stream);
+int md5hip_final_ctx(struct MD5Context *d_ctxs, uint64_t n, unsigned char *d_digests, void *stream);
+
+/*
  * CRC-32 block checksums -- the checksum netcache itself computes at the
  * block-completion site: nc_crc_t blk_make_crc(inode, blk, len, fastcrc)
  * (netcache/common/blk_io.c:354-430, compiled with NC_ENABLE_CRC), CRC-32

@@ -88,6 +88,9 @@ def lib():
         "md5_batch_submit_device_async": (i, [vp, vp, vp, u64, vp, i, vp]),
         "md5_batch_submit_device": (i, [vp, vp, vp, u64, vp, i]),
         "md5_batch_flush": (i, [vp]),
+        "md5hip_init_ctx": (i, [vp, u64, vp]),
+        "md5hip_update_ctx": (i, [vp, vp, vp, u64, vp]),
+        "md5hip_final_ctx": (i, [vp, u64, vp, vp]),
         "md5hip_batcher_destroy": (None, [vp]),
         "md5_batch_submit": (i, [vp, vp, vp, u64, vp]),
         "md5_batch_submit_iov": (i, [vp, vp, vp, u64, vp]),
@@ -151,7 +154,8 @@ EXPORTS = ["MD5Init", "MD5Update", "MD5Final", "nc_MD5Init", "nc_MD5Update", "nc
            "md5hip_batch_verify_headers", "md5hip_host_register", "md5hip_host_unregister",
            "md5hip_batcher_set_gather", "md5hip_pool_set_gather", "md5hip_queue_create",
            "md5hip_batcher_set_inflight", "md5hip_batcher_get_stats", "md5_batch_submit_device_async",
-           "md5_batch_submit_device", "md5_batch_flush"]
+           "md5_batch_submit_device", "md5_batch_flush", "md5hip_init_ctx", "md5hip_update_ctx",
+           "md5hip_final_ctx"]
 
 
 def check(fn, rc):

@@ -615,6 +615,164 @@ crc32_desc(const uint8_t* __restrict__ base, const uint64_t* __restrict__ offs,
 }
 
 // ---------------------------------------------------------------------------
+// MD5Update / MD5Final on caller-owned contexts (md5.c:169-265), one lane per
+// context: the reference's streaming state machine, batched.  The context is
+// md5.h:33-38's 88-byte struct MD5Context { u32 buf[4]; u32 bits[2]; u8 in[64]; }
+// in device memory, updated byte for byte as md5.c leaves it:
+//   bits  += len << 3 with the carry into bits[1] (md5.c:177-182);
+//   t = pending bytes; if t and len < 64 - t: in[t .. t+len) = data, done
+//   (md5.c:186-193); else the pending block is completed and compressed, then
+//   every whole 64-B block of data (md5.c:204-210); in[] is left holding the
+//   tail in its first bytes and, past them, the last block compressed (the
+//   memcpy at md5.c:214 writes only the tail), or its old bytes if none was.
+//   Final: 0x80, zeros, bit count, one or two compressions, digest = buf, the
+//   whole context zeroed (md5.c:221-265).
+// Data may sit at any byte alignment (the reference takes any void*).
+// ---------------------------------------------------------------------------
+struct CtxWords {
+  uint32_t w[22];     // buf[0..3], bits[0..1], in[] as 16 little-endian words
+};
+
+__device__ __forceinline__ void ctx_load(CtxWords& c, const uint32_t* p) {
+#pragma unroll
+  for (int k = 0; k < 22; ++k) c.w[k] = p[k];
+}
+__device__ __forceinline__ void ctx_store(uint32_t* p, const CtxWords& c) {
+#pragma unroll
+  for (int k = 0; k < 22; ++k) p[k] = c.w[k];
+}
+__global__ void __launch_bounds__(256)
+md5_update_ctx(uint32_t* __restrict__ ctxs, const uint64_t* __restrict__ ptrs,
+               const uint32_t* __restrict__ lens, uint64_t n) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint32_t* cp = ctxs + 22 * i;
+  CtxWords c;
+  ctx_load(c, cp);
+  const uint32_t len = lens[i];
+  const uint8_t* data = reinterpret_cast<const uint8_t*>(ptrs[i]);
+  const uint32_t t0 = c.w[4];
+  const uint32_t lo = t0 + (len << 3);                 // md5.c:179-182
+  c.w[5] += (lo < t0 ? 1u : 0u) + (len >> 29);
+  c.w[4] = lo;
+  const uint32_t t = (t0 >> 3) & 63u;
+  uint32_t in[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) in[j] = c.w[6 + j];
+  if (t && len < 64u - t) {                            // md5.c:189-192: no block completes
+    for (uint32_t k = 0; k < len; ++k) {
+      const uint32_t pos = t + k;
+      const uint32_t b = data[k];
+#pragma unroll
+      for (int j = 0; j < 16; ++j)
+        if ((uint32_t)j == (pos >> 2)) {
+          const uint32_t sh = 8u * (pos & 3u);
+          in[j] = (in[j] & ~(0xFFu << sh)) | (b << sh);
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < 16; ++j) c.w[6 + j] = in[j];
+    ctx_store(cp, c);
+    return;
+  }
+  State st{c.w[0], c.w[1], c.w[2], c.w[3]};
+  uint32_t pos = 0;                                    // bytes of data consumed
+  uint32_t last[16];                                   // the last block compressed
+  bool any = false;
+  if (t) {                                             // md5.c:194-199: complete the pending block
+    const uint32_t need = 64u - t;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) last[j] = in[j];
+    for (uint32_t k = 0; k < need; ++k) {
+      const uint32_t p2 = t + k;
+      const uint32_t b = data[k];
+#pragma unroll
+      for (int j = 0; j < 16; ++j)
+        if ((uint32_t)j == (p2 >> 2)) {
+          const uint32_t sh = 8u * (p2 & 3u);
+          last[j] = (last[j] & ~(0xFFu << sh)) | (b << sh);
+        }
+    }
+    compress(st, [&](int q) __attribute__((always_inline)) { return last[q]; });
+    pos = need;
+    any = true;
+  }
+  const uint32_t nblk = (len - pos) >> 6;             // md5.c:204-210
+  if (nblk) {
+    const uint8_t* p = data + pos;
+    const bool aligned = ((uintptr_t)p & 15u) == 0;
+    uint4 w[4];
+    for (uint32_t blk = 0; blk < nblk; ++blk) {
+      if (aligned) load_block(w, reinterpret_cast<const uint4*>(p + ((uint64_t)blk << 6)));
+      else load_block_unaligned(w, p + ((uint64_t)blk << 6));
+      compress_regs(st, w);
+      if (blk + 1 == nblk) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          last[4 * k] = w[k].x; last[4 * k + 1] = w[k].y;
+          last[4 * k + 2] = w[k].z; last[4 * k + 3] = w[k].w;
+        }
+      }
+    }
+    pos += nblk << 6;
+    any = true;
+  }
+  const uint32_t r = len - pos;                        // md5.c:214: memcpy(in, buf, r)
+  uint32_t tw[16];
+  load_tail(data + pos, r, tw);
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const uint32_t keep = any ? last[j] : in[j];
+    const int nb = (int)r - 4 * j;                     // tail bytes in word j
+    const uint32_t m = nb >= 4 ? 0xFFFFFFFFu : nb <= 0 ? 0u : ((1u << (8 * nb)) - 1u);
+    c.w[6 + j] = (tw[j] & m) | (keep & ~m);
+  }
+  c.w[0] = st.a; c.w[1] = st.b; c.w[2] = st.c; c.w[3] = st.d;
+  ctx_store(cp, c);
+}
+
+__global__ void __launch_bounds__(256)
+md5_final_ctx(uint32_t* __restrict__ ctxs, uint64_t n, uint4* __restrict__ digests) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint32_t* cp = ctxs + 22 * i;
+  CtxWords c;
+  ctx_load(c, cp);
+  const uint32_t count = (c.w[4] >> 3) & 63u;          // md5.c:229
+  uint32_t w[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {                       // in[0..count), 0x80, zeros (md5.c:233-254)
+    const int nb = (int)count - 4 * j;
+    const uint32_t m = nb >= 4 ? 0xFFFFFFFFu : nb <= 0 ? 0u : ((1u << (8 * nb)) - 1u);
+    w[j] = c.w[6 + j] & m;
+    if ((uint32_t)j == (count >> 2)) w[j] |= 0x80u << (8u * (count & 3u));
+  }
+  State st{c.w[0], c.w[1], c.w[2], c.w[3]};
+  if (count >= 56u) {                                  // md5.c:240-249: two blocks
+    compress(st, [&](int q) __attribute__((always_inline)) { return w[q]; });
+#pragma unroll
+    for (int j = 0; j < 14; ++j) w[j] = 0u;
+  }
+  w[14] = c.w[4];                                      // md5.c:257-259
+  w[15] = c.w[5];
+  compress(st, [&](int q) __attribute__((always_inline)) { return w[q]; });
+  digests[i] = make_uint4(st.a, st.b, st.c, st.d);     // md5.c:262-263
+#pragma unroll
+  for (int k = 0; k < 22; ++k) c.w[k] = 0u;            // md5.c:264
+  ctx_store(cp, c);
+}
+
+__global__ void __launch_bounds__(256)
+md5_init_ctx(uint32_t* __restrict__ ctxs, uint64_t n) {  // md5.c:153-163 (in[] untouched)
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint32_t* cp = ctxs + 22 * i;
+  const State s0 = initial_state();
+  cp[0] = s0.a; cp[1] = s0.b; cp[2] = s0.c; cp[3] = s0.d;
+  cp[4] = 0u; cp[5] = 0u;
+}
+
+// ---------------------------------------------------------------------------
 // Device-side gather for the batcher's zero-copy path: segment k of a slice
 // is read from registered (pinned, device-mapped) host memory over PCIe and
 // written to its packed place in the slice's HBM buffer.  One workgroup per

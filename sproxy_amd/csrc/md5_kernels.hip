@@ -224,6 +224,43 @@ int crc32hip_desc(const void* d_base, const uint64_t* d_offsets, const uint32_t*
   return launched();
 }
 
+// Batched MD5Init / MD5Update / MD5Final on caller-owned contexts.
+int md5hip_init_ctx(struct MD5Context* d_ctxs, uint64_t n, void* stream) {
+  if (n == 0) return 0;
+  if (!d_ctxs || ((uintptr_t)d_ctxs & 3u)) return -EINVAL;
+  if (int e = device_ok()) return e;
+  const uint64_t g = (n + kBlock - 1) / kBlock;
+  if (g > 0x7fffffffull) return -EINVAL;
+  hipLaunchKernelGGL(md5_init_ctx, dim3((uint32_t)g), dim3(kBlock), 0, (hipStream_t)stream,
+                     reinterpret_cast<uint32_t*>(d_ctxs), n);
+  return launched();
+}
+
+int md5hip_update_ctx(struct MD5Context* d_ctxs, const void* const* d_ptrs, const uint32_t* d_lens,
+                      uint64_t n, void* stream) {
+  if (n == 0) return 0;
+  if (!d_ctxs || !d_ptrs || !d_lens || ((uintptr_t)d_ctxs & 3u)) return -EINVAL;
+  if (int e = device_ok()) return e;
+  const uint64_t g = (n + kBlock - 1) / kBlock;
+  if (g > 0x7fffffffull) return -EINVAL;
+  hipLaunchKernelGGL(md5_update_ctx, dim3((uint32_t)g), dim3(kBlock), 0, (hipStream_t)stream,
+                     reinterpret_cast<uint32_t*>(d_ctxs), reinterpret_cast<const uint64_t*>(d_ptrs),
+                     d_lens, n);
+  return launched();
+}
+
+int md5hip_final_ctx(struct MD5Context* d_ctxs, uint64_t n, unsigned char* d_digests, void* stream) {
+  if (n == 0) return 0;
+  if (!d_ctxs || !d_digests || ((uintptr_t)d_ctxs & 3u) || ((uintptr_t)d_digests & 15u))
+    return -EINVAL;
+  if (int e = device_ok()) return e;
+  const uint64_t g = (n + kBlock - 1) / kBlock;
+  if (g > 0x7fffffffull) return -EINVAL;
+  hipLaunchKernelGGL(md5_final_ctx, dim3((uint32_t)g), dim3(kBlock), 0, (hipStream_t)stream,
+                     reinterpret_cast<uint32_t*>(d_ctxs), n, reinterpret_cast<uint4*>(d_digests));
+  return launched();
+}
+
 int md5hip_gather_launch(const struct md5hip_seg* d_segs, uint64_t nseg, unsigned char* d_dst,
                          void* stream) {
   static_assert(sizeof(md5hip_seg) == sizeof(GatherSeg), "segment layout");

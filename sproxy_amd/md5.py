@@ -155,6 +155,46 @@ def digest_desc(base, offsets, lens, order=None, out=None, stream=None, variant=
     return out
 
 
+def _ctx_tensor(ctxs):
+    _need_cuda(ctxs, "ctxs")
+    if ctxs.dtype != torch.uint8 or ctxs.dim() != 2 or ctxs.shape[1] != 88:
+        raise ValueError("ctxs must be a uint8 [n, 88] device tensor (struct MD5Context, md5.h:33-38)")
+    return ctxs.shape[0]
+
+
+def init_ctx(ctxs, stream=None):
+    """MD5Init on every context of a uint8 [n, 88] device tensor (in[] untouched)."""
+    n = _ctx_tensor(ctxs)
+    check("md5hip_init_ctx", lib().md5hip_init_ctx(ctxs.data_ptr(), n, _stream(stream)))
+    return ctxs
+
+
+def update_ctx(ctxs, ptrs, lens, stream=None):
+    """MD5Update(ctx[i], ptrs[i], lens[i]) for every i: ptrs an int64 device
+    tensor of device addresses, lens an int32 device tensor."""
+    n = _ctx_tensor(ctxs)
+    _need_cuda(ptrs, "ptrs")
+    _need_cuda(lens, "lens")
+    if ptrs.dtype != torch.int64 or lens.dtype not in (torch.int32, torch.uint32):
+        raise TypeError("ptrs must be int64 and lens int32")
+    if ptrs.numel() != n or lens.numel() != n:
+        raise ValueError("one pointer and one length per context")
+    check("md5hip_update_ctx", lib().md5hip_update_ctx(ctxs.data_ptr(), ptrs.data_ptr(), lens.data_ptr(),
+                                                       n, _stream(stream)))
+    return ctxs
+
+
+def final_ctx(ctxs, out=None, stream=None):
+    """MD5Final on every context: uint8 [n, 16] digests on the device; the
+    contexts are zeroed (md5.c:264)."""
+    n = _ctx_tensor(ctxs)
+    if out is None:
+        out = torch.empty((n, 16), dtype=torch.uint8, device=ctxs.device)
+    _need_cuda(out, "out")
+    check("md5hip_final_ctx", lib().md5hip_final_ctx(ctxs.data_ptr(), n, out.data_ptr(), _stream(stream)))
+    return out
+
+
 CRC_VARIANTS = {"auto": 0, "xdma16": 6}   # enum crc32hip_variant
 
 
@@ -557,7 +597,7 @@ def pool_plan(lens, nparts: int) -> np.ndarray:
     return first
 
 
-__all__ = ["MD5Context", "MD5Init", "MD5Update", "MD5Final", "MD5_DIGEST_SIZE", "MD5HipError", "arena_empty",
+__all__ = ["init_ctx", "update_ctx", "final_ctx", "MD5Context", "MD5Init", "MD5Update", "MD5Final", "MD5_DIGEST_SIZE", "MD5HipError", "arena_empty",
            "plan_desc",
            "md5", "digest_fixed", "digest_desc", "crc32_fixed", "crc32_desc", "plan_order", "fill_synthetic", "Batcher",
            "Pool", "Queue", "pool_plan", "CRC_VARIANTS", "DESC_VARIANTS",
