@@ -337,23 +337,22 @@ def cpu_baseline_crc(reps=7):
 # --------------------------------------------------------------------------- traffic evidence
 def load_traffic(path, kernel, workload):
     """HBM bytes per launch of `kernel` on `workload` from the committed
-    rocprofv3 PMC summary (profiles/traffic.json, scripts/traffic_json.py),
-    keyed by the SHA-256 of libmd5hip.so's device code object: a summary taken
-    from other kernel code, or another workload, reads as null."""
+    rocprofv3 PMC summary (profiles/traffic.json, scripts/traffic_json.py).
+    Each entry carries the SHA-256 of the kernel's machine code it measured;
+    unless the library's current code for that kernel has the same hash, the
+    entry is stale and traffic reads null."""
     if not path or not os.path.exists(path):
         return None, "no traffic summary"
     try:
-        d = json.load(open(path))
+        ent = json.load(open(path)).get("entries", {}).get(f"{kernel}@{workload}")
     except Exception as e:  # pragma: no cover
         return None, f"unreadable: {e}"
-    h = m.code_object_hash()
-    ent = d.get("by_code_object", {}).get(h)
     if ent is None:
-        return None, f"stale: no PMC summary for code object {h[:16]}"
-    v = ent.get("kernels", {}).get(f"{kernel}@{workload}")
-    if v is None:
-        return None, f"no PMC entry for {kernel}@{workload} (code object {h[:16]})"
-    return v["bytes"], f"rocprofv3 PMC FETCH_SIZE/WRITE_SIZE, code object {h[:16]}, {v.get('source', '')}"
+        return None, f"no PMC entry for {kernel}@{workload}"
+    h = m.kernel_code_hash(kernel)
+    if ent.get("code_hash") != h:
+        return None, f"stale: {kernel} code {h[:16]} != measured {str(ent.get('code_hash'))[:16]}"
+    return ent["bytes"], f"rocprofv3 PMC FETCH_SIZE/WRITE_SIZE, kernel code {h[:16]}; {ent.get('source', '')}"
 
 
 # --------------------------------------------------------------------------- configs

@@ -22,7 +22,7 @@ def short(name):
 def main(d):
     vals = defaultdict(lambda: defaultdict(list))
     dur = defaultdict(list)
-    for f in sorted(glob.glob(os.path.join(d, "p*", "pmc_counter_collection.csv"))):
+    for f in sorted(glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)):
         per = defaultdict(lambda: defaultdict(float))
         meta = {}
         for r in csv.DictReader(open(f)):

@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
-"""Merge rocprofv3 PMC passes into profiles/traffic.json, keyed by the SHA-256
-of libmd5hip.so's device code object (sproxy_amd._lib.code_object_hash), so
-bench.py reports counter bytes only for the kernel code that was measured.
+"""Merge rocprofv3 PMC passes into profiles/traffic.json: one entry per
+kernel@workload, with the SHA-256 of that kernel's machine code in the
+library that ran (sproxy_amd._lib.kernel_code_hash), so bench.py reports
+counter bytes only while the kernel's code is the code that was measured.
 
 usage: traffic_json.py FETCH_DIR WRITE_DIR WORKLOAD [--out profiles/traffic.json]
   FETCH_DIR / WRITE_DIR: `rocprofv3 --pmc FETCH_SIZE` / `--pmc WRITE_SIZE`
@@ -46,24 +47,25 @@ def main():
     p.add_argument("--out", default=os.path.join(REPO, "profiles", "traffic.json"))
     p.add_argument("--source", default="")
     a = p.parse_args()
-    from sproxy_amd._lib import code_object_hash
-    h = code_object_hash()
+    from sproxy_amd._lib import kernel_code_hash
     fs, nf = per_kernel(a.fetch, "FETCH_SIZE")
     ws, _ = per_kernel(a.write, "WRITE_SIZE")
     d = json.load(open(a.out)) if os.path.exists(a.out) else {}
-    d.setdefault("_note", "HBM bytes per launch from rocprofv3 PMC (read = 2*1024*FETCH_SIZE, "
-                          "write = 1024*WRITE_SIZE; MI355X_MICROARCH.md HBM section), keyed by the "
-                          "SHA-256 of libmd5hip.so's .hip_fatbin and the bench workload")
-    ent = d.setdefault("by_code_object", {}).setdefault(h, {"kernels": {}})
+    d["_note"] = ("HBM bytes per launch from rocprofv3 PMC (read = 2*1024*FETCH_SIZE, write = "
+                  "1024*WRITE_SIZE; MI355X_MICROARCH.md HBM section), per kernel@workload, with "
+                  "the SHA-256 of the kernel's machine code that was measured")
+    ent = d.setdefault("entries", {})
+    new = {}
     for k, v in fs.items():
         if not k.startswith(("md5_", "crc32_")):
             continue
-        ent["kernels"][f"{k}@{a.workload}"] = {
+        new[f"{k}@{a.workload}"] = {
             "bytes": int(2 * 1024 * v + 1024 * ws.get(k, 0.0)),
             "read_bytes": int(2 * 1024 * v), "write_bytes": int(1024 * ws.get(k, 0.0)),
-            "dispatches": nf[k], "source": a.source}
+            "dispatches": nf[k], "code_hash": kernel_code_hash(k), "source": a.source}
+    ent.update(new)
     json.dump(d, open(a.out, "w"), indent=1, sort_keys=True)
-    print(json.dumps(ent, indent=1))
+    print(json.dumps(new, indent=1))
 
 
 if __name__ == "__main__":

@@ -163,6 +163,75 @@ def check(fn, rc):
         raise MD5HipError(fn, rc)
 
 
+def _elf_sections(elf: bytes):
+    import struct
+    if elf[:4] != b"\x7fELF" or elf[4] != 2:
+        raise ValueError("not an ELF64 object")
+    shoff, = struct.unpack_from("<Q", elf, 0x28)
+    shentsize, shnum, shstrndx = struct.unpack_from("<HHH", elf, 0x3A)
+    secs = [struct.unpack_from("<IIQQQQIIQQ", elf, shoff + k * shentsize) for k in range(shnum)]
+    stroff = secs[shstrndx][4]
+    out = {}
+    for sec in secs:
+        name = elf[stroff + sec[0]:elf.index(b"\0", stroff + sec[0])].decode()
+        out[name] = sec           # (name, type, flags, addr, offset, size, link, info, align, entsize)
+    return out
+
+
+def _device_elf(path: str = LIB_PATH) -> bytes:
+    """The gfx950 code object inside the library's offload bundle."""
+    import struct
+    with open(path, "rb") as f:
+        elf = f.read()
+    sec = _elf_sections(elf)[".hip_fatbin"]
+    fb = elf[sec[4]:sec[4] + sec[5]]
+    magic = b"__CLANG_OFFLOAD_BUNDLE__"
+    if not fb.startswith(magic):
+        raise ValueError(f"{path}: unsupported offload bundle")
+    nent, = struct.unpack_from("<Q", fb, len(magic))
+    pos = len(magic) + 8
+    for _ in range(nent):
+        off, size, tlen = struct.unpack_from("<QQQ", fb, pos)
+        triple = fb[pos + 24:pos + 24 + tlen].decode()
+        pos += 24 + tlen
+        if "gfx950" in triple:
+            return fb[off:off + size]
+    raise ValueError(f"{path}: no gfx950 code object")
+
+
+def kernel_code_hash(kernel: str, path: str = LIB_PATH) -> str:
+    """SHA-256 of one kernel's machine code plus its kernel descriptor in the
+    library's gfx950 code object (`kernel`: the rocprof short name, e.g.
+    md5_fixed_xdma1nt).  profiles/traffic.json records it beside each PMC
+    measurement, so counter bytes stay attached to the code they measured."""
+    import hashlib
+    import struct
+    co = _device_elf(path)
+    secs = _elf_sections(co)
+    symtab, strtab = secs[".symtab"], secs[".strtab"]
+    ent = symtab[9] or 24
+    tag = f"{len(kernel)}{kernel}".encode()
+    h = hashlib.sha256()
+    found = []
+    for k in range(symtab[5] // ent):
+        st_name, st_info, st_other, st_shndx, st_value, st_size = struct.unpack_from(
+            "<IBBHQQ", co, symtab[4] + k * ent)
+        name = co[strtab[4] + st_name:co.index(b"\0", strtab[4] + st_name)]
+        if tag not in name or st_size == 0:
+            continue
+        sec = [s for s in secs.values() if s[3] <= st_value < s[3] + s[5] and s[1] != 8]
+        if not sec:
+            continue
+        off = sec[0][4] + (st_value - sec[0][3])
+        found.append((name, co[off:off + st_size]))
+    if not found:
+        raise KeyError(f"kernel {kernel} not in {path}")
+    for name, code in sorted(found):
+        h.update(name)
+        h.update(code)
+    return h.hexdigest()
+
+
 def code_object_hash(path: str = LIB_PATH) -> str:
     """SHA-256 of the library's device code (its .hip_fatbin ELF section):
     counter evidence (profiles/traffic.json) is keyed by it, so numbers taken

@@ -274,19 +274,25 @@ struct Crc32LaneHasher {
 
 // Slicing-by-4 over 16 lane copies laid out so ONE v_perm_b32 forms each
 // lookup address: entry e of table t, copy c at word e*64 + t*16 + c, i.e.
-// byte address (e << 8) | (t << 6) | (c << 2).  v_perm_b32 drops the index
-// byte into bits 8..15 next to the lane's (c << 2) byte, and t << 6 rides in
-// the ds_read_b32 immediate offset -- 1 VALU per lookup instead of a byte
-// extract plus a shift-or.  The price: ds_read_b32 banks on word mod 32 =
-// (t & 1) * 16 + c, so lanes l and l + 16 of a 32-lane group (same copy)
-// always share a bank: a fixed 2-way conflict, where the interleaved layout of
-// Crc32LaneHasher<16> is 1.5-way on average.  64 KiB of LDS either way.
+// byte address (e << 8) | (t << 6) | (c << 2) (64 KiB).  v_perm_b32 drops the
+// index byte into bits 8..15 next to a per-lane constant byte (t << 6) |
+// (c << 2).  ds_read_b32 banks on word mod 32 = (t & 1) * 16 + c over 32-lane
+// groups (MI355X_MICROARCH §LDS), so if every lane looked up the same table
+// per instruction, lanes l and l + 16 (same copy) would always share a bank
+// (the round-1 fixed 2-way conflict, profiles/r01_pmc_summary_final_box2.json).
+// Instead lanes with bit 4 set take the four tables in the order 1, 0, 3, 2:
+// in every lookup instruction lanes 0-15 read an even (odd) table and lanes
+// 16-31 the odd (even) one, i.e. the two halves of the group sit in opposite
+// bank halves -- conflict-free.  The four lookups are XORed, so the order is
+// free; each lane holds its per-slot constant byte and v_perm selector in
+// VGPRs (the table no longer rides in the ds_read immediate).
 struct Crc32PermHasher {
   using State = Crc32State;
   using Out = uint32_t;
   static constexpr int kLdsBytes = 256 * 64 * 4;
   const uint8_t* lds;
-  uint32_t lane4;                      // (lane % 16) * 4 in byte 0
+  uint32_t lane4;                      // (lane % 16) * 4: table 0, for the byte-wise tail
+  uint32_t lb[4], sel[4];              // slot k: (t << 6) | (c << 2), and the v_perm selector
   __device__ __forceinline__ void setup(uint8_t* l) {
     uint32_t* t = reinterpret_cast<uint32_t*>(l);
     for (uint32_t k = threadIdx.x; k < 256u * 64u; k += blockDim.x)
@@ -294,20 +300,30 @@ struct Crc32PermHasher {
     __syncthreads();
     lds = l;
     lane4 = (threadIdx.x & 15u) * 4u;
+    const uint32_t h = (threadIdx.x >> 4) & 1u;
+#pragma unroll
+    for (uint32_t k = 0; k < 4; ++k) {
+      const uint32_t tab = k ^ h;                   // this lane's table in slot k
+      lb[k] = (tab << 6) | lane4;
+      // byte 0 <- lb byte 0, byte 1 <- c byte (3 - tab), bytes 2-3 <- 0
+      sel[k] = 0x0C0C0000u | ((4u + 3u - tab) << 8);
+    }
   }
-  // table t, index = byte j of x
-  template <int T, int J>
-  __device__ __forceinline__ uint32_t look(uint32_t x) const {
-    // selector bytes: 0 -> lane4 byte 0, 4 + J -> x byte J, 0x0C -> zero
-    const uint32_t addr = __builtin_amdgcn_perm(x, lane4, 0x0C0C0000u | ((4u + J) << 8));
-    return *reinterpret_cast<const uint32_t*>(lds + addr + T * 64);
+  __device__ __forceinline__ uint32_t slot(uint32_t c, int k) const {
+    const uint32_t addr = __builtin_amdgcn_perm(c, lb[k], sel[k]);
+    return *reinterpret_cast<const uint32_t*>(lds + addr);
   }
   static __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
     return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
   }
   __device__ __forceinline__ uint32_t step4(uint32_t c, uint32_t w) const {
-    c ^= w;
-    return xor3(look<0, 3>(c), look<1, 2>(c), look<2, 1>(c)) ^ look<3, 0>(c);
+    c ^= w;      // T0[b3] ^ T1[b2] ^ T2[b1] ^ T3[b0] (crc32.c slicing), in this lane's slot order
+    return xor3(slot(c, 0), slot(c, 1), slot(c, 2)) ^ slot(c, 3);
+  }
+  // table 0, index = byte 0 of x (the byte-wise tail, crc32.c:236-238)
+  __device__ __forceinline__ uint32_t look0(uint32_t x) const {
+    const uint32_t addr = __builtin_amdgcn_perm(x, lane4, 0x0C0C0400u);
+    return *reinterpret_cast<const uint32_t*>(lds + addr);
   }
   __device__ __forceinline__ State init() { return State{0xFFFFFFFFu}; }
   __device__ __forceinline__ void block(State& st, const uint4 (&w)[4]) {
@@ -336,7 +352,7 @@ struct Crc32PermHasher {
         if ((uint32_t)j == (done >> 2)) wd = w[j];
 #pragma unroll
       for (int b = 0; b < 3; ++b)      // the last 1..3 bytes, one at a time (crc32.c:236-238)
-        if (done + (uint32_t)b < r) c = look<0, 0>(c ^ (wd >> (8 * b))) ^ (c >> 8);
+        if (done + (uint32_t)b < r) c = look0(c ^ (wd >> (8 * b))) ^ (c >> 8);
     }
     st.c = ~c;
   }

@@ -907,6 +907,18 @@ int diag_launch_lds(const uint8_t* base, uint64_t n, uint32_t len, uint64_t stri
 
 namespace md5hip {
 template __global__ void md5_fixed_direct<4, Md5Hasher<false>>(const uint8_t*, uint64_t, uint32_t, uint64_t, uint4*);
+template __global__ void crc32_fast<true>(const uint8_t*, const uint64_t*, const uint32_t*,
+                                          uint64_t, uint64_t, uint32_t, uint32_t, uint32_t*);
+}
+
+// the round-1 fastcrc kernel (lane-direct), fixed-length chunks
+extern "C" int md5diag_crc_fast_lane(const void* d_base, uint64_t n, uint32_t len, uint64_t stride,
+                                     uint32_t fastcrc, uint32_t* d_out, void* stream) {
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(crc32_fast<true>, dim3((uint32_t)((n + 63) / 64)), dim3(64), 0, (hipStream_t)stream,
+                     (const uint8_t*)d_base, (const uint64_t*)nullptr, (const uint32_t*)nullptr, n,
+                     stride, len, fastcrc, d_out);
+  return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }
 
 extern "C" int md5diag_variant_fixed(int v, const void* d_base, uint64_t n, uint32_t len,

@@ -356,20 +356,69 @@ __device__ __forceinline__ bool long_outlier(const uint32_t* __restrict__ lens,
 // 64-B blocks (256 KiB)
 constexpr uint32_t kHybridLongBlocks = 4096;
 
+// Where chunk i of a descriptor batch lies: (offset, length) arrays, packed
+// onto lanes in `order` when given.
+struct DescArrays {
+  const uint64_t* __restrict__ offs;
+  const uint32_t* __restrict__ lens;
+  const uint32_t* __restrict__ order;
+  static constexpr bool kPairXor = false;
+  __device__ __forceinline__ uint64_t index(uint64_t i) const { return order ? (uint64_t)order[i] : i; }
+  __device__ __forceinline__ uint64_t off(uint64_t c) const { return offs[c]; }
+  __device__ __forceinline__ uint32_t len(uint64_t c) const { return lens[c]; }
+};
+
+// blk_make_crc's fastcrc windows (blk_io.c:408-424) as a descriptor batch of
+// 2n rows: row 2k = the first F bytes of chunk k, row 2k+1 = its last F
+// bytes; a chunk of <= F bytes is row 2k alone (row 2k+1 empty: CRC 0, the
+// XOR identity).  kPairXor: lanes 2k and 2k+1 combine, out[k] = crc ^ crc.
+// Chunk k at offs[k] / lens[k], or (offs == nullptr) at k * stride, flen.
+struct FastWindows {
+  const uint64_t* __restrict__ offs;
+  const uint32_t* __restrict__ lens;
+  uint64_t stride;
+  uint32_t flen, F;
+  static constexpr bool kPairXor = true;
+  __device__ __forceinline__ uint64_t index(uint64_t i) const { return i; }
+  __device__ __forceinline__ uint32_t clen(uint64_t k) const { return offs ? lens[k] : flen; }
+  __device__ __forceinline__ uint64_t off(uint64_t c) const {
+    const uint64_t k = c >> 1;
+    const uint64_t o = offs ? offs[k] : k * stride;
+    const uint32_t L = clen(k);
+    return ((c & 1u) && L > F) ? o + (L - F) : o;
+  }
+  __device__ __forceinline__ uint32_t len(uint64_t c) const {
+    const uint32_t L = clen(c >> 1);
+    return L <= F ? ((c & 1u) ? 0u : L) : F;
+  }
+};
+
+// A finished lane's digest: stored at c, or (kPairXor) XORed with its pair
+// lane and stored by the even lane at c / 2.  Pairs are live together.
+template <class Src, class H>
+__device__ __forceinline__ void emit(H& h, typename H::Out* __restrict__ out, uint64_t c,
+                                     const typename H::State& st) {
+  if constexpr (Src::kPairXor) {
+    const uint32_t v = st.c ^ (uint32_t)__shfl_xor((int)st.c, 1, 64);
+    if (!(c & 1u)) out[c >> 1] = v;
+  } else {
+    h.store(out, c, st);
+  }
+}
+
 template <int CP, class H, uint32_t kLong = 0, int D = 1, bool kHalf = false, bool kPeel = true,
-          bool kDma = false>
+          bool kDma = false, class Src = DescArrays>
 __device__ __forceinline__ void desc_xpose_group(H& h, const uint8_t* __restrict__ base,
-                                                 const uint64_t* __restrict__ offs,
-                                                 const uint32_t* __restrict__ lens,
-                                                 const uint32_t* __restrict__ order, uint64_t n,
+                                                 const Src& src, uint64_t n,
                                                  uint64_t first, typename H::Out* __restrict__ out,
                                                  uint8_t* img, uint32_t nlong = 0) {
   const uint32_t lane = threadIdx.x & 63u;
   const uint64_t i = first + lane;
   const bool live = i < n;
-  const uint64_t c = order ? (uint64_t)order[live ? i : first] : (live ? i : first);
-  const uint8_t* chunk = base + offs[c];
-  const uint32_t len = live ? lens[c] : 0u;
+  const uint64_t c = src.index(live ? i : first);
+  const uint64_t off = src.off(c);
+  const uint8_t* chunk = base + off;
+  const uint32_t len = live ? src.len(c) : 0u;
   const uint32_t nfull = len >> 6;
   const uint32_t nst = nfull >> 1;                       // this lane's 128-B stages
   const uint32_t smax = wave_max(nst);
@@ -382,21 +431,20 @@ __device__ __forceinline__ void desc_xpose_group(H& h, const uint8_t* __restrict
   if (kLong && bmax >= kLong && (first >> 6) < nlong) {
     if (live) {
       lane_range<H, 8>(h, st, chunk, len);
-      h.store(out, c, st);
+      emit<Src>(h, out, c, st);
     }
     return;
   }
   if (unaligned) {
     if (live) {                      // rare: a short ring keeps VGPRs for the main path
       lane_range<H, 2>(h, st, chunk, len);
-      h.store(out, c, st);
+      emit<Src>(h, out, c, st);
     }
     return;
   }
   if (smax) {
     // the row with the most stages stands in for rows without any
     const uint32_t mrow = __builtin_ctzll(__ballot(nst == smax));
-    const uint64_t off = offs[c];
     const uint8_t* rptr[8];            // base + offset: stays a global pointer (no flat loads)
     uint32_t rlast[8];
 #pragma unroll
@@ -506,7 +554,7 @@ __device__ __forceinline__ void desc_xpose_group(H& h, const uint8_t* __restrict
       h.block(st, w);
     }
     h.finish(st, chunk + ((uint64_t)nfull << 6), len & 63u, len);
-    h.store(out, c, st);
+    emit<Src>(h, out, c, st);
   }
 }
 
@@ -520,8 +568,8 @@ __device__ __forceinline__ void desc_xpose_body(const uint8_t* __restrict__ base
   H h;
   const uint64_t first = ((uint64_t)blockIdx.x * blockDim.x) + (threadIdx.x & ~63u);
   if (first >= n) return;
-  desc_xpose_group<CP, H, kLong, D, false, true, kDma>(h, base, offs, lens, order, n, first, out,
-                                                      img, nlong);
+  desc_xpose_group<CP, H, kLong, D, false, true, kDma>(h, base, DescArrays{offs, lens, order}, n,
+                                                      first, out, img, nlong);
 }
 
 __global__ void __launch_bounds__(64)
@@ -575,34 +623,29 @@ crc32_desc_xdma16(const uint8_t* __restrict__ base, const uint64_t* __restrict__
   uint8_t* img = lds + Crc32PermHasher::kLdsBytes + wave * 8192u;
   const uint64_t ngroups = (n + 63) / 64;
   for (uint64_t gi = (uint64_t)wave * gridDim.x + blockIdx.x; gi < ngroups; gi += (uint64_t)gridDim.x * 12u)
-    desc_xpose_group<2, Crc32PermHasher, 0, 1, false, true, true>(h, base, offs, lens, order, n,
-                                                                  gi * 64u, out, img);
+    desc_xpose_group<2, Crc32PermHasher, 0, 1, false, true, true>(
+        h, base, DescArrays{offs, lens, order}, n, gi * 64u, out, img);
 }
 
-// fastcrc (blk_io.c:408-424): len <= f -> crc(all), else crc(first f bytes)
-// ^ crc(last f bytes).  kImplicit: chunk i at base + i*stride, length flen.
-template <bool kImplicit>
-__global__ void __launch_bounds__(256)
-crc32_fast(const uint8_t* __restrict__ base, const uint64_t* __restrict__ offs,
-           const uint32_t* __restrict__ lens, uint64_t n, uint64_t stride, uint32_t flen,
-           uint32_t fast, uint32_t* __restrict__ out) {
-  __shared__ __attribute__((aligned(16))) uint8_t tabs[Crc32Hasher::kLdsBytes];
-  Crc32Hasher h;
-  h.setup(tabs);
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const uint8_t* chunk = base + (kImplicit ? i * stride : offs[i]);
-  const uint32_t len = kImplicit ? flen : lens[i];
-  Crc32State a = h.init();
-  if (len <= fast) {
-    lane_range<Crc32Hasher, 2>(h, a, chunk, len);
-  } else {
-    lane_range<Crc32Hasher, 2>(h, a, chunk, fast);
-    Crc32State b = h.init();
-    lane_range<Crc32Hasher, 2>(h, b, chunk + (len - fast), fast);
-    a.c ^= b.c;
-  }
-  out[i] = a.c;
+// fastcrc (blk_io.c:408-424) through the same LDS-DMA loader: each 64-row
+// wave group is 32 chunks' head and tail windows (FastWindows), F bytes each,
+// so a wave-instruction still reads whole 128-B runs of 8 windows; lane pairs
+// XOR their CRCs.  offs == nullptr: fixed-length chunks (k * stride, flen).
+__global__ void __launch_bounds__(768)
+crc32_fast_xdma16(const uint8_t* __restrict__ base, const uint64_t* __restrict__ offs,
+                  const uint32_t* __restrict__ lens, uint64_t n, uint64_t stride, uint32_t flen,
+                  uint32_t F, uint32_t* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds[Crc32PermHasher::kLdsBytes + 12 * 8192];
+  Crc32PermHasher h;
+  h.setup(lds);
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  uint8_t* img = lds + Crc32PermHasher::kLdsBytes + wave * 8192u;
+  const FastWindows src{offs, lens, stride, flen, F};
+  const uint64_t rows = 2 * n;
+  const uint64_t ngroups = (rows + 63) / 64;
+  for (uint64_t gi = (uint64_t)wave * gridDim.x + blockIdx.x; gi < ngroups; gi += (uint64_t)gridDim.x * 12u)
+    desc_xpose_group<2, Crc32PermHasher, 0, 1, false, true, true, FastWindows>(h, base, src, rows,
+                                                                               gi * 64u, out, img);
 }
 
 template <bool kImplicit>

@@ -13,10 +13,6 @@ template __global__ void md5_desc<true>(const uint8_t*, const uint64_t*, const u
 template __global__ void crc32_desc<true>(const uint8_t*, const uint64_t*, const uint32_t*,
                                           const uint32_t*, uint64_t, uint64_t, uint32_t,
                                           uint32_t*);
-template __global__ void crc32_fast<false>(const uint8_t*, const uint64_t*, const uint32_t*,
-                                           uint64_t, uint64_t, uint32_t, uint32_t, uint32_t*);
-template __global__ void crc32_fast<true>(const uint8_t*, const uint64_t*, const uint32_t*,
-                                          uint64_t, uint64_t, uint32_t, uint32_t, uint32_t*);
 
 }  // namespace md5hip
 
@@ -179,9 +175,10 @@ int crc32hip_fixed_variant(const void* d_base, uint64_t n, uint32_t len, uint64_
   const uint64_t g = (n + kDescBlock - 1) / kDescBlock;
   if (g > 0x7fffffffull) return -EINVAL;
   if (fastcrc && len > fastcrc) {
-    hipLaunchKernelGGL(crc32_fast<true>, dim3((uint32_t)g), dim3(kDescBlock), 0, s, base,
-                       (const uint64_t*)nullptr, (const uint32_t*)nullptr, n, stride, len,
-                       fastcrc, d_crcs);
+    // head and tail windows as 2n rows through the LDS-DMA loader
+    hipLaunchKernelGGL(crc32_fast_xdma16, dim3(per_cu_grid(2 * n)), dim3(768), 0, s, base,
+                       (const uint64_t*)nullptr, (const uint32_t*)nullptr, n, stride, len, fastcrc,
+                       d_crcs);
     return launched();
   }
   const bool aligned = ((uintptr_t)base & 15u) == 0 && (stride & 15u) == 0;
@@ -213,7 +210,7 @@ int crc32hip_desc(const void* d_base, const uint64_t* d_offsets, const uint32_t*
   const uint64_t g = (n + kDescBlock - 1) / kDescBlock;
   if (g > 0x7fffffffull) return -EINVAL;
   if (fastcrc) {
-    hipLaunchKernelGGL(crc32_fast<false>, dim3((uint32_t)g), dim3(kDescBlock), 0, s,
+    hipLaunchKernelGGL(crc32_fast_xdma16, dim3(per_cu_grid(2 * n)), dim3(768), 0, s,
                        (const uint8_t*)d_base, d_offsets, d_lens, n, (uint64_t)0, 0u, fastcrc,
                        d_crcs);
     return launched();

@@ -468,8 +468,36 @@ crc32_desc_xperm16(const uint8_t* __restrict__ base, const uint64_t* __restrict_
   uint8_t* img = lds + Crc32PermHasher::kLdsBytes + wave * 4096u;
   const uint64_t ngroups = (n + 63) / 64;
   for (uint64_t gi = (uint64_t)wave * gridDim.x + blockIdx.x; gi < ngroups; gi += (uint64_t)gridDim.x * 16u)
-    desc_xpose_group<2, Crc32PermHasher, 0, 1, true, false>(h, base, offs, lens, order, n,
+    desc_xpose_group<2, Crc32PermHasher, 0, 1, true, false>(h, base, DescArrays{offs, lens, order}, n,
                                                             gi * 64u, out, img);   // (wave-major, as above)
+}
+
+
+// round-1 fastcrc kernel: lane-direct loads over shared slicing-by-8 tables
+// fastcrc (blk_io.c:408-424): len <= f -> crc(all), else crc(first f bytes)
+// ^ crc(last f bytes).  kImplicit: chunk i at base + i*stride, length flen.
+template <bool kImplicit>
+__global__ void __launch_bounds__(256)
+crc32_fast(const uint8_t* __restrict__ base, const uint64_t* __restrict__ offs,
+           const uint32_t* __restrict__ lens, uint64_t n, uint64_t stride, uint32_t flen,
+           uint32_t fast, uint32_t* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) uint8_t tabs[Crc32Hasher::kLdsBytes];
+  Crc32Hasher h;
+  h.setup(tabs);
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint8_t* chunk = base + (kImplicit ? i * stride : offs[i]);
+  const uint32_t len = kImplicit ? flen : lens[i];
+  Crc32State a = h.init();
+  if (len <= fast) {
+    lane_range<Crc32Hasher, 2>(h, a, chunk, len);
+  } else {
+    lane_range<Crc32Hasher, 2>(h, a, chunk, fast);
+    Crc32State b = h.init();
+    lane_range<Crc32Hasher, 2>(h, b, chunk + (len - fast), fast);
+    a.c ^= b.c;
+  }
+  out[i] = a.c;
 }
 
 

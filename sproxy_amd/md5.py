@@ -303,14 +303,15 @@ def crc_kernel_name(length: int, fastcrc: int = 0) -> str:
     """The kernel crc32hip_fixed launches for 16-B aligned chunks of `length`
     bytes (bench.py's roofline names it)."""
     if 0 < fastcrc < length:
-        return "crc32_fast"
+        return "crc32_fast_xdma16"
     return "crc32_fixed_" + crc_variant_name(0)
 
 
-def code_object_hash() -> str:
-    """SHA-256 of libmd5hip.so's device code (keys profiles/traffic.json)."""
-    from ._lib import code_object_hash as h
-    return h()
+def kernel_code_hash(kernel: str) -> str:
+    """SHA-256 of one kernel's gfx950 machine code in libmd5hip.so (keys the
+    PMC entries of profiles/traffic.json)."""
+    from ._lib import kernel_code_hash as h
+    return h(kernel)
 
 
 def resolve_variant(v=AUTO) -> int:

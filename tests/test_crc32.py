@@ -174,3 +174,31 @@ def test_gpu_crc_desc_netcache_blocks(cuda):
         for order in (m.plan_order(lens).astype(np.int32), None):
             got = m.crc32_desc(d, t_off, t_len, None if order is None else _dev(order, cuda))
             assert np.array_equal(got.cpu().numpy().view(np.uint32), want), (S, order is None)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fast", [4, 100, 128, 1000, 16368])
+def test_gpu_fastcrc_xdma_windows(cuda, fast):
+    """fastcrc through the LDS-DMA loader (crc32_fast_xdma16): head and tail
+    windows as row pairs, more 32-chunk groups than one grid holds, fixed
+    16 KiB blocks and 16-B packed ragged blocks (windows of every alignment,
+    blocks shorter than the window, empty blocks), against crc32.c's
+    blk_make_crc combination (blk_io.c:408-424) in the oracle."""
+    import torch
+    n, L = 40000, 16384
+    d = torch.empty(n * L, dtype=torch.uint8, device=cuda)
+    m.fill_synthetic(d, seed=0xFA57 + fast)
+    got = m.crc32_fixed(d, n, L, fastcrc=fast).cpu().numpy().view(np.uint32)
+    host = gen.synthetic_bytes(n * L, 0xFA57 + fast)
+    want = gen.oracle_crc32_batch(host, np.arange(n, dtype=np.uint64) * L, [L] * n, fast)
+    assert np.array_equal(got, want)
+    del d, host
+    rng = np.random.default_rng(fast)
+    lens = [int(x) for x in rng.integers(0, 40000, 5000)] + [0, 1, fast - 1, fast, fast + 1]
+    offs, total = gen.pack_offsets(lens, align=16)
+    buf = gen.xorshift_array(total + 64, seed=fast)
+    want = gen.oracle_crc32_batch(buf, offs, lens, fast)
+    got = m.crc32_desc(_dev(buf, cuda), torch.tensor(offs, dtype=torch.int64, device=cuda),
+                       torch.tensor(lens, dtype=torch.int32, device=cuda),
+                       fastcrc=fast).cpu().numpy().view(np.uint32)
+    assert np.array_equal(got, want)
