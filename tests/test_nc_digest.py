@@ -141,3 +141,21 @@ def test_gpu_batch_verify_headers(cuda):
         lens = [len(x) for x in bufs]
         want_md5 = gen.oracle_digests(np.frombuffer(blob, np.uint8), np.cumsum([0] + lens[:-1]), lens)
         assert np.array_equal(b.submit(bufs), want_md5)
+
+
+def test_header_layout_against_reference_probe():
+    """include/nc_digest.h's header offsets against offsetof() in the
+    reference netcache.h compiled as is (oracle/nc_header_probe.c, `make -C
+    oracle probe`).  netcache.h needs <uuid/uuid.h>, absent in this image and
+    not stubbed, so without the probe's output this row is parity unpinned
+     and the test says so."""
+    import re
+    path = os.path.join(gen.REPO, "oracle", "_ref", "nc_header_layout.json")
+    if not os.path.exists(path):
+        pytest.skip("parity unpinned: netcache.h does not compile here without <uuid/uuid.h>")
+    lay = json.load(open(path))
+    hdr = open(os.path.join(gen.REPO, "include", "nc_digest.h")).read()
+    off = {k: int(v) for k, v in re.findall(r"#define NC_HDR_OFF_(\w+) (\d+)", hdr)}
+    assert off["MAGIC"] == lay["magic"] and off["DISK_HEADER_SIZE"] == lay["disk_header_size"]
+    assert off["HEADER_SIZE"] == lay["header_size"] and off["FLAG"] == lay["flag"]
+    assert off["CRC"] == lay["crc"] and lay["sizeof_nc_crc_t"] == 4
