@@ -1002,3 +1002,59 @@ extern "C" int md5diag_variant_crc_desc(int v, const void* d_base, const uint64_
                      (const uint8_t*)d_base, offs, lens, order, n, d_out);
   return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }
+
+// ---------------------------------------------------------------------------
+// The product descriptor kernels (XDMA / HYBRID) with a per-wave record:
+// HW_ID, XCC_ID, s_memrealtime (100 MHz) at start and end -- where the waves
+// of a coalesced mixed batch ran and for how long (scripts/c3_trace_x.py).
+//   kind 0  md5_desc_xdma      kind 1  md5_desc_hybrid (whole-line refill, product)
+//   kind 2  md5_desc_hybrid with the round-1 single-block refill (A/B)
+// rec == nullptr: no record (timing-only A/B).
+// ---------------------------------------------------------------------------
+namespace md5hip {
+template <uint32_t kLong, bool kLongPair>
+__global__ void __launch_bounds__(64)
+diag_desc_x(const uint8_t* __restrict__ base, const uint64_t* __restrict__ offs,
+            const uint32_t* __restrict__ lens, const uint32_t* __restrict__ order, uint64_t n,
+            uint4* __restrict__ out, uint32_t nlong, uint64_t* __restrict__ rec) {
+  __shared__ __attribute__((aligned(16))) uint8_t img[8192];
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  Md5Hasher<true> h;
+  const uint64_t first = (uint64_t)blockIdx.x * 64u;
+  if (first < n)
+    desc_xpose_group<2, Md5Hasher<true>, kLong, 1, false, true, true, DescArrays, kLongPair>(
+        h, base, DescArrays{offs, lens, order}, n, first, out, img, nlong);
+  const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
+  if (rec && (threadIdx.x & 63u) == 0) {
+    uint32_t hw, xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    const uint64_t w = blockIdx.x;
+    rec[4 * w + 0] = hw;
+    rec[4 * w + 1] = xcc;
+    rec[4 * w + 2] = t0;
+    rec[4 * w + 3] = t1;
+  }
+}
+}  // namespace md5hip
+
+extern "C" int md5diag_desc_x(int kind, const void* base, const uint64_t* offs, const uint32_t* lens,
+                              const uint32_t* order, uint64_t n, void* out, uint32_t nlong, void* rec,
+                              void* stream) {
+  if (n == 0) return 0;
+  const dim3 g((uint32_t)((n + 63) / 64)), b(64);
+  hipStream_t s = (hipStream_t)stream;
+  const uint8_t* bs = (const uint8_t*)base;
+  uint64_t* r = (uint64_t*)rec;
+  if (kind == 0)
+    hipLaunchKernelGGL((diag_desc_x<0, true>), g, b, 0, s, bs, offs, lens, order, n, (uint4*)out, nlong, r);
+  else if (kind == 1)
+    hipLaunchKernelGGL((diag_desc_x<kHybridLongBlocks, true>), g, b, 0, s, bs, offs, lens, order, n,
+                       (uint4*)out, nlong, r);
+  else if (kind == 2)
+    hipLaunchKernelGGL((diag_desc_x<kHybridLongBlocks, false>), g, b, 0, s, bs, offs, lens, order, n,
+                       (uint4*)out, nlong, r);
+  else
+    return -EINVAL;
+  return hipGetLastError() == hipSuccess ? 0 : -EIO;
+}

@@ -406,8 +406,11 @@ __device__ __forceinline__ void emit(H& h, typename H::Out* __restrict__ out, ui
   }
 }
 
+// kLongPair: HYBRID's lane-direct long waves refill their 8-block ring two
+// blocks (one whole 128-B line) at a time, so no lane leaves half a line
+// behind to be fetched again after eviction (ring_steps).
 template <int CP, class H, uint32_t kLong = 0, int D = 1, bool kHalf = false, bool kPeel = true,
-          bool kDma = false, class Src = DescArrays>
+          bool kDma = false, class Src = DescArrays, bool kLongPair = true>
 __device__ __forceinline__ void desc_xpose_group(H& h, const uint8_t* __restrict__ base,
                                                  const Src& src, uint64_t n,
                                                  uint64_t first, typename H::Out* __restrict__ out,
@@ -430,7 +433,7 @@ __device__ __forceinline__ void desc_xpose_group(H& h, const uint8_t* __restrict
   const bool unaligned = __ballot(live && (((uintptr_t)chunk & 15u) != 0)) != 0;
   if (kLong && bmax >= kLong && (first >> 6) < nlong) {
     if (live) {
-      lane_range<H, 8>(h, st, chunk, len);
+      lane_range<H, 8, kLongPair>(h, st, chunk, len);
       emit<Src>(h, out, c, st);
     }
     return;
