@@ -82,7 +82,11 @@ enum md5hip_desc_variant {
                                batches whose longest chunks bound the launch) */
     MD5HIP_DESC_XDMA = 4,   /* whole-line loads of 8 chunks x 128 B by LDS-DMA into a
                                transpose image; waves holding an unaligned chunk go LANE */
-    MD5HIP_DESC_NUM_VARIANTS = 5
+    MD5HIP_DESC_BALANCED = 5, /* XDMA's loader in a persistent grid of one wave per SIMD
+                               taking 64-chunk groups longest-first (LPT list scheduling):
+                               the planner's choice for mixed batches holding several
+                               waves of work per SIMD (coalesced submissions) */
+    MD5HIP_DESC_NUM_VARIANTS = 6
 };
 int md5hip_digest_desc_variant(const void *d_base, const uint64_t *d_offsets,
                                const uint32_t *d_lens, const uint32_t *d_order, uint64_t n,
@@ -161,9 +165,12 @@ int md5hip_arena_free(void *d_ptr);
 /*
  * Host planner for a descriptor batch: fills order[] as md5hip_plan_order and
  * returns the enum md5hip_desc_variant to launch it with (>= 0), or -errno.
- * HYBRID when the batch's longest chunks (>= 256 KiB) stand out -- the chunk
- * two waves per CU deep in the order is at most a quarter as long, so their
- * serial chains bound the launch -- else XDMA.
+ * With the longest chunk >= 256 KiB and the median 64-chunk group at most an
+ * eighth of the longest (a mixed batch): BALANCED when the batch holds at
+ * least 0.4 x (SIMDs x the longest chain) of work, so the placement of waves
+ * on SIMDs decides the time; else HYBRID when the longest chunks stand out
+ * (the chunk two waves per CU deep in the order is at most a quarter as
+ * long), so their serial chains bound the launch; else XDMA.
  */
 int md5hip_plan_desc(const uint32_t *lens, uint64_t n, uint32_t *order);
 

@@ -41,7 +41,7 @@ def batch(K, seed0):
     return big, L, O, order, var
 
 
-def stats(rec, L, order, clk_hz=100e6):
+def stats(rec, L, order, clk_hz=100e6, persistent=False):
     hw, xcc, t0, t1 = rec[:, 0], rec[:, 1], rec[:, 2].astype(np.int64), rec[:, 3].astype(np.int64)
     base = t0.min()
     s, e = (t0 - base) / clk_hz * 1e3, (t1 - base) / clk_hz * 1e3        # ms
@@ -56,9 +56,13 @@ def stats(rec, L, order, clk_hz=100e6):
     np.maximum.at(end, inv, e)
     nw = np.bincount(inv)
     nwave = rec.shape[0]
+    q = lambda a: [round(float(x), 3) for x in np.quantile(a, [0, 0.1, 0.5, 0.9, 1.0])]
+    if persistent:
+        return {"waves": int(nwave), "simds_used": int(uniq.size), "span_ms": round(float(e.max()), 3),
+                "waves_per_simd_q": q(nw), "wave_end_ms_q": q(e), "groups_per_wave_q": q(rec[:, 4]),
+                "busy_frac": round(float((e - s).sum() / (nwave * e.max())), 3)}
     wave_max = np.array([L[order[64 * w:64 * w + 64]].max() for w in range(nwave)])
     longw = wave_max == (1 << 20)
-    q = lambda a: [round(float(x), 3) for x in np.quantile(a, [0, 0.1, 0.5, 0.9, 1.0])]
     return {"waves": int(nwave), "simds_used": int(uniq.size), "span_ms": round(float(e.max()), 3),
             "waves_per_simd_q": q(nw), "simd_busy_ms_q": q(busy), "simd_end_ms_q": q(end),
             "busy_sum_over_simds_x_span": round(float(busy.sum() / (uniq.size * e.max())), 3),
@@ -76,6 +80,7 @@ def main():
     D = ctypes.CDLL(DIAG)
     vp = ctypes.c_void_p
     D.md5diag_desc_x.argtypes = [ctypes.c_int, vp, vp, vp, vp, ctypes.c_uint64, vp, ctypes.c_uint32, vp, vp]
+    D.md5diag_desc_balanced.argtypes = [vp, vp, vp, vp, ctypes.c_uint64, vp, vp, vp]
     cus = torch.cuda.get_device_properties(0).multi_processor_count
     out = {}
     for K in a.batches:
@@ -100,17 +105,36 @@ def main():
                 e1.record()
                 torch.cuda.synchronize()
                 ms[k].append(e0.elapsed_time(e1))
+        for v in ("xdma", "hybrid", "balanced"):        # the product kernels themselves
+            ms["product_" + v] = []
+        for _ in range(a.rounds):
+            for v in ("xdma", "hybrid", "balanced"):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                m.digest_desc(big, dO, dL, dR, out=dig[0], variant=v)
+                e1.record()
+                torch.cuda.synchronize()
+                ms["product_" + v].append(e0.elapsed_time(e1))
         ref = m.digest_desc(big, dO, dL, dR, variant=var)
+        assert run(0) == 0
         same = {k: bool(torch.equal(dig[k], ref)) for k in range(3)}
         res = {"chunks": int(n), "payload_gib": round(float(L.sum()) / 2**30, 2), "planner": var,
                "ms": {name: [round(x, 3) for x in ms[k]] for k, name in
-                      ((0, "xdma"), (1, "hybrid_pair"), (2, "hybrid_nopair"))},
+                      ((0, "xdma"), (1, "hybrid_pair"), (2, "hybrid_nopair"), ("product_xdma", "product_xdma"),
+                       ("product_hybrid", "product_hybrid"), ("product_balanced", "product_balanced"))},
                "digests_equal_product": same}
         for k, name in ((0, "xdma"), (1, "hybrid_pair")):
             rec = torch.zeros(((n + 63) // 64, 4), dtype=torch.int64, device="cuda")
             assert run(k, rec) == 0
             torch.cuda.synchronize()
             res["trace_" + name] = stats(rec.cpu().numpy().astype(np.uint64), L, order)
+        recb = torch.zeros((4 * cus, 5), dtype=torch.int64, device="cuda")
+        digb = torch.empty((n, 16), dtype=torch.uint8, device="cuda")
+        assert D.md5diag_desc_balanced(big.data_ptr(), dO.data_ptr(), dL.data_ptr(), dR.data_ptr(), n,
+                                       digb.data_ptr(), recb.data_ptr(), st) == 0
+        torch.cuda.synchronize()
+        res["trace_balanced"] = stats(recb.cpu().numpy().astype(np.uint64), L, order, persistent=True)
+        res["balanced_equal_product"] = bool(torch.equal(digb, ref))
         out[f"K{K}"] = res
         del big, dO, dL, dR, dig
         torch.cuda.empty_cache()

@@ -593,6 +593,51 @@ md5_desc_hybrid(const uint8_t* __restrict__ base, const uint64_t* __restrict__ o
 }
 
 // ---------------------------------------------------------------------------
+// Descriptor batch, LPT-scheduled ("BALANCED"): a persistent grid of ONE wave
+// per SIMD (4-wave workgroups holding more than half a CU's LDS, so each CU
+// runs exactly one) pulls 64-chunk groups in longest-first order from a
+// device counter: list scheduling of the longest-processing-time order on
+// 4 x CUs machines.  For a mixed batch holding several waves of work per SIMD
+// (coalesced C3 submissions), the hardware's placement -- all waves resident
+// at once, ~5 per SIMD, a strided slice of the order on each -- leaves SIMDs
+// loaded unevenly: 1 MiB chains ran 2x their solo time sharing a SIMD and
+// SIMDs went idle from 54 % of the launch on (scripts/c3_trace_x.py,
+// profiles/r02_c3_trace.json).  Here every SIMD takes the next-longest group
+// whenever its wave frees up.  ctr[0] hands out groups, ctr[1] counts waves
+// done; the last wave out resets both, so a counter serves the next launch
+// on its stream (md5_kernels.hip keeps one per device and stream).
+// ---------------------------------------------------------------------------
+constexpr uint32_t kBalancedLds = 88u * 1024u;   // > 80 KiB: one workgroup per CU
+
+__global__ void __launch_bounds__(256)
+md5_desc_balanced(const uint8_t* __restrict__ base, const uint64_t* __restrict__ offs,
+                  const uint32_t* __restrict__ lens, const uint32_t* __restrict__ order, uint64_t n,
+                  uint4* __restrict__ out, uint32_t* __restrict__ ctr) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds_dyn[];   // kBalancedLds bytes
+  Md5Hasher<true> h;
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  uint8_t* img = lds_dyn + wave * 8192u;
+  const uint64_t ngroups = (n + 63) / 64;
+  const DescArrays src{offs, lens, order};
+  for (;;) {
+    uint32_t g = 0;
+    if (lane == 0) g = atomicAdd(&ctr[0], 1u);
+    g = __builtin_amdgcn_readfirstlane((uint32_t)__shfl((int)g, 0, 64));
+    if (g >= ngroups) break;
+    desc_xpose_group<2, Md5Hasher<true>, 0, 1, false, true, true>(h, base, src, n, (uint64_t)g * 64u,
+                                                                  out, img);
+  }
+  if (lane == 0) {
+    const uint32_t total = gridDim.x * (blockDim.x >> 6);
+    if (atomicAdd(&ctr[1], 1u) == total - 1u) {     // every wave has made its last grab
+      atomicExch(&ctr[0], 0u);
+      atomicExch(&ctr[1], 0u);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // CRC-32 batches (netcache blk_make_crc, blk_io.c:354-430), same loaders.
 // ---------------------------------------------------------------------------
 // XDMA16: the XPERM16 tables (64 KiB) beside twelve waves' full 8 KiB images

@@ -22,6 +22,7 @@ template __global__ void crc32_desc<true>(const uint8_t*, const uint64_t*, const
 #include <errno.h>
 #include <stdlib.h>
 #include <string.h>
+#include <map>
 #include <mutex>
 #include <vector>
 
@@ -54,6 +55,25 @@ int cu_count() {
       cus <= 0)
     return 256;
   return cus;
+}
+
+// BALANCED's self-resetting group counters: one pair per (device, stream),
+// allocated and zeroed on first use (launches on one stream are ordered, so
+// a counter reset by the last wave of launch k is zero for launch k+1).
+std::mutex g_ctr_mu;
+std::map<std::pair<int, hipStream_t>, uint32_t*> g_ctr;
+
+uint32_t* balanced_counter(hipStream_t s) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  std::lock_guard<std::mutex> lk(g_ctr_mu);
+  auto it = g_ctr.find({dev, s});
+  if (it != g_ctr.end()) return it->second;
+  uint32_t* c = nullptr;
+  if (hipMalloc(&c, 2 * sizeof(uint32_t)) != hipSuccess) return nullptr;
+  if (hipMemset(c, 0, 2 * sizeof(uint32_t)) != hipSuccess) { (void)hipFree(c); return nullptr; }
+  g_ctr[{dev, s}] = c;
+  return c;
 }
 
 // One workgroup of `threads` per CU, grid-stride over 64-chunk groups.
@@ -98,7 +118,7 @@ int md5hip_digest_desc_variant(const void* d_base, const uint64_t* d_offsets,
   if (!d_base || !d_offsets || !d_lens || !d_digests) return -EINVAL;
   if (((uintptr_t)d_digests & 15u) != 0) return -EINVAL;
   if (variant != MD5HIP_DESC_AUTO && variant != MD5HIP_DESC_LANE && variant != MD5HIP_DESC_HYBRID &&
-      variant != MD5HIP_DESC_XDMA)
+      variant != MD5HIP_DESC_XDMA && variant != MD5HIP_DESC_BALANCED)
     return -EINVAL;
   if (int e = device_ok()) return e;
   const uint64_t g = (n + 63) / 64;
@@ -110,6 +130,20 @@ int md5hip_digest_desc_variant(const void* d_base, const uint64_t* d_offsets,
     // run their chains lane-direct (md5hip_plan_desc picks HYBRID)
     hipLaunchKernelGGL(md5_desc_hybrid, dim3((uint32_t)g), dim3(64), 0, s, base, d_offsets, d_lens,
                        d_order, n, (uint4*)d_digests, (uint32_t)cu_count());
+    return launched();
+  }
+  if (variant == MD5HIP_DESC_BALANCED) {
+    uint32_t* ctr = balanced_counter(s);
+    if (!ctr) return -ENOMEM;
+    static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(md5_desc_balanced),
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                 (int)kBalancedLds) == hipSuccess;
+    if (!attr) return -ENODEV;
+    // the kernel resets its counter on exit; zero it on the stream anyway, so
+    // a launch that never finished (a fault) cannot poison the next one
+    if (hipMemsetAsync(ctr, 0, 2 * sizeof(uint32_t), s) != hipSuccess) return -EIO;
+    hipLaunchKernelGGL(md5_desc_balanced, dim3((uint32_t)cu_count()), dim3(256), kBalancedLds, s,
+                       base, d_offsets, d_lens, d_order, n, (uint4*)d_digests, ctr);
     return launched();
   }
   if (variant == MD5HIP_DESC_AUTO || variant == MD5HIP_DESC_XDMA) {
@@ -410,17 +444,29 @@ int md5hip_arena_free(void* ptr) {
   return rc;
 }
 
-// Planner for descriptor batches: the longest-first order, and HYBRID when
-// the first waves' chunks (>= 256 KiB) stand out from the batch -- the chunk
-// two waves per CU deep in the order is at most a quarter as long -- so that
-// their serial chains, not the bytes, bound the launch (a mixed C3 batch, or
-// fewer long chunks than two waves per CU); XDMA otherwise (equal-length
-// netcache blocks).  DESIGN.md §5, profiles/r01_desc_hybrid_ab.json.
+// Planner for descriptor batches (md5hip.h): the longest-first order, and
+//  - BALANCED for a mixed batch (longest chunk >= 256 KiB, median 64-chunk
+//    group <= 1/8 of it) holding >= 0.4 x (SIMDs x longest chain) of work:
+//    several waves per SIMD, where LPT placement beats the hardware's
+//    (coalesced C3 submissions, profiles/r02_c3_trace.json);
+//  - HYBRID when the longest chunks stand out -- the chunk two waves per CU
+//    deep in the order is at most a quarter as long -- so their serial chains
+//    bound the launch (one C3 batch; fewer long chunks than two waves per CU);
+//  - XDMA otherwise (equal-length netcache blocks).  DESIGN.md §5.
 int md5hip_plan_desc(const uint32_t* lens, uint64_t n, uint32_t* order) {
   if (int e = md5hip_plan_order(lens, n, order)) return e;
   if (n == 0) return MD5HIP_DESC_XDMA;
   const uint32_t bmax = lens[order[0]] >> 6;
   if (bmax < kHybridLongBlocks) return MD5HIP_DESC_XDMA;
+  const uint64_t ngroups = (n + 63) / 64;
+  const uint64_t median = (uint64_t)(lens[order[(ngroups / 2) * 64]] >> 6) + 1;
+  if (8u * median <= (uint64_t)bmax + 1) {
+    // work in block-steps: each group runs as long as its first (longest) lane
+    uint64_t total = 0;
+    for (uint64_t g = 0; g < ngroups; ++g) total += (uint64_t)(lens[order[g * 64]] >> 6) + 1;
+    const uint64_t simds = 4ull * (uint64_t)cu_count();
+    if (10u * total >= 4u * simds * ((uint64_t)bmax + 1)) return MD5HIP_DESC_BALANCED;
+  }
   const uint64_t depth = (uint64_t)cu_count() * 128u;
   const uint64_t p = depth < n - 1 ? depth : n - 1;
   return 4ull * (lens[order[p]] >> 6) <= bmax ? MD5HIP_DESC_HYBRID : MD5HIP_DESC_XDMA;

@@ -25,12 +25,20 @@
  *   7. MD5Init/Update/Final page by page (the per-message drop-in, §1)
  *   8. the device entry: blocks packed into a batch arena (md5hip_arena_alloc),
  *      order and kernel from md5hip_plan_desc, md5hip_digest_desc_variant
+ *   9. the same blocks from the arena through the device-input queue
+ *      (md5hip_queue_create, md5_batch_submit_device_async, §2h), digests to
+ *      host and to device memory, tickets waited in reverse order
+ *  10. MD5Init/Update/Final on one device context per block, one update per
+ *      16 KiB page (md5hip_*_ctx, §2i)
+ *  11. one batcher shared by four "ASIO" threads, each submitting its blocks
+ *      asynchronously and collecting its own tickets (§2, §2g)
  *
  * Exit 0 = all equal; 1 = a mismatch or error; 77 = no usable HIP device
  * (md5hip_batcher_create returned -ENODEV: the batched entries fail loudly,
  * they never fall back to the host).
  */
 #include <errno.h>
+#include <pthread.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -96,6 +104,36 @@ static uint64_t blk_segments(const fc_inode_t *inode, fc_blk_t *const *blks, int
     }
     first[nblk] = ns;
     return ns;
+}
+
+/* §11: one "ASIO" thread of a pool sharing one batcher */
+struct asio_job {
+    md5hip_batcher *b;
+    const struct md5hip_iov *segs;
+    const uint64_t *first;
+    int lo, hi, reps;
+    unsigned char (*want)[16];
+    int bad, rc;
+};
+
+static void *asio_thread(void *arg)
+{
+    struct asio_job *j = arg;
+    unsigned char dig[8][NBLK_MAX][16];
+    uint64_t tk[8];
+    uint64_t rebased[NBLK_MAX + 1];
+    for (int b = j->lo; b <= j->hi; b++) rebased[b - j->lo] = j->first[b] - j->first[j->lo];
+    for (int r = 0; r < j->reps; r++) {
+        const int rc = md5_batch_submit_iov_async(j->b, j->segs + j->first[j->lo], rebased,
+                                                  (uint64_t)(j->hi - j->lo), &dig[r][0][0], &tk[r]);
+        if (rc && !j->rc) j->rc = rc;
+    }
+    for (int r = j->reps - 1; r >= 0; r--) {        /* tickets in reverse: out-of-order completion */
+        const int rc = md5_batch_wait(j->b, tk[r]);
+        if (rc && !j->rc) j->rc = rc;
+        for (int b = j->lo; b < j->hi; b++) j->bad += memcmp(dig[r][b - j->lo], j->want[b], 16) != 0;
+    }
+    return NULL;
 }
 
 /* the block's bytes, gathered on the host for the oracle */
@@ -310,12 +348,94 @@ int main(void)
                   "digest copy");
             for (int b = 0; b < nblk; b++)
                 CHECK(memcmp(digest[b], want_md5[b], 16) == 0, "arena block %d", b);
+
+            /* 9. the device-input queue over the same arena */
+            md5hip_batcher *q = NULL;
+            rc = md5hip_queue_create(0, 0, 3, &q);
+            CHECK(rc == 0 && q, "md5hip_queue_create = %d", rc);
+            if (rc == 0) {
+                uint64_t addr[NBLK_MAX], t_h = 0, t_d = 0;
+                for (int b = 0; b < nblk; b++) addr[b] = (uint64_t)(uintptr_t)d_arena + offs[b];
+                memset(digest, 0, sizeof digest);
+                (void)hipMemset(d_dig, 0, 16 * NBLK_MAX);
+                rc = md5_batch_submit_device_async(q, addr, lens, (uint64_t)nblk, &digest[0][0], 0, &t_h);
+                CHECK(rc == 0, "submit_device_async(host digests) = %d", rc);
+                rc = md5_batch_submit_device_async(q, addr, lens, (uint64_t)nblk, d_dig, 1, &t_d);
+                CHECK(rc == 0, "submit_device_async(device digests) = %d", rc);
+                CHECK(md5_batch_wait(q, t_d) == 0 && md5_batch_wait(q, t_h) == 0, "queue waits");
+                for (int b = 0; b < nblk; b++)
+                    CHECK(memcmp(digest[b], want_md5[b], 16) == 0, "queue host digest %d", b);
+                memset(digest, 0, sizeof digest);
+                CHECK(hipMemcpy(digest, d_dig, 16 * (size_t)nblk, hipMemcpyDeviceToHost) == hipSuccess,
+                      "queue digest copy");
+                for (int b = 0; b < nblk; b++)
+                    CHECK(memcmp(digest[b], want_md5[b], 16) == 0, "queue device digest %d", b);
+                md5hip_batcher_destroy(q);
+            }
+
+            /* 10. one device context per block, one MD5Update per 16 KiB page */
+            void *d_ctx = NULL, *d_ptr = NULL, *d_pl = NULL;
+            ok = hipMalloc(&d_ctx, 88 * NBLK_MAX) == hipSuccess &&
+                 hipMalloc(&d_ptr, 8 * NBLK_MAX) == hipSuccess &&
+                 hipMalloc(&d_pl, 4 * NBLK_MAX) == hipSuccess;
+            CHECK(ok, "context buffers");
+            if (ok) {
+                CHECK(md5hip_init_ctx(d_ctx, (uint64_t)nblk, NULL) == 0, "md5hip_init_ctx");
+                for (unsigned p = 0; p < PAGES_PER_BLOCK; p++) {
+                    uint64_t ptr[NBLK_MAX];
+                    uint32_t pl[NBLK_MAX];
+                    for (int b = 0; b < nblk; b++) {
+                        const long long rem = (long long)lens[b] - (long long)p * NC_PAGE_SIZE;
+                        pl[b] = rem <= 0 ? 0u : rem < NC_PAGE_SIZE ? (uint32_t)rem : NC_PAGE_SIZE;
+                        ptr[b] = (uint64_t)(uintptr_t)d_arena + offs[b] + (uint64_t)p * NC_PAGE_SIZE;
+                    }
+                    CHECK(hipMemcpy(d_ptr, ptr, 8 * (size_t)nblk, hipMemcpyHostToDevice) == hipSuccess &&
+                          hipMemcpy(d_pl, pl, 4 * (size_t)nblk, hipMemcpyHostToDevice) == hipSuccess,
+                          "page descriptors");
+                    CHECK(md5hip_update_ctx(d_ctx, (const void *const *)d_ptr, d_pl, (uint64_t)nblk,
+                                            NULL) == 0, "md5hip_update_ctx page %u", p);
+                }
+                CHECK(md5hip_final_ctx(d_ctx, (uint64_t)nblk, d_dig, NULL) == 0, "md5hip_final_ctx");
+                memset(digest, 0, sizeof digest);
+                CHECK(hipMemcpy(digest, d_dig, 16 * (size_t)nblk, hipMemcpyDeviceToHost) == hipSuccess,
+                      "ctx digest copy");
+                for (int b = 0; b < nblk; b++)
+                    CHECK(memcmp(digest[b], want_md5[b], 16) == 0, "context block %d", b);
+            }
+            (void)hipFree(d_ctx);
+            (void)hipFree(d_ptr);
+            (void)hipFree(d_pl);
         }
         (void)hipFree(d_off);
         (void)hipFree(d_len);
         (void)hipFree(d_ord);
         (void)hipFree(d_dig);
         if (d_arena) CHECK(md5hip_arena_free(d_arena) == 0, "md5hip_arena_free");
+    }
+
+    /* 11. four "ASIO" threads share one batcher */
+    {
+        md5hip_batcher *shared = NULL;
+        rc = md5hip_batcher_create(0, 16u << 20, 4, &shared);
+        CHECK(rc == 0 && shared, "shared batcher = %d", rc);
+        if (rc == 0) {
+            struct asio_job jobs[4];
+            pthread_t th[4];
+            for (int t = 0; t < 4; t++) {
+                jobs[t] = (struct asio_job){shared, segs, first, t * nblk / 4, (t + 1) * nblk / 4, 8,
+                                            want_md5, 0, 0};
+                CHECK(pthread_create(&th[t], NULL, asio_thread, &jobs[t]) == 0, "pthread_create");
+            }
+            for (int t = 0; t < 4; t++) {
+                pthread_join(th[t], NULL);
+                CHECK(jobs[t].rc == 0 && jobs[t].bad == 0, "asio thread %d: rc %d, %d bad", t,
+                      jobs[t].rc, jobs[t].bad);
+            }
+            struct md5hip_batcher_stats st;
+            CHECK(md5hip_batcher_get_stats(shared, &st) == 0 && st.submissions == 32,
+                  "shared batcher stats");
+            md5hip_batcher_destroy(shared);
+        }
     }
 
     free(tmp);
@@ -325,7 +445,8 @@ int main(void)
         return 1;
     }
     printf("netcache_site ok: %d blocks (%llu bytes, %d pages scattered), MD5 / CRC-32 / fastcrc / "
-           "verify / async / zero-copy x3 / pool / MD5Init-Update-Final / arena+plan bit-exact vs oracle\n",
+           "verify / async / zero-copy x3 / pool / MD5Init-Update-Final / arena+plan / device queue / "
+           "device contexts / shared batcher x4 threads bit-exact vs oracle\n",
            nblk, (unsigned long long)inode.size, npages);
     return 0;
 }

@@ -176,3 +176,33 @@ def test_arena_freed_right_after_async_launch(cuda):
         torch.cuda.synchronize()
         host = gen.synthetic_bytes(n * L, 70 + k)
         assert np.array_equal(out.cpu().numpy(), gen.oracle_digests_fixed(host, n, L)), k
+
+
+def test_planner_balanced_for_coalesced_mixed_batches(cuda):
+    """Three C3 batches coalesced: the planner picks BALANCED (LPT over one
+    wave per SIMD); its digests equal the oracle on a sample and the other
+    descriptor kernels on the whole batch; two launches back to back on one
+    stream reuse the self-resetting group counter."""
+    import sys
+    sys.path.insert(0, gen.REPO)
+    import bench
+    lk = [bench.c3_lens(2 << 30, 70 + j) for j in range(3)]
+    L = np.concatenate(lk)
+    offs = np.concatenate([[0], np.cumsum((L + 15) // 16 * 16)[:-1]])
+    total = int(offs[-1] + L[-1] + 64)
+    data = torch.empty(total, dtype=torch.uint8, device=cuda)
+    m.fill_synthetic(data[: total // 16 * 16], seed=0xBA1)
+    order, var = m.plan_desc(L.astype(np.uint32))
+    assert var == "balanced"
+    args = (data, torch.from_numpy(offs).to(cuda), torch.from_numpy(L.astype(np.int32)).to(cuda),
+            torch.from_numpy(order.astype(np.int32)).to(cuda))
+    a = m.digest_desc(*args, variant="balanced")
+    b = m.digest_desc(*args, variant="balanced")
+    for v in ("xdma", "hybrid", "lane"):
+        assert torch.equal(m.digest_desc(*args, variant=v), a), v
+    assert torch.equal(a, b)
+    idx = np.unique(np.concatenate([order[:300], order[-300:],
+                                    np.random.default_rng(4).integers(0, L.size, 600)]))
+    host = data.cpu().numpy()
+    want = gen.oracle_digests(host, offs[idx], L[idx])
+    assert np.array_equal(a.cpu().numpy()[idx], want)
