@@ -54,7 +54,7 @@ def parse_args(argv):
     p.add_argument("--warmup", type=int, default=20,
                    help="untimed launches first: the board settles its clock over the first ~15 "
                         "launches of a 3 ms kernel (slow start, profiles/r01_bench_kernel_trace_startup.json)")
-    p.add_argument("--config", default="c2", choices=["c2", "c3", "c3q", "c5", "crc"])
+    p.add_argument("--config", default="c2", choices=["c2", "c3", "c3q", "c5", "crc", "ctx"])
     p.add_argument("--chunks", type=int, default=0,
                    help="chunks per GPU (weak scaling); 0 = 1,048,576 (C2) at N=1, "
                         "2,097,152 (the C4 shard) at N>1")
@@ -749,6 +749,51 @@ def run_c3q(a, rank, world, local, device, backend):
     return per_rank_line(res, rank, world, local, device, backend, payload * a.steps, wall, par)
 
 
+def run_ctx(a, rank, world, local, device, backend):
+    """Batched MD5Update on caller contexts (md5hip_update_ctx): one context
+    per object, each step appends the next 16 KiB block of every object (the
+    netcache streaming shape: objects arriving block by block).  A step = one
+    md5hip_update_ctx launch over all contexts; MD5Final after timing."""
+    import numpy as np
+    L = a.len
+    n = a.chunks or (1 << 20)
+    data = torch.empty(n * L, dtype=torch.uint8, device="cuda")
+    m.fill_synthetic(data, seed=0x5EED0000 + rank)
+    ctx = torch.zeros((n, 88), dtype=torch.uint8, device="cuda")
+    m.init_ctx(ctx)
+    ptrs = torch.arange(n, dtype=torch.int64, device="cuda") * L + data.data_ptr()
+    lens = torch.full((n,), L, dtype=torch.int32, device="cuda")
+    fn = lambda: m.update_ctx(ctx, ptrs, lens)  # noqa: E731
+    wall, dev_ms = timed_steps(fn, a.steps, a.warmup, world)
+    wall_max = max_over_ranks(wall, world)
+    dev_ms_max = max_over_ranks(dev_ms, world)
+    dig = m.final_ctx(ctx)
+    # parity: each object hashed (warmup + steps) times its block -> the same
+    # digest as MD5 over the block repeated; checked on a sample by the host reference
+    par = None
+    if a.parity_sample:
+        k = min(n, max(16, a.parity_sample // 64))
+        idx = np.unique(np.concatenate([[0, n - 1], np.random.default_rng(5).integers(0, n, k)]))
+        rows = data.view(n, L)[torch.from_numpy(idx).to(data.device)].cpu().numpy()
+        reps = a.warmup + a.steps
+        rep = np.tile(rows, (1, reps)).reshape(-1)
+        par = check_sample(rep, np.arange(idx.size, dtype=np.int64) * L * reps,
+                           np.full(idx.size, L * reps), dig.index_select(0, torch.from_numpy(idx).to(dig.device)).cpu().numpy())
+    alg = float(n) * (L + 2 * 88)
+    achieved = alg / (dev_ms_max * 1e-3) / 1e9
+    res = {"metric": "device-resident batched MD5Update GiB/s (md5hip_update_ctx, 16 KiB per context per call)",
+           "value": round(float(n) * L * world * a.steps / wall_max / GIB, 2), "unit": "GiB/s",
+           "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+           "ms_per_step": round(wall_max / a.steps * 1e3, 4), "higher_is_better": True, "scaling": "weak",
+           "vs_baseline": None, "dtype": "u32", "data": "synthetic",
+           "config": {"workload": f"{n} contexts x {L} B per update", "contexts": n, "update_bytes": L},
+           "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": round(achieved / HBM_PEAK_GBS, 4), "kernel": "md5hip::md5_update_ctx",
+                        "avg_launch_ms": round(dev_ms_max, 4), "alg_bytes_per_launch": int(alg),
+                        "alg_bytes_note": "block bytes + the 88-B context read and written", "traffic": None}}
+    return per_rank_line(res, rank, world, local, device, backend, float(n) * L * a.steps, wall, par)
+
+
 def run_c5(a, rank, world, local, device, backend):
     """End to end from pinned host memory: H2D -> MD5 -> D2H over pipelined
     batcher slots (md5hip_batch_host_fixed)."""
@@ -817,8 +862,8 @@ def main(argv=None):
     if a.dry_run:
         res = run_dry(a, rank, world, local, device, backend)
     else:
-        res = {"c2": run_c2, "c3": run_c3, "c3q": run_c3q, "c5": run_c5,
-               "crc": run_crc}[a.config](a, rank, world, local, device, backend)
+        res = {"c2": run_c2, "c3": run_c3, "c3q": run_c3q, "c5": run_c5, "crc": run_crc,
+               "ctx": run_ctx}[a.config](a, rank, world, local, device, backend)
     if rank == 0 and world == 1 and not a.dry_run and not a.no_cpu_baseline:
         if a.config == "c2":
             res["cpu_baseline"] = cpu_baseline()

@@ -15,5 +15,7 @@ for f in 1 2; do
   echo "c3q inflight $f rc=$r"; cut -c1-330 $O/c3q_f$f.json; [ $r -eq 0 ] || exit $r
 done
 timeout -k 10 400 python bench.py --config c3 --steps 10 --warmup 3 > $O/c3.json 2> $O/c3.err; r=$?
-cut -c1-300 $O/c3.json
+cut -c1-300 $O/c3.json; [ $r -eq 0 ] || exit $r
+timeout -k 10 300 python bench.py --config ctx --steps 20 --warmup 5 > $O/ctx.json 2> $O/ctx.err; r=$?
+cut -c1-400 $O/ctx.json
 exit $r

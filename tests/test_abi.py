@@ -204,3 +204,22 @@ def test_pool_plan_partitions_by_bytes():
     assert L.md5hip_pool_plan(None, 5, 0, (ctypes.c_uint64 * 2)()) == EINVAL
     h = ctypes.c_void_p()
     assert L.md5hip_pool_create(None, 0, 0, 0, ctypes.byref(h)) == EINVAL
+
+
+def test_plan_desc_picks_balanced_for_coalesced_mixed_batches():
+    """BALANCED (LPT over one wave per SIMD) for mixed batches holding several
+    waves of work per SIMD -- coalesced C3 submissions -- but not for one C3
+    batch (chain-bound: HYBRID) nor for equal-length netcache blocks (XDMA)."""
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    one = bench.c3_lens(16 << 30, 1000).astype(np.uint32)
+    assert m.plan_desc(one)[1] == "hybrid"
+    three = np.concatenate([bench.c3_lens(16 << 30, 3000 + 31 * j) for j in range(3)]).astype(np.uint32)
+    order, v = m.plan_desc(three)
+    assert v == "balanced" and np.array_equal(order, m.plan_order(three))
+    five = np.concatenate([bench.c3_lens(16 << 30, 3000 + 31 * j) for j in range(5)]).astype(np.uint32)
+    assert m.plan_desc(five)[1] == "balanced"
+    big_uniform = np.full(1 << 20, 16384, np.uint32)
+    big_uniform[::8] = 100
+    assert m.plan_desc(big_uniform)[1] == "xdma"

@@ -178,11 +178,12 @@ def test_arena_freed_right_after_async_launch(cuda):
         assert np.array_equal(out.cpu().numpy(), gen.oracle_digests_fixed(host, n, L)), k
 
 
-def test_planner_balanced_for_coalesced_mixed_batches(cuda):
-    """Three C3 batches coalesced: the planner picks BALANCED (LPT over one
-    wave per SIMD); its digests equal the oracle on a sample and the other
-    descriptor kernels on the whole batch; two launches back to back on one
-    stream reuse the self-resetting group counter."""
+def test_balanced_on_coalesced_mixed_batches(cuda):
+    """BALANCED (LPT over one wave per SIMD) on three coalesced C3-shaped
+    batches: digests equal the oracle on a sample and the other descriptor
+    kernels on the whole batch; two launches back to back on one stream reuse
+    the self-resetting group counter.  (The planner's choice of BALANCED at
+    the bench's sizes is tests/test_abi.py::test_planner_choices.)"""
     import sys
     sys.path.insert(0, gen.REPO)
     import bench
@@ -192,8 +193,7 @@ def test_planner_balanced_for_coalesced_mixed_batches(cuda):
     total = int(offs[-1] + L[-1] + 64)
     data = torch.empty(total, dtype=torch.uint8, device=cuda)
     m.fill_synthetic(data[: total // 16 * 16], seed=0xBA1)
-    order, var = m.plan_desc(L.astype(np.uint32))
-    assert var == "balanced"
+    order, _ = m.plan_desc(L.astype(np.uint32))
     args = (data, torch.from_numpy(offs).to(cuda), torch.from_numpy(L.astype(np.int32)).to(cuda),
             torch.from_numpy(order.astype(np.int32)).to(cuda))
     a = m.digest_desc(*args, variant="balanced")
