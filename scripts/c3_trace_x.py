@@ -80,7 +80,8 @@ def main():
     D = ctypes.CDLL(DIAG)
     vp = ctypes.c_void_p
     D.md5diag_desc_x.argtypes = [ctypes.c_int, vp, vp, vp, vp, ctypes.c_uint64, vp, ctypes.c_uint32, vp, vp]
-    D.md5diag_desc_balanced.argtypes = [vp, vp, vp, vp, ctypes.c_uint64, vp, vp, vp]
+    D.md5diag_desc_balanced.argtypes = [ctypes.c_int, vp, vp, vp, vp, ctypes.c_uint64, vp, vp, vp]
+    BAL = {0: "bal_w4_nb2", 1: "bal_w4_nb1", 2: "bal_w8_nb2", 3: "bal_w8_nb1"}
     cus = torch.cuda.get_device_properties(0).multi_processor_count
     out = {}
     for K in a.batches:
@@ -115,26 +116,41 @@ def main():
                 e1.record()
                 torch.cuda.synchronize()
                 ms["product_" + v].append(e0.elapsed_time(e1))
+        digb = torch.empty((n, 16), dtype=torch.uint8, device="cuda")
+        runb = lambda k, rec=None: D.md5diag_desc_balanced(k, big.data_ptr(), dO.data_ptr(), dL.data_ptr(),  # noqa
+                                                          dR.data_ptr(), n, digb.data_ptr(),
+                                                          rec.data_ptr() if rec is not None else None, st)
+        for k in BAL:
+            assert runb(k) == 0
+            ms[BAL[k]] = []
+        for _ in range(a.rounds):
+            for k in BAL:
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                runb(k)
+                e1.record()
+                torch.cuda.synchronize()
+                ms[BAL[k]].append(e0.elapsed_time(e1))
         ref = m.digest_desc(big, dO, dL, dR, variant=var)
         assert run(0) == 0
         same = {k: bool(torch.equal(dig[k], ref)) for k in range(3)}
         res = {"chunks": int(n), "payload_gib": round(float(L.sum()) / 2**30, 2), "planner": var,
                "ms": {name: [round(x, 3) for x in ms[k]] for k, name in
                       ((0, "xdma"), (1, "hybrid_pair"), (2, "hybrid_nopair"), ("product_xdma", "product_xdma"),
-                       ("product_hybrid", "product_hybrid"), ("product_balanced", "product_balanced"))},
+                       ("product_hybrid", "product_hybrid"), ("product_balanced", "product_balanced"))
+                      + tuple((v, v) for v in BAL.values())},
                "digests_equal_product": same}
         for k, name in ((0, "xdma"), (1, "hybrid_pair")):
             rec = torch.zeros(((n + 63) // 64, 4), dtype=torch.int64, device="cuda")
             assert run(k, rec) == 0
             torch.cuda.synchronize()
             res["trace_" + name] = stats(rec.cpu().numpy().astype(np.uint64), L, order)
-        recb = torch.zeros((4 * cus, 5), dtype=torch.int64, device="cuda")
-        digb = torch.empty((n, 16), dtype=torch.uint8, device="cuda")
-        assert D.md5diag_desc_balanced(big.data_ptr(), dO.data_ptr(), dL.data_ptr(), dR.data_ptr(), n,
-                                       digb.data_ptr(), recb.data_ptr(), st) == 0
-        torch.cuda.synchronize()
-        res["trace_balanced"] = stats(recb.cpu().numpy().astype(np.uint64), L, order, persistent=True)
-        res["balanced_equal_product"] = bool(torch.equal(digb, ref))
+        for k in (0, 2):
+            recb = torch.zeros(((8 if k >= 2 else 4) * cus, 5), dtype=torch.int64, device="cuda")
+            assert runb(k, recb) == 0
+            torch.cuda.synchronize()
+            res["trace_" + BAL[k]] = stats(recb.cpu().numpy().astype(np.uint64), L, order, persistent=True)
+            res[BAL[k] + "_equal_product"] = bool(torch.equal(digb, ref))
         out[f"K{K}"] = res
         del big, dO, dL, dR, dig
         torch.cuda.empty_cache()

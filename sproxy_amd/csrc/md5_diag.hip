@@ -1059,11 +1059,12 @@ extern "C" int md5diag_desc_x(int kind, const void* base, const uint64_t* offs, 
   return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }
 
-// md5_desc_balanced with the per-wave record of md5diag_desc_x (one record
-// per persistent wave: its whole run over the groups it took) plus the number
-// of groups each wave took.
+// md5_desc_balanced_t with the per-wave record of md5diag_desc_x (one record
+// per persistent wave: its whole run over the groups it took, and how many)
+// for WPB waves per workgroup and NB LDS-DMA images per wave (A/B).
 namespace md5hip {
-__global__ void __launch_bounds__(256)
+template <int WPB, int NB>
+__global__ void __launch_bounds__(64 * WPB)
 diag_desc_balanced(const uint8_t* __restrict__ base, const uint64_t* __restrict__ offs,
                    const uint32_t* __restrict__ lens, const uint32_t* __restrict__ order, uint64_t n,
                    uint4* __restrict__ out, uint32_t* __restrict__ ctr, uint64_t* __restrict__ rec) {
@@ -1072,7 +1073,7 @@ diag_desc_balanced(const uint8_t* __restrict__ base, const uint64_t* __restrict_
   Md5Hasher<true> h;
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  uint8_t* img = lds_dyn + wave * 8192u;
+  uint8_t* img = lds_dyn + wave * 16384u;
   const uint64_t ngroups = (n + 63) / 64;
   const DescArrays src{offs, lens, order};
   uint32_t taken = 0;
@@ -1082,15 +1083,15 @@ diag_desc_balanced(const uint8_t* __restrict__ base, const uint64_t* __restrict_
     g = __builtin_amdgcn_readfirstlane((uint32_t)__shfl((int)g, 0, 64));
     if (g >= ngroups) break;
     ++taken;
-    desc_xpose_group<2, Md5Hasher<true>, 0, 1, false, true, true>(h, base, src, n, (uint64_t)g * 64u,
-                                                                  out, img);
+    desc_xpose_group<2, Md5Hasher<true>, 0, 1, false, true, true, DescArrays, true, NB>(
+        h, base, src, n, (uint64_t)g * 64u, out, img);
   }
   const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
-  if (lane == 0) {
+  if (lane == 0 && rec) {
     uint32_t hw, xcc;
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-    const uint64_t w = (uint64_t)blockIdx.x * 4u + wave;
+    const uint64_t w = (uint64_t)blockIdx.x * WPB + wave;
     rec[5 * w + 0] = hw;
     rec[5 * w + 1] = xcc;
     rec[5 * w + 2] = t0;
@@ -1100,19 +1101,36 @@ diag_desc_balanced(const uint8_t* __restrict__ base, const uint64_t* __restrict_
 }
 }  // namespace md5hip
 
-// rec: 5 x uint64 per wave, 4 x CUs waves
-extern "C" int md5diag_desc_balanced(const void* base, const uint64_t* offs, const uint32_t* lens,
-                                     const uint32_t* order, uint64_t n, void* out, void* rec,
-                                     void* stream) {
+namespace {
+template <int WPB, int NB>
+int diag_launch_balanced(const void* base, const uint64_t* offs, const uint32_t* lens,
+                         const uint32_t* order, uint64_t n, void* out, uint32_t* ctr, void* rec,
+                         hipStream_t s) {
+  const uint32_t lds = BalancedCfg<WPB>::kLds;
+  if (hipFuncSetAttribute(reinterpret_cast<const void*>(diag_desc_balanced<WPB, NB>),
+                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+    return -ENODEV;
+  hipLaunchKernelGGL((diag_desc_balanced<WPB, NB>), dim3((uint32_t)diag_cus()), dim3(64 * WPB), lds, s,
+                     (const uint8_t*)base, offs, lens, order, n, (uint4*)out, ctr, (uint64_t*)rec);
+  return hipGetLastError() == hipSuccess ? 0 : -EIO;
+}
+}  // namespace
+
+// rec: 5 x uint64 per wave (WPB x CUs waves), or nullptr.  kind: 0 = 4 waves
+// per WG / 2 images (the product's shape), 1 = 4 / 1, 2 = 8 / 2, 3 = 8 / 1.
+extern "C" int md5diag_desc_balanced(int kind, const void* base, const uint64_t* offs,
+                                     const uint32_t* lens, const uint32_t* order, uint64_t n,
+                                     void* out, void* rec, void* stream) {
   if (n == 0) return 0;
   static uint32_t* ctr = nullptr;
   if (!ctr && hipMalloc(&ctr, 8) != hipSuccess) return -ENOMEM;
   hipStream_t s = (hipStream_t)stream;
   if (hipMemsetAsync(ctr, 0, 8, s) != hipSuccess) return -EIO;
-  if (hipFuncSetAttribute(reinterpret_cast<const void*>(diag_desc_balanced),
-                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)kBalancedLds) != hipSuccess)
-    return -ENODEV;
-  hipLaunchKernelGGL(diag_desc_balanced, dim3((uint32_t)diag_cus()), dim3(256), kBalancedLds, s,
-                     (const uint8_t*)base, offs, lens, order, n, (uint4*)out, ctr, (uint64_t*)rec);
-  return hipGetLastError() == hipSuccess ? 0 : -EIO;
+  switch (kind) {
+    case 0: return diag_launch_balanced<4, 2>(base, offs, lens, order, n, out, ctr, rec, s);
+    case 1: return diag_launch_balanced<4, 1>(base, offs, lens, order, n, out, ctr, rec, s);
+    case 2: return diag_launch_balanced<8, 2>(base, offs, lens, order, n, out, ctr, rec, s);
+    case 3: return diag_launch_balanced<8, 1>(base, offs, lens, order, n, out, ctr, rec, s);
+    default: return -EINVAL;
+  }
 }

@@ -409,8 +409,11 @@ __device__ __forceinline__ void emit(H& h, typename H::Out* __restrict__ out, ui
 // kLongPair: HYBRID's lane-direct long waves refill their 8-block ring two
 // blocks (one whole 128-B line) at a time, so no lane leaves half a line
 // behind to be fetched again after eviction (ring_steps).
+// NB (kDma): LDS-DMA images per wave.  2: `img` holds two 8 KiB images and
+// the DMA of stage s+2 is issued as soon as stage s is read, so a lone wave
+// on its SIMD (BALANCED) keeps a stage in flight under each compression.
 template <int CP, class H, uint32_t kLong = 0, int D = 1, bool kHalf = false, bool kPeel = true,
-          bool kDma = false, class Src = DescArrays, bool kLongPair = true>
+          bool kDma = false, class Src = DescArrays, bool kLongPair = true, int NB = 1>
 __device__ __forceinline__ void desc_xpose_group(H& h, const uint8_t* __restrict__ base,
                                                  const Src& src, uint64_t n,
                                                  uint64_t first, typename H::Out* __restrict__ out,
@@ -429,6 +432,7 @@ __device__ __forceinline__ void desc_xpose_group(H& h, const uint8_t* __restrict
   if (bmax >= 4096u) __builtin_amdgcn_s_setprio(3);      // as desc_body
   else if (bmax >= 1024u) __builtin_amdgcn_s_setprio(2);
   else if (bmax >= 256u) __builtin_amdgcn_s_setprio(1);
+  else __builtin_amdgcn_s_setprio(0);                    // (a persistent wave's previous group)
   typename H::State st = h.init();
   const bool unaligned = __ballot(live && (((uintptr_t)chunk & 15u) != 0)) != 0;
   if (kLong && bmax >= kLong && (first >> 6) < nlong) {
@@ -507,7 +511,38 @@ __device__ __forceinline__ void desc_xpose_group(H& h, const uint8_t* __restrict
         h.block(st, w[1]);
       }
     };
-    if constexpr (kDma) {
+    if constexpr (kDma && NB == 2) {
+      static_assert(D == 1 && !kHalf, "LDS-DMA images: full 8 KiB stages");
+      auto issue = [&](uint32_t stg) __attribute__((always_inline)) {
+        uint8_t* im = img + (stg & 1u) * 8192u;
+#pragma unroll
+        for (int r = 0; r < 8; ++r)
+          __builtin_amdgcn_global_load_lds(rptr[r] + (min(stg, rlast[r]) << 7), im + r * 1024,
+                                           16, 0, CP);
+      };
+      issue(0);
+      if (smax > 1) issue(1);
+      for (uint32_t stg = 0; stg < smax; ++stg) {
+        // stage stg's 8 loads are done once at most the next stage's 8 are
+        // outstanding (loads complete in issue order)
+        if (stg + 1 < smax) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        uint4 w[2][4];
+        const uint8_t* row = myrow + (stg & 1u) * 8192u;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          const u32x4 v = *reinterpret_cast<const u32x4*>(row + ((q ^ g) * 16));
+          w[q >> 2][q & 3] = make_uint4(v.x, v.y, v.z, v.w);
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // reads done before the refill
+        if (stg + 2 < smax) issue(stg + 2);
+        __builtin_amdgcn_sched_barrier(0);
+        if (stg < nst) {
+          h.block(st, w[0]);
+          h.block(st, w[1]);
+        }
+      }
+    } else if constexpr (kDma) {
       static_assert(D == 1 && !kHalf, "LDS-DMA image: one full 8 KiB stage");
       auto issue = [&](uint32_t stg) __attribute__((always_inline)) {
 #pragma unroll
@@ -607,17 +642,25 @@ md5_desc_hybrid(const uint8_t* __restrict__ base, const uint64_t* __restrict__ o
 // done; the last wave out resets both, so a counter serves the next launch
 // on its stream (md5_kernels.hip keeps one per device and stream).
 // ---------------------------------------------------------------------------
-constexpr uint32_t kBalancedLds = 88u * 1024u;   // > 80 KiB: one workgroup per CU
+// WPB waves per workgroup (one per SIMD at 4, two at 8), each with two 8 KiB
+// LDS-DMA images; the workgroup asks for more than half the CU's LDS, so a CU
+// runs exactly one.
+template <int WPB>
+struct BalancedCfg {
+  static constexpr uint32_t kLds = WPB * 16384u > 81920u ? WPB * 16384u : 81920u + 16384u;
+};
+constexpr uint32_t kBalancedWaves = 4;
 
-__global__ void __launch_bounds__(256)
-md5_desc_balanced(const uint8_t* __restrict__ base, const uint64_t* __restrict__ offs,
-                  const uint32_t* __restrict__ lens, const uint32_t* __restrict__ order, uint64_t n,
-                  uint4* __restrict__ out, uint32_t* __restrict__ ctr) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t lds_dyn[];   // kBalancedLds bytes
+template <int WPB>
+__global__ void __launch_bounds__(64 * WPB)
+md5_desc_balanced_t(const uint8_t* __restrict__ base, const uint64_t* __restrict__ offs,
+                    const uint32_t* __restrict__ lens, const uint32_t* __restrict__ order, uint64_t n,
+                    uint4* __restrict__ out, uint32_t* __restrict__ ctr) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds_dyn[];   // BalancedCfg<WPB>::kLds
   Md5Hasher<true> h;
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  uint8_t* img = lds_dyn + wave * 8192u;
+  uint8_t* img = lds_dyn + wave * 16384u;
   const uint64_t ngroups = (n + 63) / 64;
   const DescArrays src{offs, lens, order};
   for (;;) {
@@ -625,8 +668,8 @@ md5_desc_balanced(const uint8_t* __restrict__ base, const uint64_t* __restrict__
     if (lane == 0) g = atomicAdd(&ctr[0], 1u);
     g = __builtin_amdgcn_readfirstlane((uint32_t)__shfl((int)g, 0, 64));
     if (g >= ngroups) break;
-    desc_xpose_group<2, Md5Hasher<true>, 0, 1, false, true, true>(h, base, src, n, (uint64_t)g * 64u,
-                                                                  out, img);
+    desc_xpose_group<2, Md5Hasher<true>, 0, 1, false, true, true, DescArrays, true, 2>(
+        h, base, src, n, (uint64_t)g * 64u, out, img);
   }
   if (lane == 0) {
     const uint32_t total = gridDim.x * (blockDim.x >> 6);

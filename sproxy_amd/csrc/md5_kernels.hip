@@ -135,14 +135,16 @@ int md5hip_digest_desc_variant(const void* d_base, const uint64_t* d_offsets,
   if (variant == MD5HIP_DESC_BALANCED) {
     uint32_t* ctr = balanced_counter(s);
     if (!ctr) return -ENOMEM;
-    static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(md5_desc_balanced),
+    constexpr int W = (int)kBalancedWaves;
+    constexpr uint32_t lds = BalancedCfg<W>::kLds;
+    static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(md5_desc_balanced_t<W>),
                                                  hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                 (int)kBalancedLds) == hipSuccess;
+                                                 (int)lds) == hipSuccess;
     if (!attr) return -ENODEV;
     // the kernel resets its counter on exit; zero it on the stream anyway, so
     // a launch that never finished (a fault) cannot poison the next one
     if (hipMemsetAsync(ctr, 0, 2 * sizeof(uint32_t), s) != hipSuccess) return -EIO;
-    hipLaunchKernelGGL(md5_desc_balanced, dim3((uint32_t)cu_count()), dim3(256), kBalancedLds, s,
+    hipLaunchKernelGGL(md5_desc_balanced_t<W>, dim3((uint32_t)cu_count()), dim3(64 * W), lds, s,
                        base, d_offsets, d_lens, d_order, n, (uint4*)d_digests, ctr);
     return launched();
   }

@@ -206,3 +206,36 @@ def test_balanced_on_coalesced_mixed_batches(cuda):
     host = data.cpu().numpy()
     want = gen.oracle_digests(host, offs[idx], L[idx])
     assert np.array_equal(a.cpu().numpy()[idx], want)
+
+
+def test_zero_copy_adjacent_registrations(cuda):
+    """Two adjacent host ranges registered separately (two pinned
+    allocations) and blocks whose pages run across the boundary: the DMA
+    gather list never merges a copy over two registrations, and
+    every gather mode returns the oracle digests."""
+    buf = np.frombuffer(gen.xorshift_bytes(4 << 20, seed=77), np.uint8).copy()
+    base = buf.ctypes.data
+    cut = ((base + (2 << 20) + 4095) & ~4095) - base          # page-aligned split point
+    lo, hi = buf[:cut], buf[cut:]
+    page = 16384
+    blocks = []
+    for k in range(24):                                        # pages straddling the boundary
+        s0 = cut - (k + 1) * 4096
+        blocks.append([buf[s0:s0 + page], buf[s0 + page:s0 + 2 * page]])
+    joined = [b"".join(x.tobytes() for x in segs) for segs in blocks]
+    arena = np.frombuffer(b"".join(joined) + b"\0", np.uint8)
+    lens = [len(j) for j in joined]
+    want = gen.oracle_digests(arena, np.cumsum([0] + lens[:-1]), lens)
+    m.register_host(lo)
+    m.register_host(hi)
+    try:
+        with m.Batcher(device=0, slice_bytes=1 << 20, nslots=2) as b:
+            for mode in (b.GATHER_DMA, b.GATHER_DEVICE, b.GATHER_AUTO, b.GATHER_HOST):
+                b.set_gather(mode)
+                assert np.array_equal(b.submit_iov(blocks), want), mode
+                flat = [buf[cut - 3 * page: cut + 3 * page]]     # one segment over both ranges
+                got = b.submit(flat)
+                assert bytes(got[0]) == bytes(gen.oracle_digests(buf, [cut - 3 * page], [6 * page])[0])
+    finally:
+        m.unregister_host(lo)
+        m.unregister_host(hi)
