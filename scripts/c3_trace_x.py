@@ -81,7 +81,7 @@ def main():
     vp = ctypes.c_void_p
     D.md5diag_desc_x.argtypes = [ctypes.c_int, vp, vp, vp, vp, ctypes.c_uint64, vp, ctypes.c_uint32, vp, vp]
     D.md5diag_desc_balanced.argtypes = [ctypes.c_int, vp, vp, vp, vp, ctypes.c_uint64, vp, vp, vp]
-    BAL = {0: "bal_w4_nb2", 1: "bal_w4_nb1", 2: "bal_w8_nb2", 3: "bal_w8_nb1"}
+    BAL = {0: "bal_w4_nb1", 1: "bal_w4_nb2", 2: "bal_w8_nb1", 3: "bal_w8_split", 4: "bal_w8_split_nb2"}
     cus = torch.cuda.get_device_properties(0).multi_processor_count
     out = {}
     for K in a.batches:
@@ -145,7 +145,7 @@ def main():
             assert run(k, rec) == 0
             torch.cuda.synchronize()
             res["trace_" + name] = stats(rec.cpu().numpy().astype(np.uint64), L, order)
-        for k in (0, 2):
+        for k in (0, 3):
             recb = torch.zeros(((8 if k >= 2 else 4) * cus, 5), dtype=torch.int64, device="cuda")
             assert runb(k, recb) == 0
             torch.cuda.synchronize()

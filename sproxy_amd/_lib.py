@@ -199,36 +199,53 @@ def _device_elf(path: str = LIB_PATH) -> bytes:
     raise ValueError(f"{path}: no gfx950 code object")
 
 
+OBJDUMP = "/opt/rocm/lib/llvm/bin/llvm-objdump"
+
+
 def kernel_code_hash(kernel: str, path: str = LIB_PATH) -> str:
-    """SHA-256 of one kernel's machine code plus its kernel descriptor in the
-    library's gfx950 code object (`kernel`: the rocprof short name, e.g.
-    md5_fixed_xdma1nt).  profiles/traffic.json records it beside each PMC
-    measurement, so counter bytes stay attached to the code they measured."""
+    """SHA-256 of one kernel's gfx950 machine code in the library, position
+    independent: the kernel (`kernel` = the rocprof short name, e.g.
+    md5_fixed_xdma1nt) is disassembled from the library's code object and its
+    text hashed with the PC-relative literals after s_getpc_b64 (addresses of
+    constants, which move whenever another kernel changes size) masked.
+    profiles/traffic.json records it beside each PMC measurement, so counter
+    bytes stay attached to the code they measured."""
     import hashlib
+    import re
     import struct
+    import subprocess
+    import tempfile
     co = _device_elf(path)
     secs = _elf_sections(co)
     symtab, strtab = secs[".symtab"], secs[".strtab"]
     ent = symtab[9] or 24
     tag = f"{len(kernel)}{kernel}".encode()
-    h = hashlib.sha256()
-    found = []
+    names = set()
     for k in range(symtab[5] // ent):
-        st_name, st_info, st_other, st_shndx, st_value, st_size = struct.unpack_from(
-            "<IBBHQQ", co, symtab[4] + k * ent)
+        st_name, st_info, _, _, _, st_size = struct.unpack_from("<IBBHQQ", co, symtab[4] + k * ent)
         name = co[strtab[4] + st_name:co.index(b"\0", strtab[4] + st_name)]
-        if tag not in name or st_size == 0:
-            continue
-        sec = [s for s in secs.values() if s[3] <= st_value < s[3] + s[5] and s[1] != 8]
-        if not sec:
-            continue
-        off = sec[0][4] + (st_value - sec[0][3])
-        found.append((name, co[off:off + st_size]))
-    if not found:
+        if tag in name and st_size > 64 and (st_info & 0xF) == 2:      # STT_FUNC
+            names.add(name.decode())
+    if not names:
         raise KeyError(f"kernel {kernel} not in {path}")
-    for name, code in sorted(found):
-        h.update(name)
-        h.update(code)
+    with tempfile.NamedTemporaryFile(suffix=".co") as f:
+        f.write(co)
+        f.flush()
+        text = subprocess.run([OBJDUMP, "-d", "--no-show-raw-insn", "--no-leading-addr",
+                               "--disassemble-symbols=" + ",".join(sorted(names)), f.name],
+                              capture_output=True, text=True, check=True).stdout
+    h = hashlib.sha256()
+    pcrel = 0
+    for line in text.splitlines():
+        ins = line.split("//")[0].strip()
+        if not ins or ins.endswith("file format elf64-amdgpu") or ins.startswith("Disassembly of"):
+            continue
+        if pcrel and re.match(r"s_addc?_u32 ", ins):
+            ins = re.sub(r",[^,]*$", ", PCREL", ins)
+            pcrel -= 1
+        else:
+            pcrel = 2 if ins.startswith("s_getpc_b64") else 0
+        h.update(ins.encode() + b"\n")
     return h.hexdigest()
 
 

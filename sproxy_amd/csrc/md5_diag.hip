@@ -1061,37 +1061,22 @@ extern "C" int md5diag_desc_x(int kind, const void* base, const uint64_t* offs, 
 
 // md5_desc_balanced_t with the per-wave record of md5diag_desc_x (one record
 // per persistent wave: its whole run over the groups it took, and how many)
-// for WPB waves per workgroup and NB LDS-DMA images per wave (A/B).
+// for WPB waves per workgroup, NB LDS-DMA images per wave, split queues (A/B).
 namespace md5hip {
-template <int WPB, int NB>
+template <int WPB, int NB, bool kSplit>
 __global__ void __launch_bounds__(64 * WPB)
 diag_desc_balanced(const uint8_t* __restrict__ base, const uint64_t* __restrict__ offs,
                    const uint32_t* __restrict__ lens, const uint32_t* __restrict__ order, uint64_t n,
                    uint4* __restrict__ out, uint32_t* __restrict__ ctr, uint64_t* __restrict__ rec) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds_dyn[];
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-  Md5Hasher<true> h;
-  const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  uint8_t* img = lds_dyn + wave * 16384u;
-  const uint64_t ngroups = (n + 63) / 64;
-  const DescArrays src{offs, lens, order};
-  uint32_t taken = 0;
-  for (;;) {
-    uint32_t g = 0;
-    if (lane == 0) g = atomicAdd(&ctr[0], 1u);
-    g = __builtin_amdgcn_readfirstlane((uint32_t)__shfl((int)g, 0, 64));
-    if (g >= ngroups) break;
-    ++taken;
-    desc_xpose_group<2, Md5Hasher<true>, 0, 1, false, true, true, DescArrays, true, NB>(
-        h, base, src, n, (uint64_t)g * 64u, out, img);
-  }
+  const uint32_t taken = balanced_body<WPB, NB, kSplit>(base, offs, lens, order, n, out, ctr, lds_dyn);
   const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
-  if (lane == 0 && rec) {
+  if ((threadIdx.x & 63u) == 0 && rec) {
     uint32_t hw, xcc;
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-    const uint64_t w = (uint64_t)blockIdx.x * WPB + wave;
+    const uint64_t w = (uint64_t)blockIdx.x * WPB + (threadIdx.x >> 6);
     rec[5 * w + 0] = hw;
     rec[5 * w + 1] = xcc;
     rec[5 * w + 2] = t0;
@@ -1102,35 +1087,38 @@ diag_desc_balanced(const uint8_t* __restrict__ base, const uint64_t* __restrict_
 }  // namespace md5hip
 
 namespace {
-template <int WPB, int NB>
+template <int WPB, int NB, bool kSplit>
 int diag_launch_balanced(const void* base, const uint64_t* offs, const uint32_t* lens,
                          const uint32_t* order, uint64_t n, void* out, uint32_t* ctr, void* rec,
                          hipStream_t s) {
   const uint32_t lds = BalancedCfg<WPB>::kLds;
-  if (hipFuncSetAttribute(reinterpret_cast<const void*>(diag_desc_balanced<WPB, NB>),
+  if (hipFuncSetAttribute(reinterpret_cast<const void*>(diag_desc_balanced<WPB, NB, kSplit>),
                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
     return -ENODEV;
-  hipLaunchKernelGGL((diag_desc_balanced<WPB, NB>), dim3((uint32_t)diag_cus()), dim3(64 * WPB), lds, s,
-                     (const uint8_t*)base, offs, lens, order, n, (uint4*)out, ctr, (uint64_t*)rec);
+  hipLaunchKernelGGL((diag_desc_balanced<WPB, NB, kSplit>), dim3((uint32_t)diag_cus()), dim3(64 * WPB),
+                     lds, s, (const uint8_t*)base, offs, lens, order, n, (uint4*)out, ctr,
+                     (uint64_t*)rec);
   return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }
 }  // namespace
 
 // rec: 5 x uint64 per wave (WPB x CUs waves), or nullptr.  kind: 0 = 4 waves
-// per WG / 2 images (the product's shape), 1 = 4 / 1, 2 = 8 / 2, 3 = 8 / 1.
+// per WG / 1 image, 1 = 4 / 2 images, 2 = 8 / 1, 3 = 8 / 1 split queues
+// (the product's shape), 4 = 8 / 2 split.
 extern "C" int md5diag_desc_balanced(int kind, const void* base, const uint64_t* offs,
                                      const uint32_t* lens, const uint32_t* order, uint64_t n,
                                      void* out, void* rec, void* stream) {
   if (n == 0) return 0;
   static uint32_t* ctr = nullptr;
-  if (!ctr && hipMalloc(&ctr, 8) != hipSuccess) return -ENOMEM;
+  if (!ctr && hipMalloc(&ctr, 16) != hipSuccess) return -ENOMEM;
   hipStream_t s = (hipStream_t)stream;
-  if (hipMemsetAsync(ctr, 0, 8, s) != hipSuccess) return -EIO;
+  if (hipMemsetAsync(ctr, 0, 16, s) != hipSuccess) return -EIO;
   switch (kind) {
-    case 0: return diag_launch_balanced<4, 2>(base, offs, lens, order, n, out, ctr, rec, s);
-    case 1: return diag_launch_balanced<4, 1>(base, offs, lens, order, n, out, ctr, rec, s);
-    case 2: return diag_launch_balanced<8, 2>(base, offs, lens, order, n, out, ctr, rec, s);
-    case 3: return diag_launch_balanced<8, 1>(base, offs, lens, order, n, out, ctr, rec, s);
+    case 0: return diag_launch_balanced<4, 1, false>(base, offs, lens, order, n, out, ctr, rec, s);
+    case 1: return diag_launch_balanced<4, 2, false>(base, offs, lens, order, n, out, ctr, rec, s);
+    case 2: return diag_launch_balanced<8, 1, false>(base, offs, lens, order, n, out, ctr, rec, s);
+    case 3: return diag_launch_balanced<8, 1, true>(base, offs, lens, order, n, out, ctr, rec, s);
+    case 4: return diag_launch_balanced<8, 2, true>(base, offs, lens, order, n, out, ctr, rec, s);
     default: return -EINVAL;
   }
 }

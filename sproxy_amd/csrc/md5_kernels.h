@@ -649,35 +649,90 @@ template <int WPB>
 struct BalancedCfg {
   static constexpr uint32_t kLds = WPB * 16384u > 81920u ? WPB * 16384u : 81920u + 16384u;
 };
-constexpr uint32_t kBalancedWaves = 4;
 
-template <int WPB>
+// The persistent body.  kSplit (WPB = 8, two waves per SIMD): groups whose
+// first (longest) chunk is >= 256 KiB form the LONG queue, the rest the SHORT
+// queue; waves 0-3 of the workgroup (one per SIMD) take LONG groups, waves
+// 4-7 SHORT ones, each falling back to the other queue when its own is empty.
+// So every SIMD runs one serial chain at a time at s_setprio 3, and the short
+// groups fill the chain's issue gaps at a lower priority instead of slowing it
+// -- a lone MD5 chain issues only ~80 % of a SIMD's VALU rate (the dependent
+// latency), two long chains on one SIMD halve each other's speed.
+// ctr[0] long (all groups, unsplit), ctr[1] short, ctr[2] waves done.
+// Returns the number of groups this wave took (diagnostics).
+template <int WPB, int NB, bool kSplit>
+__device__ __forceinline__ uint32_t balanced_body(const uint8_t* __restrict__ base,
+                                                  const uint64_t* __restrict__ offs,
+                                                  const uint32_t* __restrict__ lens,
+                                                  const uint32_t* __restrict__ order, uint64_t n,
+                                                  uint4* __restrict__ out, uint32_t* __restrict__ ctr,
+                                                  uint8_t* lds) {
+  static_assert(!kSplit || WPB == 8, "split queues: one long and one short wave per SIMD");
+  Md5Hasher<true> h;
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  uint8_t* img = lds + wave * (NB == 2 ? 16384u : 8192u);
+  const uint64_t ngroups = (n + 63) / 64;
+  const DescArrays src{offs, lens, order};
+  uint64_t nlong = ngroups;
+  if constexpr (kSplit) {          // first group whose first chunk is < 256 KiB (longest-first)
+    uint64_t lo = 0, hi = ngroups;
+    while (lo < hi) {
+      const uint64_t mid = (lo + hi) >> 1;
+      const uint32_t L = lens[src.index(mid * 64u)];
+      if ((L >> 6) >= kHybridLongBlocks) lo = mid + 1;
+      else hi = mid;
+    }
+    nlong = __builtin_amdgcn_readfirstlane((uint32_t)lo);
+  }
+  const bool pref_long = !kSplit || wave < 4;
+  auto take = [&](bool lng) __attribute__((always_inline)) -> uint64_t {
+    uint32_t t = 0;
+    if (lane == 0) t = atomicAdd(&ctr[lng ? 0 : 1], 1u);
+    t = __builtin_amdgcn_readfirstlane((uint32_t)__shfl((int)t, 0, 64));
+    const uint64_t g = lng ? (uint64_t)t : nlong + t;
+    return (lng ? g < nlong : g < ngroups) ? g : ~0ull;
+  };
+  uint32_t taken = 0;
+  bool mine = true;                // still drawing from the preferred queue
+  for (;;) {
+    uint64_t g = ~0ull;
+    if (mine) {
+      g = take(pref_long);
+      if (g == ~0ull) mine = false;
+    }
+    if (g == ~0ull) {
+      if (!kSplit) break;
+      g = take(!pref_long);
+      if (g == ~0ull) break;
+    }
+    ++taken;
+    desc_xpose_group<2, Md5Hasher<true>, 0, 1, false, true, true, DescArrays, true, NB>(
+        h, base, src, n, g * 64u, out, img);
+  }
+  if (lane == 0) {
+    const uint32_t total = gridDim.x * (blockDim.x >> 6);
+    if (atomicAdd(&ctr[2], 1u) == total - 1u) {     // every wave has made its last grab
+      atomicExch(&ctr[0], 0u);
+      atomicExch(&ctr[1], 0u);
+      atomicExch(&ctr[2], 0u);
+    }
+  }
+  return taken;
+}
+
+// the product's shape: 8 waves per CU, split queues, one image
+constexpr int kBalancedWaves = 8;
+constexpr int kBalancedImages = 1;
+constexpr bool kBalancedSplit = true;
+
+template <int WPB, int NB, bool kSplit>
 __global__ void __launch_bounds__(64 * WPB)
 md5_desc_balanced_t(const uint8_t* __restrict__ base, const uint64_t* __restrict__ offs,
                     const uint32_t* __restrict__ lens, const uint32_t* __restrict__ order, uint64_t n,
                     uint4* __restrict__ out, uint32_t* __restrict__ ctr) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds_dyn[];   // BalancedCfg<WPB>::kLds
-  Md5Hasher<true> h;
-  const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  uint8_t* img = lds_dyn + wave * 16384u;
-  const uint64_t ngroups = (n + 63) / 64;
-  const DescArrays src{offs, lens, order};
-  for (;;) {
-    uint32_t g = 0;
-    if (lane == 0) g = atomicAdd(&ctr[0], 1u);
-    g = __builtin_amdgcn_readfirstlane((uint32_t)__shfl((int)g, 0, 64));
-    if (g >= ngroups) break;
-    desc_xpose_group<2, Md5Hasher<true>, 0, 1, false, true, true, DescArrays, true, 2>(
-        h, base, src, n, (uint64_t)g * 64u, out, img);
-  }
-  if (lane == 0) {
-    const uint32_t total = gridDim.x * (blockDim.x >> 6);
-    if (atomicAdd(&ctr[1], 1u) == total - 1u) {     // every wave has made its last grab
-      atomicExch(&ctr[0], 0u);
-      atomicExch(&ctr[1], 0u);
-    }
-  }
+  (void)balanced_body<WPB, NB, kSplit>(base, offs, lens, order, n, out, ctr, lds_dyn);
 }
 
 // ---------------------------------------------------------------------------

@@ -70,8 +70,8 @@ uint32_t* balanced_counter(hipStream_t s) {
   auto it = g_ctr.find({dev, s});
   if (it != g_ctr.end()) return it->second;
   uint32_t* c = nullptr;
-  if (hipMalloc(&c, 2 * sizeof(uint32_t)) != hipSuccess) return nullptr;
-  if (hipMemset(c, 0, 2 * sizeof(uint32_t)) != hipSuccess) { (void)hipFree(c); return nullptr; }
+  if (hipMalloc(&c, 4 * sizeof(uint32_t)) != hipSuccess) return nullptr;
+  if (hipMemset(c, 0, 4 * sizeof(uint32_t)) != hipSuccess) { (void)hipFree(c); return nullptr; }
   g_ctr[{dev, s}] = c;
   return c;
 }
@@ -135,16 +135,17 @@ int md5hip_digest_desc_variant(const void* d_base, const uint64_t* d_offsets,
   if (variant == MD5HIP_DESC_BALANCED) {
     uint32_t* ctr = balanced_counter(s);
     if (!ctr) return -ENOMEM;
-    constexpr int W = (int)kBalancedWaves;
+    constexpr int W = kBalancedWaves;
     constexpr uint32_t lds = BalancedCfg<W>::kLds;
-    static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(md5_desc_balanced_t<W>),
+    auto kern = md5_desc_balanced_t<W, kBalancedImages, kBalancedSplit>;
+    static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                                                  hipFuncAttributeMaxDynamicSharedMemorySize,
                                                  (int)lds) == hipSuccess;
     if (!attr) return -ENODEV;
     // the kernel resets its counter on exit; zero it on the stream anyway, so
     // a launch that never finished (a fault) cannot poison the next one
-    if (hipMemsetAsync(ctr, 0, 2 * sizeof(uint32_t), s) != hipSuccess) return -EIO;
-    hipLaunchKernelGGL(md5_desc_balanced_t<W>, dim3((uint32_t)cu_count()), dim3(64 * W), lds, s,
+    if (hipMemsetAsync(ctr, 0, 4 * sizeof(uint32_t), s) != hipSuccess) return -EIO;
+    hipLaunchKernelGGL(kern, dim3((uint32_t)cu_count()), dim3(64 * W), lds, s,
                        base, d_offsets, d_lens, d_order, n, (uint4*)d_digests, ctr);
     return launched();
   }
