@@ -721,10 +721,12 @@ __device__ __forceinline__ uint32_t balanced_body(const uint8_t* __restrict__ ba
   return taken;
 }
 
-// the product's shape: 8 waves per CU, split queues, one image
-constexpr int kBalancedWaves = 8;
+// the product's shape (profiles/r02_c3_balanced_ab.json): one
+// wave per SIMD, one image, one queue.  Two images, 8 waves per CU and the
+// split long/short queues (diag kinds 1-4) all measured slower.
+constexpr int kBalancedWaves = 4;
 constexpr int kBalancedImages = 1;
-constexpr bool kBalancedSplit = true;
+constexpr bool kBalancedSplit = false;
 
 template <int WPB, int NB, bool kSplit>
 __global__ void __launch_bounds__(64 * WPB)
