@@ -1063,14 +1063,15 @@ extern "C" int md5diag_desc_x(int kind, const void* base, const uint64_t* offs, 
 // per persistent wave: its whole run over the groups it took, and how many)
 // for WPB waves per workgroup, NB LDS-DMA images per wave, split queues (A/B).
 namespace md5hip {
-template <int WPB, int NB, bool kSplit>
+template <int WPB, int NB, bool kSplit, int W = 1, bool kHashOff = false>
 __global__ void __launch_bounds__(64 * WPB)
 diag_desc_balanced(const uint8_t* __restrict__ base, const uint64_t* __restrict__ offs,
                    const uint32_t* __restrict__ lens, const uint32_t* __restrict__ order, uint64_t n,
                    uint4* __restrict__ out, uint32_t* __restrict__ ctr, uint64_t* __restrict__ rec) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds_dyn[];
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-  const uint32_t taken = balanced_body<WPB, NB, kSplit>(base, offs, lens, order, n, out, ctr, lds_dyn);
+  const uint32_t taken =
+      balanced_body<WPB, NB, kSplit, W, kHashOff>(base, offs, lens, order, n, out, ctr, lds_dyn);
   const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
   if ((threadIdx.x & 63u) == 0 && rec) {
     uint32_t hw, xcc;
@@ -1087,24 +1088,27 @@ diag_desc_balanced(const uint8_t* __restrict__ base, const uint64_t* __restrict_
 }  // namespace md5hip
 
 namespace {
-template <int WPB, int NB, bool kSplit>
+template <int WPB, int NB, bool kSplit, int W = 1, bool kHashOff = false>
 int diag_launch_balanced(const void* base, const uint64_t* offs, const uint32_t* lens,
                          const uint32_t* order, uint64_t n, void* out, uint32_t* ctr, void* rec,
                          hipStream_t s) {
-  const uint32_t lds = BalancedCfg<WPB>::kLds;
-  if (hipFuncSetAttribute(reinterpret_cast<const void*>(diag_desc_balanced<WPB, NB, kSplit>),
+  const uint32_t lds = BalancedCfg<WPB, NB, W>::kLds;
+  auto kern = diag_desc_balanced<WPB, NB, kSplit, W, kHashOff>;
+  if (hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
     return -ENODEV;
-  hipLaunchKernelGGL((diag_desc_balanced<WPB, NB, kSplit>), dim3((uint32_t)diag_cus()), dim3(64 * WPB),
+  hipLaunchKernelGGL(kern, dim3((uint32_t)diag_cus()), dim3(64 * WPB),
                      lds, s, (const uint8_t*)base, offs, lens, order, n, (uint4*)out, ctr,
                      (uint64_t*)rec);
   return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }
 }  // namespace
 
-// rec: 5 x uint64 per wave (WPB x CUs waves), or nullptr.  kind: 0 = 4 waves
-// per WG / 1 image, 1 = 4 / 2 images, 2 = 8 / 1, 3 = 8 / 1 split queues
-// (the product's shape), 4 = 8 / 2 split.
+// rec: 5 x uint64 per wave (WPB x CUs waves), or nullptr.  kind (waves per
+// WG / buffers NB / 128-B stages per wide stage W): 0 = 4/1/1, 1 = 4/2/1, 2 = 8/1/1, 3 = 8/1/1 split queues, 4 = 8/2/1 split,
+// 5 = 4/1/2, 6 = 4/1/4 (the product's shape), 7 = 4/2/2, 14 = 4/1/5; loads
+// only (no compression, digests meaningless): 8 = 4/1/1, 9 = 4/1/2,
+// 10 = 4/1/4, 11 = 4/2/2, 12 = 4/2/1, 13 = 8/1/1, 15 = 4/1/5.
 extern "C" int md5diag_desc_balanced(int kind, const void* base, const uint64_t* offs,
                                      const uint32_t* lens, const uint32_t* order, uint64_t n,
                                      void* out, void* rec, void* stream) {
@@ -1119,6 +1123,17 @@ extern "C" int md5diag_desc_balanced(int kind, const void* base, const uint64_t*
     case 2: return diag_launch_balanced<8, 1, false>(base, offs, lens, order, n, out, ctr, rec, s);
     case 3: return diag_launch_balanced<8, 1, true>(base, offs, lens, order, n, out, ctr, rec, s);
     case 4: return diag_launch_balanced<8, 2, true>(base, offs, lens, order, n, out, ctr, rec, s);
+    case 5: return diag_launch_balanced<4, 1, false, 2>(base, offs, lens, order, n, out, ctr, rec, s);
+    case 6: return diag_launch_balanced<4, 1, false, 4>(base, offs, lens, order, n, out, ctr, rec, s);
+    case 7: return diag_launch_balanced<4, 2, false, 2>(base, offs, lens, order, n, out, ctr, rec, s);
+    case 8: return diag_launch_balanced<4, 1, false, 1, true>(base, offs, lens, order, n, out, ctr, rec, s);
+    case 9: return diag_launch_balanced<4, 1, false, 2, true>(base, offs, lens, order, n, out, ctr, rec, s);
+    case 10: return diag_launch_balanced<4, 1, false, 4, true>(base, offs, lens, order, n, out, ctr, rec, s);
+    case 11: return diag_launch_balanced<4, 2, false, 2, true>(base, offs, lens, order, n, out, ctr, rec, s);
+    case 12: return diag_launch_balanced<4, 2, false, 1, true>(base, offs, lens, order, n, out, ctr, rec, s);
+    case 13: return diag_launch_balanced<8, 1, false, 1, true>(base, offs, lens, order, n, out, ctr, rec, s);
+    case 14: return diag_launch_balanced<4, 1, false, 5>(base, offs, lens, order, n, out, ctr, rec, s);
+    case 15: return diag_launch_balanced<4, 1, false, 5, true>(base, offs, lens, order, n, out, ctr, rec, s);
     default: return -EINVAL;
   }
 }

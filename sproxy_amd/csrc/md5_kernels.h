@@ -409,11 +409,25 @@ __device__ __forceinline__ void emit(H& h, typename H::Out* __restrict__ out, ui
 // kLongPair: HYBRID's lane-direct long waves refill their 8-block ring two
 // blocks (one whole 128-B line) at a time, so no lane leaves half a line
 // behind to be fetched again after eviction (ring_steps).
-// NB (kDma): LDS-DMA images per wave.  2: `img` holds two 8 KiB images and
-// the DMA of stage s+2 is issued as soon as stage s is read, so a lone wave
-// on its SIMD (BALANCED) keeps a stage in flight under each compression.
+// NB (kDma): LDS-DMA buffers per wave.  2: the DMA of wide stage s+2 is
+// issued as soon as wide stage s is read, so a lone wave on its SIMD
+// (BALANCED) keeps a stage in flight under each compression.
+// W (kDma): 128-B stages per wide stage; a buffer is W 8 KiB images, and the
+// W loads of one row (8 chunks) go out back to back, so each chunk is read
+// W x 128 B contiguous per visit instead of 128 B.
+// kHashOff: loads only, no compression (diagnostic memory-side ceiling).
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  static_assert(N == 0 || N == 8 || N == 16 || N == 32, "vmcnt immediates in use");
+  if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else if constexpr (N == 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
+}
+
 template <int CP, class H, uint32_t kLong = 0, int D = 1, bool kHalf = false, bool kPeel = true,
-          bool kDma = false, class Src = DescArrays, bool kLongPair = true, int NB = 1>
+          bool kDma = false, class Src = DescArrays, bool kLongPair = true, int NB = 1, int W = 1,
+          bool kHashOff = false>
 __device__ __forceinline__ void desc_xpose_group(H& h, const uint8_t* __restrict__ base,
                                                  const Src& src, uint64_t n,
                                                  uint64_t first, typename H::Out* __restrict__ out,
@@ -511,35 +525,55 @@ __device__ __forceinline__ void desc_xpose_group(H& h, const uint8_t* __restrict
         h.block(st, w[1]);
       }
     };
-    if constexpr (kDma && NB == 2) {
-      static_assert(D == 1 && !kHalf, "LDS-DMA images: full 8 KiB stages");
-      auto issue = [&](uint32_t stg) __attribute__((always_inline)) {
-        uint8_t* im = img + (stg & 1u) * 8192u;
+    if constexpr (kDma && (NB == 2 || W > 1)) {
+      static_assert(D == 1 && !kHalf && (NB == 1 || NB == 2), "LDS-DMA images: full 8 KiB stages");
+      const uint32_t nws = (smax + W - 1) / W;              // wide stages
+      auto issue = [&](uint32_t ws) __attribute__((always_inline)) {
+        uint8_t* im = img + (ws % NB) * (W * 8192u);
 #pragma unroll
-        for (int r = 0; r < 8; ++r)
-          __builtin_amdgcn_global_load_lds(rptr[r] + (min(stg, rlast[r]) << 7), im + r * 1024,
-                                           16, 0, CP);
+        for (int r = 0; r < 8; ++r) {
+#pragma unroll
+          for (int j = 0; j < W; ++j) {
+            const uint32_t stg = ws * W + j;
+            if (W == 1 || stg < smax)                       // wave-uniform
+              __builtin_amdgcn_global_load_lds(rptr[r] + (min(stg, rlast[r]) << 7),
+                                               im + j * 8192 + r * 1024, 16, 0, CP);
+          }
+        }
       };
       issue(0);
-      if (smax > 1) issue(1);
-      for (uint32_t stg = 0; stg < smax; ++stg) {
-        // stage stg's 8 loads are done once at most the next stage's 8 are
-        // outstanding (loads complete in issue order)
-        if (stg + 1 < smax) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        uint4 w[2][4];
-        const uint8_t* row = myrow + (stg & 1u) * 8192u;
+      if (NB == 2 && nws > 1) issue(1);
+      for (uint32_t ws = 0; ws < nws; ++ws) {
+        // wide stage ws is in once at most the next one's loads are
+        // outstanding (loads complete in issue order); a partial next one
+        // (the group's last) falls back to a full drain
+        if constexpr (NB == 2) {
+          if ((ws + 2) * W <= smax) wait_vmcnt<8 * W>();
+          else wait_vmcnt<0>();
+        } else {
+          wait_vmcnt<0>();
+        }
+        uint4 w[W][2][4];
+        const uint8_t* row = myrow + (ws % NB) * (W * 8192u);
 #pragma unroll
-        for (int q = 0; q < 8; ++q) {
-          const u32x4 v = *reinterpret_cast<const u32x4*>(row + ((q ^ g) * 16));
-          w[q >> 2][q & 3] = make_uint4(v.x, v.y, v.z, v.w);
+        for (int j = 0; j < W; ++j) {
+#pragma unroll
+          for (int q = 0; q < 8; ++q) {
+            const u32x4 v = *reinterpret_cast<const u32x4*>(row + j * 8192 + ((q ^ g) * 16));
+            w[j][q >> 2][q & 3] = make_uint4(v.x, v.y, v.z, v.w);
+          }
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // reads done before the refill
-        if (stg + 2 < smax) issue(stg + 2);
+        if (ws + NB < nws) issue(ws + NB);
         __builtin_amdgcn_sched_barrier(0);
-        if (stg < nst) {
-          h.block(st, w[0]);
-          h.block(st, w[1]);
+        if constexpr (!kHashOff) {
+#pragma unroll
+          for (int j = 0; j < W; ++j) {
+            if (ws * W + j < nst) {
+              h.block(st, w[j][0]);
+              h.block(st, w[j][1]);
+            }
+          }
         }
       }
     } else if constexpr (kDma) {
@@ -642,12 +676,14 @@ md5_desc_hybrid(const uint8_t* __restrict__ base, const uint64_t* __restrict__ o
 // done; the last wave out resets both, so a counter serves the next launch
 // on its stream (md5_kernels.hip keeps one per device and stream).
 // ---------------------------------------------------------------------------
-// WPB waves per workgroup (one per SIMD at 4, two at 8), each with two 8 KiB
-// LDS-DMA images; the workgroup asks for more than half the CU's LDS, so a CU
-// runs exactly one.
-template <int WPB>
+// WPB waves per workgroup (one per SIMD at 4, two at 8), each with NB x W
+// 8 KiB LDS-DMA images; the workgroup asks for more than half the CU's LDS,
+// so a CU runs exactly one.
+template <int WPB, int NB = 1, int W = 1>
 struct BalancedCfg {
-  static constexpr uint32_t kLds = WPB * 16384u > 81920u ? WPB * 16384u : 81920u + 16384u;
+  static constexpr uint32_t kWave = NB * W * 8192u;
+  static constexpr uint32_t kLds = WPB * kWave > 81920u ? WPB * kWave : 81920u + 16384u;
+  static_assert(WPB * kWave <= 160u * 1024u, "LDS per CU");
 };
 
 // The persistent body.  kSplit (WPB = 8, two waves per SIMD): groups whose
@@ -660,7 +696,7 @@ struct BalancedCfg {
 // latency), two long chains on one SIMD halve each other's speed.
 // ctr[0] long (all groups, unsplit), ctr[1] short, ctr[2] waves done.
 // Returns the number of groups this wave took (diagnostics).
-template <int WPB, int NB, bool kSplit>
+template <int WPB, int NB, bool kSplit, int W = 1, bool kHashOff = false>
 __device__ __forceinline__ uint32_t balanced_body(const uint8_t* __restrict__ base,
                                                   const uint64_t* __restrict__ offs,
                                                   const uint32_t* __restrict__ lens,
@@ -671,7 +707,7 @@ __device__ __forceinline__ uint32_t balanced_body(const uint8_t* __restrict__ ba
   Md5Hasher<true> h;
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  uint8_t* img = lds + wave * (NB == 2 ? 16384u : 8192u);
+  uint8_t* img = lds + wave * BalancedCfg<WPB, NB, W>::kWave;
   const uint64_t ngroups = (n + 63) / 64;
   const DescArrays src{offs, lens, order};
   uint64_t nlong = ngroups;
@@ -707,7 +743,7 @@ __device__ __forceinline__ uint32_t balanced_body(const uint8_t* __restrict__ ba
       if (g == ~0ull) break;
     }
     ++taken;
-    desc_xpose_group<2, Md5Hasher<true>, 0, 1, false, true, true, DescArrays, true, NB>(
+    desc_xpose_group<2, Md5Hasher<true>, 0, 1, false, true, true, DescArrays, true, NB, W, kHashOff>(
         h, base, src, n, g * 64u, out, img);
   }
   if (lane == 0) {
@@ -721,20 +757,26 @@ __device__ __forceinline__ uint32_t balanced_body(const uint8_t* __restrict__ ba
   return taken;
 }
 
-// the product's shape (profiles/r02_c3_balanced_ab.json): one
-// wave per SIMD, one image, one queue.  Two images, 8 waves per CU and the
-// split long/short queues (diag kinds 1-4) all measured slower.
+// the product's shape (profiles/r02_c3_balanced_ab.json,
+// r02_c3_wide_ab.json): one wave per SIMD, one buffer of four 128-B stages
+// (512 B contiguous per chunk per visit), one queue.  With 128 B per chunk per
+// visit the loads alone (no compression) top out at 3.9 TB/s on coalesced C3
+// batches -- 64 chunks a wave, each a different DRAM row -- and the hashing
+// kernel ran at that ceiling; 256 B / 512 B lift the ceiling to 4.8 / 5.5 TB/s
+// and the kernel to 4.8 / 5.0.  Two buffers, 8 waves per CU and split
+// long/short queues (diag kinds 1-4) measured slower.
 constexpr int kBalancedWaves = 4;
 constexpr int kBalancedImages = 1;
+constexpr int kBalancedWide = 4;
 constexpr bool kBalancedSplit = false;
 
-template <int WPB, int NB, bool kSplit>
+template <int WPB, int NB, bool kSplit, int W>
 __global__ void __launch_bounds__(64 * WPB)
 md5_desc_balanced_t(const uint8_t* __restrict__ base, const uint64_t* __restrict__ offs,
                     const uint32_t* __restrict__ lens, const uint32_t* __restrict__ order, uint64_t n,
                     uint4* __restrict__ out, uint32_t* __restrict__ ctr) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t lds_dyn[];   // BalancedCfg<WPB>::kLds
-  (void)balanced_body<WPB, NB, kSplit>(base, offs, lens, order, n, out, ctr, lds_dyn);
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds_dyn[];   // BalancedCfg<WPB, NB, W>::kLds
+  (void)balanced_body<WPB, NB, kSplit, W>(base, offs, lens, order, n, out, ctr, lds_dyn);
 }
 
 // ---------------------------------------------------------------------------

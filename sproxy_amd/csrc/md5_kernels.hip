@@ -135,9 +135,9 @@ int md5hip_digest_desc_variant(const void* d_base, const uint64_t* d_offsets,
   if (variant == MD5HIP_DESC_BALANCED) {
     uint32_t* ctr = balanced_counter(s);
     if (!ctr) return -ENOMEM;
-    constexpr int W = kBalancedWaves;
-    constexpr uint32_t lds = BalancedCfg<W>::kLds;
-    auto kern = md5_desc_balanced_t<W, kBalancedImages, kBalancedSplit>;
+    constexpr int WPB = kBalancedWaves;
+    constexpr uint32_t lds = BalancedCfg<WPB, kBalancedImages, kBalancedWide>::kLds;
+    auto kern = md5_desc_balanced_t<WPB, kBalancedImages, kBalancedSplit, kBalancedWide>;
     static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                                                  hipFuncAttributeMaxDynamicSharedMemorySize,
                                                  (int)lds) == hipSuccess;
@@ -145,7 +145,7 @@ int md5hip_digest_desc_variant(const void* d_base, const uint64_t* d_offsets,
     // the kernel resets its counter on exit; zero it on the stream anyway, so
     // a launch that never finished (a fault) cannot poison the next one
     if (hipMemsetAsync(ctr, 0, 4 * sizeof(uint32_t), s) != hipSuccess) return -EIO;
-    hipLaunchKernelGGL(kern, dim3((uint32_t)cu_count()), dim3(64 * W), lds, s,
+    hipLaunchKernelGGL(kern, dim3((uint32_t)cu_count()), dim3(64 * WPB), lds, s,
                        base, d_offsets, d_lens, d_order, n, (uint4*)d_digests, ctr);
     return launched();
   }
