@@ -79,8 +79,9 @@ def parse_args(argv):
                    help="C3 batches planned and launched together for the coalesced rate (0/1 = off)")
     p.add_argument("--c3-streams", type=int, default=3,
                    help="streams for C3's streamed rate (batches in flight)")
-    p.add_argument("--c3-legs", default="all", choices=["all", "main"],
-                   help="main: only the single-batch launches (PMC passes count one kernel)")
+    p.add_argument("--c3-legs", default="all", choices=["all", "main", "coalesced"],
+                   help="main / coalesced: only the single-batch / the coalesced launches "
+                        "(PMC passes count one kernel on one workload)")
     p.add_argument("--c3q-batches", type=int, default=6,
                    help="--config c3q: C3 submissions streamed through one md5hip_queue")
     p.add_argument("--c3q-inflight", type=int, default=2,
@@ -544,11 +545,55 @@ def c3_sample(lens, order, k, seed):
     return np.unique(np.concatenate([np.asarray(p, dtype=np.int64) for p in pick]))
 
 
+def c3_coalesced(a, lens, rank, world):
+    """K C3 batches (the main batch's lengths + K-1 more, own bytes) planned
+    and launched as one descriptor batch -- what md5hip_queue does with K
+    pending submissions (--config c3q) -- timed with HIP events."""
+    import numpy as np
+    K = a.c3_coalesce
+    lk = [lens] + [c3_lens(a.c3_bytes, 2000 + 17 * j + rank) for j in range(1, K)]
+    ok_ = [c3_offsets(x)[0] for x in lk]
+    spans = [(c3_offsets(x)[1] + 15) // 16 * 16 for x in lk]
+    starts = np.concatenate([[0], np.cumsum(spans)[:-1]])
+    big = m.arena_empty(int(sum(spans)))
+    m.fill_synthetic(big, seed=0xC3C + rank)
+    L_all = np.concatenate(lk)
+    O_all = np.concatenate([o + st for o, st in zip(ok_, starts)])
+    ordK, varK = m.plan_desc(L_all.astype(np.uint32))
+    dO, dL = torch.from_numpy(O_all).cuda(), torch.from_numpy(L_all.astype(np.int32)).cuda()
+    dR = torch.from_numpy(ordK.astype(np.int32)).cuda()
+    outK = torch.empty((L_all.size, 16), dtype=torch.uint8, device="cuda")
+    _, k_ms = timed_steps(lambda: m.digest_desc(big, dO, dL, dR, out=outK, variant=varK),
+                          max(5, a.steps // 2), max(2, a.warmup // 4), world)
+    pay = float(L_all.sum())
+    kname = "md5_desc_" + ("balanced_t" if varK == "balanced" else varK)
+    traffic, tnote = load_traffic(a.traffic, kname, f"c3k{K}@{a.c3_bytes}s{1000 + rank}")
+    par = sample_desc(big, O_all, L_all, outK, c3_sample(L_all, ordK, a.parity_sample // 2, 191 + rank)) \
+        if a.parity_sample else None
+    alg = pay + 16 * L_all.size
+    return {"batches": K, "chunks": int(L_all.size), "payload_bytes": int(pay), "kernel": varK,
+            "ms_per_launch": round(k_ms, 4), "ms_per_batch": round(k_ms / K, 4),
+            "value": round(pay * world / (k_ms * 1e-3) / GIB, 2), "unit": "GiB/s",
+            "roofline": {"bound": "hbm", "achieved": round(alg / (k_ms * 1e-3) / 1e9, 1),
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(alg / (k_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                         "traffic": traffic, "traffic_source": tnote, "kernel": "md5hip::" + kname,
+                         "alg_bytes_per_launch": int(alg)},
+            "parity": par,
+            "note": "K C3 batches coalesced into one planned descriptor launch (distinct bytes)"}
+
+
 def run_c3(a, rank, world, local, device, backend):
     """Mixed lengths 4 KiB..1 MiB (netcache chunk_size range, httpd.c:7968) with
     1-in-8 ragged tails, packed 16-B aligned, lanes packed longest-first."""
     import numpy as np
     lens = c3_lens(a.c3_bytes, 1000 + rank)
+    if a.c3_legs == "coalesced":
+        coal = c3_coalesced(a, lens, rank, world)
+        return per_rank_line({"metric": "C3 coalesced launches only (profiling run)", "value": coal["value"],
+                              "unit": "GiB/s", "n_gpus": world, "config": {"workload": "C3 coalesced"},
+                              "coalesced": coal}, rank, world, local, device, backend,
+                             coal["payload_bytes"], coal["ms_per_launch"] * 1e-3, coal["parity"])
     offs, total = c3_offsets(lens)
     # the batch lives in an arena (md5hip_arena_alloc: 1 GiB-aligned virtual
     # range, large page-table fragments), where HYBRID's lane-direct chains
@@ -609,29 +654,7 @@ def run_c3(a, rank, world, local, device, backend):
     del outs
     # coalesced: K such batches (own lengths, own bytes) planned and launched
     # as one descriptor batch by hand (what md5hip_queue does, --config c3q)
-    coal = None
-    K = a.c3_coalesce
-    if K > 1:
-        lk = [lens] + [c3_lens(a.c3_bytes, 2000 + 17 * j + rank) for j in range(1, K)]
-        ok_ = [c3_offsets(x)[0] for x in lk]
-        spans = [(c3_offsets(x)[1] + 15) // 16 * 16 for x in lk]
-        starts = np.concatenate([[0], np.cumsum(spans)[:-1]])
-        big = m.arena_empty(int(sum(spans)))
-        m.fill_synthetic(big, seed=0xC3C + rank)
-        L_all = np.concatenate(lk)
-        O_all = np.concatenate([o + st for o, st in zip(ok_, starts)])
-        ordK, varK = m.plan_desc(L_all.astype(np.uint32))
-        dO, dL = torch.from_numpy(O_all).cuda(), torch.from_numpy(L_all.astype(np.int32)).cuda()
-        dR = torch.from_numpy(ordK.astype(np.int32)).cuda()
-        outK = torch.empty((L_all.size, 16), dtype=torch.uint8, device="cuda")
-        _, k_ms = timed_steps(lambda: m.digest_desc(big, dO, dL, dR, out=outK, variant=varK),
-                              max(5, a.steps // 2), max(2, a.warmup // 4), world)
-        pay = float(L_all.sum())
-        coal = {"batches": K, "chunks": int(L_all.size), "payload_bytes": int(pay), "kernel": varK,
-                "ms_per_launch": round(k_ms, 4), "ms_per_batch": round(k_ms / K, 4),
-                "value": round(pay * world / (k_ms * 1e-3) / GIB, 2), "unit": "GiB/s",
-                "note": "K C3 batches coalesced into one planned descriptor launch (distinct bytes)"}
-        del big, dO, dL, dR, outK
+    coal = c3_coalesced(a, lens, rank, world) if a.c3_coalesce > 1 else None
     # imbalance vs uniform -- the same payload bytes of the
     # same arena hashed as uniform 16 KiB chunks by the fixed-length kernel
     n_u = int(payload) // 16384
@@ -687,7 +710,10 @@ def run_c3q(a, rank, world, local, device, backend):
     md5hip.h): `c3q_batches` distinct C3 batches (own lengths, own bytes)
     submitted back to back, as netcache's ASIO threads would submit vectors;
     the queue coalesces whatever is pending into one planned launch per slot
-    and completes each ticket on its own.  A step = submit all + wait all."""
+    and completes each ticket on its own.  A step = submit all K; the value is
+    the pipelined stream (step k's submissions go in before step k-1's tickets
+    are waited for, so the queue never runs dry between steps), `drained` the
+    same steps with every ticket waited for before the next submission."""
     import numpy as np
     K = max(1, a.c3q_batches)
     lk = [c3_lens(a.c3_bytes, 3000 + 31 * j + rank) for j in range(K)]
@@ -700,26 +726,45 @@ def run_c3q(a, rank, world, local, device, backend):
     subs = []
     for j in range(K):
         ptrs = (base + starts[j] + ok_[j]).astype(np.uint64)
-        subs.append((ptrs, lk[j].astype(np.uint32),
-                     torch.empty((lk[j].size, 16), dtype=torch.uint8, device="cuda")))
+        subs.append((ptrs, lk[j].astype(np.uint32), None))
+    outs = [[torch.empty((x.size, 16), dtype=torch.uint8, device="cuda") for x in lk] for _ in range(2)]
     q = m.Queue(device=torch.cuda.current_device(), nslots=a.c3q_slots, inflight=a.c3q_inflight)
 
-    def step():
-        pend = [q.submit_device_async(p, L_, o) for p, L_, o in subs]
+    def submit(k):
+        return [q.submit_device_async(p, L_, o) for (p, L_, _), o in zip(subs, outs[k & 1])]
+
+    def drain(pend):
         for pn in reversed(pend):          # any order: tickets complete independently
             pn.wait()
 
+    def drained_step():
+        drain(submit(0))
+
+    def timed(fn):
+        torch.cuda.synchronize()
+        barrier(world)
+        t0 = time.perf_counter()
+        fn()
+        torch.cuda.synchronize()
+        wall = time.perf_counter() - t0
+        barrier(world)
+        return wall, max_over_ranks(wall, world)
+
+    def pipelined():
+        # step k submits its K vectors, then waits for step k-1's: the queue
+        # always holds the next step's work while a launch runs
+        prev = submit(0)
+        for k in range(1, a.steps):
+            cur = submit(k)
+            drain(prev)
+            prev = cur
+        drain(prev)
+
     for _ in range(a.warmup):
-        step()
-    torch.cuda.synchronize()
-    barrier(world)
-    t0 = time.perf_counter()
-    for _ in range(a.steps):
-        step()
-    torch.cuda.synchronize()
-    wall = time.perf_counter() - t0
-    barrier(world)
-    wall_max = max_over_ranks(wall, world)
+        drained_step()
+    wall_d, wall_d_max = timed(lambda: [drained_step() for _ in range(a.steps)])
+    wall, wall_max = timed(pipelined)
+    subs = [(p, L_, o) for (p, L_, _), o in zip(subs, outs[(a.steps - 1) & 1])]
     stats = q.stats()
     q.close()
     payload = float(sum(x.sum() for x in lk))
@@ -745,7 +790,11 @@ def run_c3q(a, rank, world, local, device, backend):
                         "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": round(payload / (wall_max / a.steps) / 1e9 / HBM_PEAK_GBS, 4),
                         "traffic": None, "kernel": "md5hip::md5_desc_* (queue launches)",
-                        "note": "wall-clock per step (submit + wait), several launches per step"}}
+                        "note": "wall-clock per step (submit + wait), several launches per step"},
+           "drained": {"value": round(payload * world * a.steps / wall_d_max / GIB, 2), "unit": "GiB/s",
+                       "ms_per_step": round(wall_d_max / a.steps * 1e3, 4),
+                       "note": "every step's tickets waited for before the next step submits: each "
+                               "step starts on an idle queue, so its first launch holds one vector"}}
     return per_rank_line(res, rank, world, local, device, backend, payload * a.steps, wall, par)
 
 

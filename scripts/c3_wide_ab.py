@@ -27,8 +27,11 @@ from sproxy_amd import md5 as m  # noqa: E402
 
 NAMES = {0: "w4_nb1_s1", 1: "w4_nb2_s1", 5: "w4_nb1_s2", 6: "w4_nb1_s4", 7: "w4_nb2_s2",
          8: "loads_w4_nb1_s1", 9: "loads_w4_nb1_s2", 10: "loads_w4_nb1_s4", 11: "loads_w4_nb2_s2",
-         12: "loads_w4_nb2_s1", 13: "loads_w8_nb1_s1", 14: "w4_nb1_s5", 15: "loads_w4_nb1_s5"}
-HASHING = (0, 1, 5, 6, 7, 14)
+         12: "loads_w4_nb2_s1", 13: "loads_w8_nb1_s1", 14: "w4_nb1_s5", 15: "loads_w4_nb1_s5",
+         16: "w4_nb1_s4_cached", 17: "loads_w4_nb1_s4_cached", 18: "w4_nb1_s2_cached", 19: "w4_nb1_s1_cached",
+         20: "w4_nb2_s1_cached", 21: "w8_nb1_s1_cached", 22: "loads_w4_nb1_s1_cached",
+         23: "w8_split_s1_cached"}
+HASHING = (0, 1, 5, 6, 7, 14, 16, 18, 19, 20, 21, 23)
 PRODUCT = ("balanced", "hybrid", "xdma")
 
 

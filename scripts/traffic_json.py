@@ -24,7 +24,9 @@ sys.path.insert(0, REPO)
 
 
 def short(name):
-    return name.split("(")[0].replace("void ", "").replace("md5hip::", "").strip()
+    # template arguments dropped: kernel_code_hash finds the (one) product
+    # instantiation by its base name
+    return name.split("(")[0].split("<")[0].replace("void ", "").replace("md5hip::", "").strip()
 
 
 def per_kernel(d, counter):

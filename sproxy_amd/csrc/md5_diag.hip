@@ -1063,7 +1063,7 @@ extern "C" int md5diag_desc_x(int kind, const void* base, const uint64_t* offs, 
 // per persistent wave: its whole run over the groups it took, and how many)
 // for WPB waves per workgroup, NB LDS-DMA images per wave, split queues (A/B).
 namespace md5hip {
-template <int WPB, int NB, bool kSplit, int W = 1, bool kHashOff = false>
+template <int WPB, int NB, bool kSplit, int W = 1, bool kHashOff = false, int CP = 2>
 __global__ void __launch_bounds__(64 * WPB)
 diag_desc_balanced(const uint8_t* __restrict__ base, const uint64_t* __restrict__ offs,
                    const uint32_t* __restrict__ lens, const uint32_t* __restrict__ order, uint64_t n,
@@ -1071,7 +1071,7 @@ diag_desc_balanced(const uint8_t* __restrict__ base, const uint64_t* __restrict_
   extern __shared__ __attribute__((aligned(16))) uint8_t lds_dyn[];
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
   const uint32_t taken =
-      balanced_body<WPB, NB, kSplit, W, kHashOff>(base, offs, lens, order, n, out, ctr, lds_dyn);
+      balanced_body<WPB, NB, kSplit, W, kHashOff, CP>(base, offs, lens, order, n, out, ctr, lds_dyn);
   const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
   if ((threadIdx.x & 63u) == 0 && rec) {
     uint32_t hw, xcc;
@@ -1088,12 +1088,12 @@ diag_desc_balanced(const uint8_t* __restrict__ base, const uint64_t* __restrict_
 }  // namespace md5hip
 
 namespace {
-template <int WPB, int NB, bool kSplit, int W = 1, bool kHashOff = false>
+template <int WPB, int NB, bool kSplit, int W = 1, bool kHashOff = false, int CP = 2>
 int diag_launch_balanced(const void* base, const uint64_t* offs, const uint32_t* lens,
                          const uint32_t* order, uint64_t n, void* out, uint32_t* ctr, void* rec,
                          hipStream_t s) {
   const uint32_t lds = BalancedCfg<WPB, NB, W>::kLds;
-  auto kern = diag_desc_balanced<WPB, NB, kSplit, W, kHashOff>;
+  auto kern = diag_desc_balanced<WPB, NB, kSplit, W, kHashOff, CP>;
   if (hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
     return -ENODEV;
@@ -1106,9 +1106,13 @@ int diag_launch_balanced(const void* base, const uint64_t* offs, const uint32_t*
 
 // rec: 5 x uint64 per wave (WPB x CUs waves), or nullptr.  kind (waves per
 // WG / buffers NB / 128-B stages per wide stage W): 0 = 4/1/1, 1 = 4/2/1, 2 = 8/1/1, 3 = 8/1/1 split queues, 4 = 8/2/1 split,
-// 5 = 4/1/2, 6 = 4/1/4 (the product's shape), 7 = 4/2/2, 14 = 4/1/5; loads
+// 5 = 4/1/2, 6 = 4/1/4, 7 = 4/2/2, 14 = 4/1/5; loads
 // only (no compression, digests meaningless): 8 = 4/1/1, 9 = 4/1/2,
-// 10 = 4/1/4, 11 = 4/2/2, 12 = 4/2/1, 13 = 8/1/1, 15 = 4/1/5.
+// 10 = 4/1/4, 11 = 4/2/2, 12 = 4/2/1, 13 = 8/1/1, 15 = 4/1/5.  Default cache
+// policy instead of nt (lines stay in L2: a 16-B-aligned chunk's visit
+// boundaries share a 128-B line): 16 = 4/1/4, 17 = 4/1/4 loads only,
+// 18 = 4/1/2, 19 = 4/1/1 (the product's shape), 20 = 4/2/1, 21 = 8/1/1, 22 = 4/1/1 loads only,
+// 23 = 8/1/1 split queues.
 extern "C" int md5diag_desc_balanced(int kind, const void* base, const uint64_t* offs,
                                      const uint32_t* lens, const uint32_t* order, uint64_t n,
                                      void* out, void* rec, void* stream) {
@@ -1134,6 +1138,14 @@ extern "C" int md5diag_desc_balanced(int kind, const void* base, const uint64_t*
     case 13: return diag_launch_balanced<8, 1, false, 1, true>(base, offs, lens, order, n, out, ctr, rec, s);
     case 14: return diag_launch_balanced<4, 1, false, 5>(base, offs, lens, order, n, out, ctr, rec, s);
     case 15: return diag_launch_balanced<4, 1, false, 5, true>(base, offs, lens, order, n, out, ctr, rec, s);
+    case 16: return diag_launch_balanced<4, 1, false, 4, false, 0>(base, offs, lens, order, n, out, ctr, rec, s);
+    case 17: return diag_launch_balanced<4, 1, false, 4, true, 0>(base, offs, lens, order, n, out, ctr, rec, s);
+    case 18: return diag_launch_balanced<4, 1, false, 2, false, 0>(base, offs, lens, order, n, out, ctr, rec, s);
+    case 19: return diag_launch_balanced<4, 1, false, 1, false, 0>(base, offs, lens, order, n, out, ctr, rec, s);
+    case 20: return diag_launch_balanced<4, 2, false, 1, false, 0>(base, offs, lens, order, n, out, ctr, rec, s);
+    case 21: return diag_launch_balanced<8, 1, false, 1, false, 0>(base, offs, lens, order, n, out, ctr, rec, s);
+    case 22: return diag_launch_balanced<4, 1, false, 1, true, 0>(base, offs, lens, order, n, out, ctr, rec, s);
+    case 23: return diag_launch_balanced<8, 1, true, 1, false, 0>(base, offs, lens, order, n, out, ctr, rec, s);
     default: return -EINVAL;
   }
 }

@@ -696,7 +696,7 @@ struct BalancedCfg {
 // latency), two long chains on one SIMD halve each other's speed.
 // ctr[0] long (all groups, unsplit), ctr[1] short, ctr[2] waves done.
 // Returns the number of groups this wave took (diagnostics).
-template <int WPB, int NB, bool kSplit, int W = 1, bool kHashOff = false>
+template <int WPB, int NB, bool kSplit, int W = 1, bool kHashOff = false, int CP = 2>
 __device__ __forceinline__ uint32_t balanced_body(const uint8_t* __restrict__ base,
                                                   const uint64_t* __restrict__ offs,
                                                   const uint32_t* __restrict__ lens,
@@ -743,7 +743,7 @@ __device__ __forceinline__ uint32_t balanced_body(const uint8_t* __restrict__ ba
       if (g == ~0ull) break;
     }
     ++taken;
-    desc_xpose_group<2, Md5Hasher<true>, 0, 1, false, true, true, DescArrays, true, NB, W, kHashOff>(
+    desc_xpose_group<CP, Md5Hasher<true>, 0, 1, false, true, true, DescArrays, true, NB, W, kHashOff>(
         h, base, src, n, g * 64u, out, img);
   }
   if (lane == 0) {
@@ -758,25 +758,28 @@ __device__ __forceinline__ uint32_t balanced_body(const uint8_t* __restrict__ ba
 }
 
 // the product's shape (profiles/r02_c3_balanced_ab.json,
-// r02_c3_wide_ab.json): one wave per SIMD, one buffer of four 128-B stages
-// (512 B contiguous per chunk per visit), one queue.  With 128 B per chunk per
-// visit the loads alone (no compression) top out at 3.9 TB/s on coalesced C3
-// batches -- 64 chunks a wave, each a different DRAM row -- and the hashing
-// kernel ran at that ceiling; 256 B / 512 B lift the ceiling to 4.8 / 5.5 TB/s
-// and the kernel to 4.8 / 5.0.  Two buffers, 8 waves per CU and split
-// long/short queues (diag kinds 1-4) measured slower.
+// r02_c3_wide_ab.json, r02_c3_cache_policy_ab.json): one wave per SIMD, one
+// 8 KiB image of 128-B stages, one queue, DEFAULT cache policy.  A C3 chunk
+// starts 16-B aligned, so each 128-B stage straddles two lines and shares one
+// with the next stage; with `nt` loads (the C2 kernel's policy, where chunks
+// are line-aligned) that line left L2 before the next stage came, and HBM
+// bytes ran 1.21-1.7x the payload, capping the loads alone at 3.9 TB/s.  The
+// default policy keeps it: 1.005x, the same kernel 22.1 -> 16.1-16.7 ms on
+// five coalesced batches.  Wider stages (W x 128 B per visit), two buffers,
+// 8 waves per CU and split long/short queues measured no better.
 constexpr int kBalancedWaves = 4;
 constexpr int kBalancedImages = 1;
-constexpr int kBalancedWide = 4;
+constexpr int kBalancedWide = 1;
 constexpr bool kBalancedSplit = false;
+constexpr int kBalancedPolicy = 0;
 
-template <int WPB, int NB, bool kSplit, int W>
+template <int WPB, int NB, bool kSplit, int W, int CP>
 __global__ void __launch_bounds__(64 * WPB)
 md5_desc_balanced_t(const uint8_t* __restrict__ base, const uint64_t* __restrict__ offs,
                     const uint32_t* __restrict__ lens, const uint32_t* __restrict__ order, uint64_t n,
                     uint4* __restrict__ out, uint32_t* __restrict__ ctr) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds_dyn[];   // BalancedCfg<WPB, NB, W>::kLds
-  (void)balanced_body<WPB, NB, kSplit, W>(base, offs, lens, order, n, out, ctr, lds_dyn);
+  (void)balanced_body<WPB, NB, kSplit, W, false, CP>(base, offs, lens, order, n, out, ctr, lds_dyn);
 }
 
 // ---------------------------------------------------------------------------

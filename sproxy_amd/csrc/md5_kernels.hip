@@ -76,6 +76,22 @@ uint32_t* balanced_counter(hipStream_t s) {
   return c;
 }
 
+// A kernel's dynamic-LDS limit raised once per device (the attribute is set
+// on the current device; a pool drives several from one process).
+bool dyn_lds_ready(const void* kern, uint32_t lds) {
+  static std::mutex mu;
+  static std::map<std::pair<int, const void*>, bool> done;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return false;
+  std::lock_guard<std::mutex> lk(mu);
+  auto it = done.find({dev, kern});
+  if (it != done.end()) return it->second;
+  const bool ok = hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) ==
+                  hipSuccess;
+  done[{dev, kern}] = ok;
+  return ok;
+}
+
 // One workgroup of `threads` per CU, grid-stride over 64-chunk groups.
 uint32_t per_cu_grid(uint64_t n) {
   const uint64_t need = (n + 63) / 64;
@@ -137,11 +153,8 @@ int md5hip_digest_desc_variant(const void* d_base, const uint64_t* d_offsets,
     if (!ctr) return -ENOMEM;
     constexpr int WPB = kBalancedWaves;
     constexpr uint32_t lds = BalancedCfg<WPB, kBalancedImages, kBalancedWide>::kLds;
-    auto kern = md5_desc_balanced_t<WPB, kBalancedImages, kBalancedSplit, kBalancedWide>;
-    static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
-                                                 hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                 (int)lds) == hipSuccess;
-    if (!attr) return -ENODEV;
+    auto kern = md5_desc_balanced_t<WPB, kBalancedImages, kBalancedSplit, kBalancedWide, kBalancedPolicy>;
+    if (!dyn_lds_ready(reinterpret_cast<const void*>(kern), lds)) return -ENODEV;
     // the kernel resets its counter on exit; zero it on the stream anyway, so
     // a launch that never finished (a fault) cannot poison the next one
     if (hipMemsetAsync(ctr, 0, 4 * sizeof(uint32_t), s) != hipSuccess) return -EIO;
