@@ -1012,17 +1012,23 @@ extern "C" int md5diag_variant_crc_desc(int v, const void* d_base, const uint64_
 // rec == nullptr: no record (timing-only A/B).
 // ---------------------------------------------------------------------------
 namespace md5hip {
-template <uint32_t kLong, bool kLongPair>
+// kVPad: the kernel claims VGPRs up to v[kVPad] (an empty asm clobber), so the
+// register file, not LDS, caps its waves per SIMD (4 at v127, 3 at v167, 2 at
+// v255) -- evenly over the four SIMDs, as HYBRID's 163 VGPRs do.
+template <uint32_t kLong, bool kLongPair, int CP = 2, int kVPad = 0>
 __global__ void __launch_bounds__(64)
 diag_desc_x(const uint8_t* __restrict__ base, const uint64_t* __restrict__ offs,
             const uint32_t* __restrict__ lens, const uint32_t* __restrict__ order, uint64_t n,
             uint4* __restrict__ out, uint32_t nlong, uint64_t* __restrict__ rec) {
   __shared__ __attribute__((aligned(16))) uint8_t img[8192];
+  if constexpr (kVPad == 127) asm volatile("" ::: "v127");
+  else if constexpr (kVPad == 167) asm volatile("" ::: "v167");
+  else if constexpr (kVPad == 255) asm volatile("" ::: "v255");
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
   Md5Hasher<true> h;
   const uint64_t first = (uint64_t)blockIdx.x * 64u;
   if (first < n)
-    desc_xpose_group<2, Md5Hasher<true>, kLong, 1, false, true, true, DescArrays, kLongPair>(
+    desc_xpose_group<CP, Md5Hasher<true>, kLong, 1, false, true, true, DescArrays, kLongPair>(
         h, base, DescArrays{offs, lens, order}, n, first, out, img, nlong);
   const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
   if (rec && (threadIdx.x & 63u) == 0) {
@@ -1054,6 +1060,29 @@ extern "C" int md5diag_desc_x(int kind, const void* base, const uint64_t* offs, 
   else if (kind == 2)
     hipLaunchKernelGGL((diag_desc_x<kHybridLongBlocks, false>), g, b, 0, s, bs, offs, lens, order, n,
                        (uint4*)out, nlong, r);
+  else if (kind == 3)        // XDMA, default cache policy
+    hipLaunchKernelGGL((diag_desc_x<0, true, 0>), g, b, 0, s, bs, offs, lens, order, n, (uint4*)out,
+                       nlong, r);
+  else if (kind == 4)        // HYBRID, default cache policy
+    hipLaunchKernelGGL((diag_desc_x<kHybridLongBlocks, true, 0>), g, b, 0, s, bs, offs, lens, order, n,
+                       (uint4*)out, nlong, r);
+  else if (kind == 8)        // XDMA, 4 / 3 / 2 waves per SIMD by VGPRs
+    hipLaunchKernelGGL((diag_desc_x<0, true, 2, 127>), g, b, 0, s, bs, offs, lens, order, n,
+                       (uint4*)out, nlong, r);
+  else if (kind == 9)
+    hipLaunchKernelGGL((diag_desc_x<0, true, 2, 167>), g, b, 0, s, bs, offs, lens, order, n,
+                       (uint4*)out, nlong, r);
+  else if (kind == 10)
+    hipLaunchKernelGGL((diag_desc_x<0, true, 2, 255>), g, b, 0, s, bs, offs, lens, order, n,
+                       (uint4*)out, nlong, r);
+  else if (kind >= 5 && kind <= 7) {   // XDMA at 16 / 12 / 8 waves per CU (dynamic LDS pad)
+    const uint32_t waves = kind == 5 ? 16u : kind == 6 ? 12u : 8u;
+    const uint32_t pad = (160u * 1024u) / waves - 8192u + 64u;
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(diag_desc_x<0, true, 2>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)pad);
+    hipLaunchKernelGGL((diag_desc_x<0, true, 2>), g, b, pad, s, bs, offs, lens, order, n, (uint4*)out,
+                       nlong, r);
+  }
   else
     return -EINVAL;
   return hipGetLastError() == hipSuccess ? 0 : -EIO;

@@ -21,6 +21,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "hashers.h"
 #include "md5_core.h"
 
@@ -141,12 +143,17 @@ __device__ __forceinline__ void xdma_group(H& h, const uint8_t* __restrict__ bas
   const uint32_t nfull = len >> 6;
   const uint32_t nstage = nfull >> 1;
   typename H::State st = h.init();
-  auto issue = [&](uint32_t stg) __attribute__((always_inline)) {
+  // CP applies to line-aligned chunks; with base or stride off the 128-B
+  // line a stage shares a line with the next, which must stay in L2: default
+  // policy (as desc_xpose_group)
+  const bool lined = ((((uintptr_t)base + wave_first * stride) | stride) & 127u) == 0;
+  auto run = [&](auto pol) __attribute__((always_inline)) {
+    constexpr int P = decltype(pol)::value;
+    auto issue = [&](uint32_t stg) __attribute__((always_inline)) {
 #pragma unroll
-    for (int r = 0; r < 8; ++r)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, img + r * 1024, 16, voff[r], stg * 128u, 0, CP);
-  };
-  if (nstage) {
+      for (int r = 0; r < 8; ++r)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, img + r * 1024, 16, voff[r], stg * 128u, 0, P);
+    };
     issue(0);
     for (uint32_t stg = 0; stg < nstage; ++stg) {
       // hipcc does not order ds_read after an LDS-DMA into the same bytes, so
@@ -164,6 +171,10 @@ __device__ __forceinline__ void xdma_group(H& h, const uint8_t* __restrict__ bas
       h.block(st, w[0]);
       h.block(st, w[1]);
     }
+  };
+  if (nstage) {
+    if (CP == 0 || !lined) run(std::integral_constant<int, 0>{});
+    else run(std::integral_constant<int, CP>{});
   }
   // leftover odd block, then the tail
   const uint64_t i = wave_first + lane;
@@ -578,26 +589,38 @@ __device__ __forceinline__ void desc_xpose_group(H& h, const uint8_t* __restrict
       }
     } else if constexpr (kDma) {
       static_assert(D == 1 && !kHalf, "LDS-DMA image: one full 8 KiB stage");
-      auto issue = [&](uint32_t stg) __attribute__((always_inline)) {
+      // Cache policy per wave: CP (nt for the product kernels) when every
+      // row starts on a 128-B line; otherwise each 128-B stage straddles two
+      // lines and shares one with the row's next stage, and nt loads let that
+      // line leave L2 before the next stage asks for it (16-B-packed ragged
+      // blocks: 1.83x HBM bytes, 1.35x time), so such waves load with the
+      // default policy (profiles/r02_desc_cache_policy_ab.json).
+      const bool lined = __ballot(((uint32_t)off & 127u) != 0 && live && nst != 0) == 0;
+      auto run = [&](auto pol) __attribute__((always_inline)) {
+        constexpr int P = decltype(pol)::value;
+        auto issue = [&](uint32_t stg) __attribute__((always_inline)) {
 #pragma unroll
-        for (int r = 0; r < 8; ++r)
-          __builtin_amdgcn_global_load_lds(rptr[r] + (min(stg, rlast[r]) << 7), img + r * 1024,
-                                           16, 0, CP);
-      };
-      issue(0);
-      for (uint32_t stg = 0; stg < smax; ++stg) {
-        // hipcc does not order ds_read after an LDS-DMA into the same bytes
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        uint4 w[2][4];
-        read_row(w);
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // reads done before the refill
-        if (stg + 1 < smax) issue(stg + 1);
-        __builtin_amdgcn_sched_barrier(0);
-        if (stg < nst) {
-          h.block(st, w[0]);
-          h.block(st, w[1]);
+          for (int r = 0; r < 8; ++r)
+            __builtin_amdgcn_global_load_lds(rptr[r] + (min(stg, rlast[r]) << 7), img + r * 1024,
+                                             16, 0, P);
+        };
+        issue(0);
+        for (uint32_t stg = 0; stg < smax; ++stg) {
+          // hipcc does not order ds_read after an LDS-DMA into the same bytes
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          uint4 w[2][4];
+          read_row(w);
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // reads done before the refill
+          if (stg + 1 < smax) issue(stg + 1);
+          __builtin_amdgcn_sched_barrier(0);
+          if (stg < nst) {
+            h.block(st, w[0]);
+            h.block(st, w[1]);
+          }
         }
-      }
+      };
+      if (CP == 0 || !lined) run(std::integral_constant<int, 0>{});
+      else run(std::integral_constant<int, CP>{});
     } else {
     // D-stage register ring (2*D blocks of prefetch per lane)
     const uint32_t lasts = smax - 1;
@@ -644,11 +667,19 @@ __device__ __forceinline__ void desc_xpose_body(const uint8_t* __restrict__ base
                                                       first, out, img, nlong);
 }
 
+// Occupancy: 81 VGPRs and the 8 KiB image would allow 5 one-wave workgroups
+// per SIMD; claiming VGPRs up to v127 (an empty asm clobber) makes the
+// register file cap it at 4 per SIMD, and the descriptor batches run 3-7 %
+// faster (u16k 3.13 -> 2.89 ms, 16-B-packed ragged 3.14 -> 3.06,
+// profiles/r02_desc_occupancy_ab.json; HYBRID's 163 VGPRs, 3 per SIMD, did
+// the same).  Capping through LDS instead (16 or 12 waves per CU) was slower:
+// with one-wave workgroups an LDS limit is per CU, not per SIMD.
 __global__ void __launch_bounds__(64)
 md5_desc_xdma(const uint8_t* __restrict__ base, const uint64_t* __restrict__ offs,
               const uint32_t* __restrict__ lens, const uint32_t* __restrict__ order, uint64_t n,
               uint4* __restrict__ out) {
   __shared__ __attribute__((aligned(16))) uint8_t img[8192];
+  asm volatile("" ::: "v127");
   desc_xpose_body<2, Md5Hasher<true>, 0, 1, true>(base, offs, lens, order, n, out, img);
 }
 
@@ -759,7 +790,9 @@ __device__ __forceinline__ uint32_t balanced_body(const uint8_t* __restrict__ ba
 
 // the product's shape (profiles/r02_c3_balanced_ab.json,
 // r02_c3_wide_ab.json, r02_c3_cache_policy_ab.json): one wave per SIMD, one
-// 8 KiB image of 128-B stages, one queue, DEFAULT cache policy.  A C3 chunk
+// 8 KiB image of 128-B stages, one queue, the DEFAULT cache policy for any
+// group with a chunk off the 128-B line (nt only for line-aligned groups,
+// as every LDS-DMA loader here).  A C3 chunk
 // starts 16-B aligned, so each 128-B stage straddles two lines and shares one
 // with the next stage; with `nt` loads (the C2 kernel's policy, where chunks
 // are line-aligned) that line left L2 before the next stage came, and HBM
@@ -771,7 +804,7 @@ constexpr int kBalancedWaves = 4;
 constexpr int kBalancedImages = 1;
 constexpr int kBalancedWide = 1;
 constexpr bool kBalancedSplit = false;
-constexpr int kBalancedPolicy = 0;
+constexpr int kBalancedPolicy = 2;   // nt for line-aligned groups only (desc_xpose_group)
 
 template <int WPB, int NB, bool kSplit, int W, int CP>
 __global__ void __launch_bounds__(64 * WPB)
@@ -1013,7 +1046,7 @@ md5_init_ctx(uint32_t* __restrict__ ctxs, uint64_t n) {  // md5.c:153-163 (in[] 
 // is read from registered (pinned, device-mapped) host memory over PCIe and
 // written to its packed place in the slice's HBM buffer.  One workgroup per
 // segment (grid-stride); 16-B accesses when both ends are 16-B aligned
-// (cache pages are 4 KiB aligned, md5_submit.c packs chunks 16-B aligned),
+// (cache pages are 4 KiB aligned, md5_submit.c packs chunks 128-B aligned),
 // bytes otherwise.
 // ---------------------------------------------------------------------------
 struct GatherSeg {

@@ -870,7 +870,10 @@ static long reserve(md5hip_batcher *b, struct slot *sl, const struct chunk_src *
         if (src->dptrs) {                                      /* device-resident: no bytes */
             sl->h_off[sl->n] = src->dptrs[j] - (uint64_t)(uintptr_t)sl->d_data;
         } else {
-            const uint64_t sz = (L + 15) & ~15ull;             /* 16-B aligned packing */
+            /* chunks packed on 128-B lines: the LDS-DMA loaders read 128-B
+             * stages, and a stage off the line shares a line with the next
+             * one (the nt policy is then off, md5_kernels.h) */
+            const uint64_t sz = (L + 127) & ~127ull;
             if (sl->used + sz > b->cap) break;
             if (zc) {
                 const uint64_t ns = src_nseg(src, j);
@@ -934,7 +937,7 @@ static int submit(md5hip_batcher *b, const struct chunk_src *src, uint64_t n, un
     for (uint64_t i = 0; i < n; i++) {
         const uint64_t L = src_len(src, i);
         if (L > 0xffffffffull) return -E2BIG;
-        if (!src->dptrs && (L + 15) / 16 * 16 > b->cap) return -E2BIG;
+        if (!src->dptrs && (L + 127) / 128 * 128 > b->cap) return -E2BIG;
     }
     struct dev_guard g;
     if (dev_enter(&g, b->device)) return -ENODEV;
