@@ -374,6 +374,7 @@ struct DescArrays {
   const uint32_t* __restrict__ lens;
   const uint32_t* __restrict__ order;
   static constexpr bool kPairXor = false;
+  static constexpr bool kAbs = false;          // off() is relative to base
   __device__ __forceinline__ uint64_t index(uint64_t i) const { return order ? (uint64_t)order[i] : i; }
   __device__ __forceinline__ uint64_t off(uint64_t c) const { return offs[c]; }
   __device__ __forceinline__ uint32_t len(uint64_t c) const { return lens[c]; }
@@ -390,6 +391,7 @@ struct FastWindows {
   uint64_t stride;
   uint32_t flen, F;
   static constexpr bool kPairXor = true;
+  static constexpr bool kAbs = false;
   __device__ __forceinline__ uint64_t index(uint64_t i) const { return i; }
   __device__ __forceinline__ uint32_t clen(uint64_t k) const { return offs ? lens[k] : flen; }
   __device__ __forceinline__ uint64_t off(uint64_t c) const {
@@ -448,7 +450,7 @@ __device__ __forceinline__ void desc_xpose_group(H& h, const uint8_t* __restrict
   const bool live = i < n;
   const uint64_t c = src.index(live ? i : first);
   const uint64_t off = src.off(c);
-  const uint8_t* chunk = base + off;
+  const uint8_t* chunk = Src::kAbs ? reinterpret_cast<const uint8_t*>((uintptr_t)off) : base + off;
   const uint32_t len = live ? src.len(c) : 0u;
   const uint32_t nfull = len >> 6;
   const uint32_t nst = nfull >> 1;                       // this lane's 128-B stages
@@ -487,7 +489,8 @@ __device__ __forceinline__ void desc_xpose_group(H& h, const uint8_t* __restrict
       const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)off, (int)row, 64);
       const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(off >> 32), (int)row, 64);
       const uint32_t part = (lane & 7u) ^ ((row >> 1) & 7u);      // source swizzle (xpose)
-      rptr[r] = base + ((((uint64_t)hi << 32) | lo) + part * 16u);
+      const uint64_t ra = (((uint64_t)hi << 32) | lo) + part * 16u;
+      rptr[r] = Src::kAbs ? reinterpret_cast<const uint8_t*>((uintptr_t)ra) : base + ra;
       rlast[r] = (rn ? rn : smax) - 1u;
     }
     const uint32_t g = (lane >> 1) & 7u;
@@ -910,16 +913,42 @@ __device__ __forceinline__ void ctx_store(uint32_t* p, const CtxWords& c) {
 #pragma unroll
   for (int k = 0; k < 22; ++k) p[k] = c.w[k];
 }
-__global__ void __launch_bounds__(256)
+// The whole 64-B blocks of an update go through the descriptor loader
+// (desc_xpose_group: LDS-DMA 128-B stages of 8 contexts' data per
+// wave-instruction, per-lane trip counts), each lane starting from its own
+// context's state instead of MD5Init's, and nothing appended after them:
+// CtxHasher's finish is empty and its store hands the state back.  LaneSpan
+// is the lane's own (absolute address, length) -- the bulk of its update.
+struct CtxHasher : Md5Hasher<true> {
+  State s0, res;
+  __device__ __forceinline__ State init() { return s0; }
+  __device__ __forceinline__ void finish(State&, const uint8_t*, uint32_t, uint64_t) {}
+  __device__ __forceinline__ void store(Out*, uint64_t, const State& st) { res = st; }
+};
+struct LaneSpan {
+  uint64_t addr;
+  uint32_t n;
+  static constexpr bool kPairXor = false;
+  static constexpr bool kAbs = true;
+  __device__ __forceinline__ uint64_t index(uint64_t i) const { return i; }
+  __device__ __forceinline__ uint64_t off(uint64_t) const { return addr; }
+  __device__ __forceinline__ uint32_t len(uint64_t) const { return n; }
+};
+
+// One wave per 64 contexts (one-wave workgroups, the loader's 8 KiB image);
+// 125 VGPRs hold it at 4 waves per SIMD, as md5_desc_xdma's clobber does.
+__global__ void __launch_bounds__(64)
 md5_update_ctx(uint32_t* __restrict__ ctxs, const uint64_t* __restrict__ ptrs,
                const uint32_t* __restrict__ lens, uint64_t n) {
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  uint32_t* cp = ctxs + 22 * i;
+  __shared__ __attribute__((aligned(16))) uint8_t img[8192];
+  const uint64_t first = (uint64_t)blockIdx.x * 64u;
+  const uint64_t i = first + (threadIdx.x & 63u);
+  const bool live = i < n;
+  uint32_t* cp = ctxs + 22 * (live ? i : first);
   CtxWords c;
   ctx_load(c, cp);
-  const uint32_t len = lens[i];
-  const uint8_t* data = reinterpret_cast<const uint8_t*>(ptrs[i]);
+  const uint32_t len = live ? lens[i] : 0u;
+  const uint8_t* data = reinterpret_cast<const uint8_t*>(live ? ptrs[i] : 0ull);
   const uint32_t t0 = c.w[4];
   const uint32_t lo = t0 + (len << 3);                 // md5.c:179-182
   c.w[5] += (lo < t0 ? 1u : 0u) + (len >> 29);
@@ -928,27 +957,23 @@ md5_update_ctx(uint32_t* __restrict__ ctxs, const uint64_t* __restrict__ ptrs,
   uint32_t in[16];
 #pragma unroll
   for (int j = 0; j < 16; ++j) in[j] = c.w[6 + j];
-  if (t && len < 64u - t) {                            // md5.c:189-192: no block completes
-    for (uint32_t k = 0; k < len; ++k) {
-      const uint32_t pos = t + k;
-      const uint32_t b = data[k];
-#pragma unroll
-      for (int j = 0; j < 16; ++j)
-        if ((uint32_t)j == (pos >> 2)) {
-          const uint32_t sh = 8u * (pos & 3u);
-          in[j] = (in[j] & ~(0xFFu << sh)) | (b << sh);
-        }
-    }
-#pragma unroll
-    for (int j = 0; j < 16; ++j) c.w[6 + j] = in[j];
-    ctx_store(cp, c);
-    return;
-  }
+  const bool append_only = t && len < 64u - t;         // md5.c:189-192: no block completes
   State st{c.w[0], c.w[1], c.w[2], c.w[3]};
   uint32_t pos = 0;                                    // bytes of data consumed
   uint32_t last[16];                                   // the last block compressed
   bool any = false;
-  if (t) {                                             // md5.c:194-199: complete the pending block
+  if (append_only) {
+    for (uint32_t k = 0; k < len; ++k) {
+      const uint32_t p2 = t + k;
+      const uint32_t b = data[k];
+#pragma unroll
+      for (int j = 0; j < 16; ++j)
+        if ((uint32_t)j == (p2 >> 2)) {
+          const uint32_t sh = 8u * (p2 & 3u);
+          in[j] = (in[j] & ~(0xFFu << sh)) | (b << sh);
+        }
+    }
+  } else if (t) {                                      // md5.c:194-199: complete the pending block
     const uint32_t need = 64u - t;
 #pragma unroll
     for (int j = 0; j < 16; ++j) last[j] = in[j];
@@ -966,22 +991,29 @@ md5_update_ctx(uint32_t* __restrict__ ctxs, const uint64_t* __restrict__ ptrs,
     pos = need;
     any = true;
   }
-  const uint32_t nblk = (len - pos) >> 6;             // md5.c:204-210
-  if (nblk) {
-    const uint8_t* p = data + pos;
-    const bool aligned = ((uintptr_t)p & 15u) == 0;
-    uint4 w[4];
-    for (uint32_t blk = 0; blk < nblk; ++blk) {
-      if (aligned) load_block(w, reinterpret_cast<const uint4*>(p + ((uint64_t)blk << 6)));
-      else load_block_unaligned(w, p + ((uint64_t)blk << 6));
-      compress_regs(st, w);
-      if (blk + 1 == nblk) {
+  const uint32_t nblk = append_only ? 0u : (len - pos) >> 6;   // md5.c:204-210
+  CtxHasher h;
+  h.s0 = st;
+  h.res = st;
+  desc_xpose_group<2, CtxHasher, 0, 1, false, true, true, LaneSpan>(
+      h, nullptr, LaneSpan{(uint64_t)(uintptr_t)(data + pos), nblk << 6}, n, first, nullptr, img);
+  if (!live) return;
+  if (append_only) {
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          last[4 * k] = w[k].x; last[4 * k + 1] = w[k].y;
-          last[4 * k + 2] = w[k].z; last[4 * k + 3] = w[k].w;
-        }
-      }
+    for (int j = 0; j < 16; ++j) c.w[6 + j] = in[j];
+    ctx_store(cp, c);
+    return;
+  }
+  st = h.res;
+  if (nblk) {                                          // the bytes md5.c leaves in in[] past the tail
+    const uint8_t* lb = data + pos + ((uint64_t)(nblk - 1) << 6);
+    uint4 w[4];
+    if (((uintptr_t)lb & 15u) == 0) load_block(w, reinterpret_cast<const uint4*>(lb));
+    else load_block_unaligned(w, lb);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      last[4 * k] = w[k].x; last[4 * k + 1] = w[k].y;
+      last[4 * k + 2] = w[k].z; last[4 * k + 3] = w[k].w;
     }
     pos += nblk << 6;
     any = true;

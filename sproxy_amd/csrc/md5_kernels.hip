@@ -288,9 +288,9 @@ int md5hip_update_ctx(struct MD5Context* d_ctxs, const void* const* d_ptrs, cons
   if (n == 0) return 0;
   if (!d_ctxs || !d_ptrs || !d_lens || ((uintptr_t)d_ctxs & 3u)) return -EINVAL;
   if (int e = device_ok()) return e;
-  const uint64_t g = (n + kBlock - 1) / kBlock;
+  const uint64_t g = (n + 63) / 64;                   // one wave per 64 contexts
   if (g > 0x7fffffffull) return -EINVAL;
-  hipLaunchKernelGGL(md5_update_ctx, dim3((uint32_t)g), dim3(kBlock), 0, (hipStream_t)stream,
+  hipLaunchKernelGGL(md5_update_ctx, dim3((uint32_t)g), dim3(64), 0, (hipStream_t)stream,
                      reinterpret_cast<uint32_t*>(d_ctxs), reinterpret_cast<const uint64_t*>(d_ptrs),
                      d_lens, n);
   return launched();
