@@ -136,3 +136,30 @@ def test_bit_count_carry_and_high_word(cuda):
     ref.update(ctx_h, data, offs, lens)
     assert ref.same(ctx.cpu().numpy(), ctx_h)
     assert np.array_equal(m.final_ctx(ctx).cpu().numpy(), ref.final(ctx_h))
+
+
+def test_lds_dma_waves_and_pending_blocks(cuda):
+    """Waves whose update data is 16-B (and 128-B) aligned take the LDS-DMA
+    loader (md5_update_ctx -> desc_xpose_group); contexts with a pending
+    partial block shift the bulk by 64 - t bytes, so neighbouring waves mix
+    the DMA and lane-direct paths.  Three rounds, every context byte against
+    the reference after each."""
+    ref = HostRef()
+    rng = np.random.default_rng(4242)
+    n = 64 * 24
+    data = gen.xorshift_array(12 << 20, seed=91)
+    d = _dev(data, cuda)
+    ctx_h = np.zeros((n, 88), np.uint8)
+    ctx = _dev(ctx_h, cuda)
+    m.init_ctx(ctx)
+    ctx_h = ctx.cpu().numpy()
+    wave = np.arange(n) // 64
+    for r in range(3):
+        lens = rng.integers(1, 200, n) * 64 + np.where(wave % 3 == 0, 0, rng.integers(0, 64, n))
+        offs = rng.integers(0, (data.size - 20000) // 128, n) * 128
+        offs = np.where(wave % 4 == 1, offs + 16 * rng.integers(1, 8, n), offs)   # 16-B, off the line
+        offs = np.where(wave % 4 == 2, offs + rng.integers(1, 16, n), offs)       # unaligned waves
+        _update(ctx, d, offs, lens, cuda)
+        ref.update(ctx_h, data, offs, lens)
+        assert ref.same(ctx.cpu().numpy(), ctx_h), r
+    assert np.array_equal(m.final_ctx(ctx).cpu().numpy(), ref.final(ctx_h))
