@@ -830,6 +830,7 @@ def run_ctx(a, rank, world, local, device, backend):
                            np.full(idx.size, L * reps), dig.index_select(0, torch.from_numpy(idx).to(dig.device)).cpu().numpy())
     alg = float(n) * (L + 2 * 88)
     achieved = alg / (dev_ms_max * 1e-3) / 1e9
+    traffic, tnote = load_traffic(a.traffic, "md5_update_ctx", f"ctx@{n}x{L}")
     res = {"metric": "device-resident batched MD5Update GiB/s (md5hip_update_ctx, 16 KiB per context per call)",
            "value": round(float(n) * L * world * a.steps / wall_max / GIB, 2), "unit": "GiB/s",
            "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
@@ -839,7 +840,8 @@ def run_ctx(a, rank, world, local, device, backend):
            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": round(achieved / HBM_PEAK_GBS, 4), "kernel": "md5hip::md5_update_ctx",
                         "avg_launch_ms": round(dev_ms_max, 4), "alg_bytes_per_launch": int(alg),
-                        "alg_bytes_note": "block bytes + the 88-B context read and written", "traffic": None}}
+                        "alg_bytes_note": "block bytes + the 88-B context read and written",
+                        "traffic": traffic, "traffic_source": tnote}}
     return per_rank_line(res, rank, world, local, device, backend, float(n) * L * a.steps, wall, par)
 
 
