@@ -877,6 +877,88 @@ crc32_fast_xdma16(const uint8_t* __restrict__ base, const uint64_t* __restrict__
                                                                                gi * 64u, out, img);
 }
 
+// fastcrc with F = 64 or 128 (the netcache harness runs 128): every window
+// is one or two whole 64-B blocks, so a group of 64 windows is one short
+// load round trip plus a few hundred VALU -- latency, not bandwidth, bound
+// it in crc32_fast_xdma16 (one group in flight per wave).  Here each lane
+// loads its own window straight into VGPRs (no LDS image: the 64 KiB of
+// tables leave room for 16 waves per CU) and the NEXT group's windows are
+// loaded before the current group is hashed, so a load round trip always
+// runs under a group's compression.  A group with a window that is not
+// exactly F bytes at a 16-B-aligned address (a chunk of <= F bytes, a
+// ragged tail window) is hashed lane-direct (lane_range) with nothing in
+// flight beside it.  Persistent: one 1024-thread workgroup per CU, groups
+// wave-major, grid-stride.
+__global__ void __launch_bounds__(1024)
+crc32_fast_pipe(const uint8_t* __restrict__ base, const uint64_t* __restrict__ offs,
+                const uint32_t* __restrict__ lens, uint64_t n, uint64_t stride, uint32_t flen,
+                uint32_t F, uint32_t* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds[Crc32PermHasher::kLdsBytes];
+  Crc32PermHasher h;
+  h.setup(lds);
+  const FastWindows src{offs, lens, stride, flen, F};
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint64_t rows = 2 * n;
+  const uint64_t ngroups = (rows + 63) / 64;
+  const uint64_t step = (uint64_t)gridDim.x * (blockDim.x >> 6);
+  const uint32_t nb = F >> 6;                             // 1 or 2 blocks per window
+  struct Win {
+    const uint8_t* p;
+    uint32_t len;
+    bool live;
+    bool pipe;                                            // wave-uniform
+  };
+  auto locate = [&](uint64_t gi) __attribute__((always_inline)) {
+    Win w;
+    const uint64_t c = gi * 64u + lane;
+    w.live = c < rows;
+    w.len = w.live ? src.len(c) : 0u;
+    w.p = base + src.off(w.live ? c : gi * 64u);         // dead lanes read a live row
+    const bool simple = !w.live || (w.len == F && ((uintptr_t)w.p & 15u) == 0);
+    w.pipe = __ballot(!simple) == 0;
+    return w;
+  };
+  auto fetch = [&](const Win& w, uint4 (&W)[2][4]) __attribute__((always_inline)) {
+    load_block(W[0], reinterpret_cast<const uint4*>(w.p));
+    if (nb == 2) load_block(W[1], reinterpret_cast<const uint4*>(w.p + 64));
+  };
+  auto hash = [&](const Win& w, uint64_t gi, uint4 (&W)[2][4]) __attribute__((always_inline)) {
+    typename Crc32PermHasher::State st = h.init();
+    if (w.pipe) {
+      h.block(st, W[0]);
+      if (nb == 2) h.block(st, W[1]);
+      h.finish(st, w.p, 0u, F);
+    } else if (w.live) {
+      lane_range<Crc32PermHasher, 2>(h, st, w.p, w.len);
+    }
+    if (w.live) emit<FastWindows>(h, out, gi * 64u + lane, st);
+  };
+  uint64_t gi = (uint64_t)wave * gridDim.x + blockIdx.x;
+  if (gi >= ngroups) return;
+  uint4 A[2][4], B[2][4];
+  Win a = locate(gi);
+  if (a.pipe) fetch(a, A);
+  for (;;) {                                             // two groups per trip: A, then B
+    const uint64_t g1 = gi + step;
+    Win b{};
+    if (g1 < ngroups) {
+      b = locate(g1);
+      if (b.pipe) fetch(b, B);
+    }
+    hash(a, gi, A);
+    if (g1 >= ngroups) break;
+    const uint64_t g2 = g1 + step;
+    if (g2 < ngroups) {
+      a = locate(g2);
+      if (a.pipe) fetch(a, A);
+    }
+    hash(b, g1, B);
+    if (g2 >= ngroups) break;
+    gi = g2;
+  }
+}
+
 template <bool kImplicit>
 __global__ void __launch_bounds__(256)
 crc32_desc(const uint8_t* __restrict__ base, const uint64_t* __restrict__ offs,

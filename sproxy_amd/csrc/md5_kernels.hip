@@ -225,6 +225,13 @@ int crc32hip_fixed_variant(const void* d_base, uint64_t n, uint32_t len, uint64_
   const uint64_t g = (n + kDescBlock - 1) / kDescBlock;
   if (g > 0x7fffffffull) return -EINVAL;
   if (fastcrc && len > fastcrc) {
+    if (fastcrc == 64 || fastcrc == 128) {
+      // one- or two-block windows: lane loads, next group in flight
+      hipLaunchKernelGGL(crc32_fast_pipe, dim3(per_cu_grid(2 * n)), dim3(1024), 0, s, base,
+                         (const uint64_t*)nullptr, (const uint32_t*)nullptr, n, stride, len, fastcrc,
+                         d_crcs);
+      return launched();
+    }
     // head and tail windows as 2n rows through the LDS-DMA loader
     hipLaunchKernelGGL(crc32_fast_xdma16, dim3(per_cu_grid(2 * n)), dim3(768), 0, s, base,
                        (const uint64_t*)nullptr, (const uint32_t*)nullptr, n, stride, len, fastcrc,
@@ -259,6 +266,12 @@ int crc32hip_desc(const void* d_base, const uint64_t* d_offsets, const uint32_t*
   hipStream_t s = (hipStream_t)stream;
   const uint64_t g = (n + kDescBlock - 1) / kDescBlock;
   if (g > 0x7fffffffull) return -EINVAL;
+  if (fastcrc == 64 || fastcrc == 128) {
+    hipLaunchKernelGGL(crc32_fast_pipe, dim3(per_cu_grid(2 * n)), dim3(1024), 0, s,
+                       (const uint8_t*)d_base, d_offsets, d_lens, n, (uint64_t)0, 0u, fastcrc,
+                       d_crcs);
+    return launched();
+  }
   if (fastcrc) {
     hipLaunchKernelGGL(crc32_fast_xdma16, dim3(per_cu_grid(2 * n)), dim3(768), 0, s,
                        (const uint8_t*)d_base, d_offsets, d_lens, n, (uint64_t)0, 0u, fastcrc,

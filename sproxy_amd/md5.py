@@ -303,7 +303,7 @@ def crc_kernel_name(length: int, fastcrc: int = 0) -> str:
     """The kernel crc32hip_fixed launches for 16-B aligned chunks of `length`
     bytes (bench.py's roofline names it)."""
     if 0 < fastcrc < length:
-        return "crc32_fast_xdma16"
+        return "crc32_fast_pipe" if fastcrc in (64, 128) else "crc32_fast_xdma16"
     return "crc32_fixed_" + crc_variant_name(0)
 
 

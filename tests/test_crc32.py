@@ -98,7 +98,7 @@ def test_gpu_crc_edges_fixed_and_unaligned(cuda, variant):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("fast", [0, 4, 128, 4096])
+@pytest.mark.parametrize("fast", [0, 4, 64, 128, 4096])
 def test_gpu_crc_desc_fastcrc(cuda, fast):
     import torch
     lens = gen.mixed_lengths(300, seed=31, max_len=1 << 17) + [0, 1, 4, 127, 128, 129, 4095, 4097]
@@ -177,10 +177,12 @@ def test_gpu_crc_desc_netcache_blocks(cuda):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("fast", [4, 100, 128, 1000, 16368])
+@pytest.mark.parametrize("fast", [4, 64, 100, 128, 1000, 16368])
 def test_gpu_fastcrc_xdma_windows(cuda, fast):
-    """fastcrc through the LDS-DMA loader (crc32_fast_xdma16): head and tail
-    windows as row pairs, more 32-chunk groups than one grid holds, fixed
+    """fastcrc through the LDS-DMA loader (crc32_fast_xdma16) and, for 64 and
+    128, the pipelined lane-load kernel (crc32_fast_pipe, whose ragged and
+    unaligned groups fall back to lane_range): head and tail windows as row
+    pairs, more 32-chunk groups than one grid holds, fixed
     16 KiB blocks and 16-B packed ragged blocks (windows of every alignment,
     blocks shorter than the window, empty blocks), against crc32.c's
     blk_make_crc combination (blk_io.c:408-424) in the oracle."""
