@@ -30,8 +30,8 @@ NAMES = {0: "w4_nb1_s1", 1: "w4_nb2_s1", 5: "w4_nb1_s2", 6: "w4_nb1_s4", 7: "w4_
          12: "loads_w4_nb2_s1", 13: "loads_w8_nb1_s1", 14: "w4_nb1_s5", 15: "loads_w4_nb1_s5",
          16: "w4_nb1_s4_cached", 17: "loads_w4_nb1_s4_cached", 18: "w4_nb1_s2_cached", 19: "w4_nb1_s1_cached",
          20: "w4_nb2_s1_cached", 21: "w8_nb1_s1_cached", 22: "loads_w4_nb1_s1_cached",
-         23: "w8_split_s1_cached"}
-HASHING = (0, 1, 5, 6, 7, 14, 16, 18, 19, 20, 21, 23)
+         23: "w8_split_s1_cached", 24: "product_shape_long_lane_256k", 25: "product_shape_long_lane_1m"}
+HASHING = (0, 1, 5, 6, 7, 14, 16, 18, 19, 20, 21, 23, 24, 25)
 PRODUCT = ("balanced", "hybrid", "xdma")
 
 
@@ -39,7 +39,7 @@ def main():
     p = argparse.ArgumentParser()
     p.add_argument("--batches", type=int, nargs="+", default=[3, 5])
     p.add_argument("--rounds", type=int, default=3)
-    p.add_argument("--kinds", type=int, nargs="+", default=sorted(NAMES))
+    p.add_argument("--kinds", type=int, nargs="*", default=sorted(NAMES))
     a = p.parse_args()
     D = ctypes.CDLL(DIAG)
     vp = ctypes.c_void_p

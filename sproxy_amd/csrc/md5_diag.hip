@@ -1092,7 +1092,8 @@ extern "C" int md5diag_desc_x(int kind, const void* base, const uint64_t* offs, 
 // per persistent wave: its whole run over the groups it took, and how many)
 // for WPB waves per workgroup, NB LDS-DMA images per wave, split queues (A/B).
 namespace md5hip {
-template <int WPB, int NB, bool kSplit, int W = 1, bool kHashOff = false, int CP = 2>
+template <int WPB, int NB, bool kSplit, int W = 1, bool kHashOff = false, int CP = 2,
+          uint32_t kLong = 0>
 __global__ void __launch_bounds__(64 * WPB)
 diag_desc_balanced(const uint8_t* __restrict__ base, const uint64_t* __restrict__ offs,
                    const uint32_t* __restrict__ lens, const uint32_t* __restrict__ order, uint64_t n,
@@ -1100,7 +1101,8 @@ diag_desc_balanced(const uint8_t* __restrict__ base, const uint64_t* __restrict_
   extern __shared__ __attribute__((aligned(16))) uint8_t lds_dyn[];
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
   const uint32_t taken =
-      balanced_body<WPB, NB, kSplit, W, kHashOff, CP>(base, offs, lens, order, n, out, ctr, lds_dyn);
+      balanced_body<WPB, NB, kSplit, W, kHashOff, CP, kLong>(base, offs, lens, order, n, out, ctr,
+                                                            lds_dyn);
   const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
   if ((threadIdx.x & 63u) == 0 && rec) {
     uint32_t hw, xcc;
@@ -1117,12 +1119,13 @@ diag_desc_balanced(const uint8_t* __restrict__ base, const uint64_t* __restrict_
 }  // namespace md5hip
 
 namespace {
-template <int WPB, int NB, bool kSplit, int W = 1, bool kHashOff = false, int CP = 2>
+template <int WPB, int NB, bool kSplit, int W = 1, bool kHashOff = false, int CP = 2,
+          uint32_t kLong = 0>
 int diag_launch_balanced(const void* base, const uint64_t* offs, const uint32_t* lens,
                          const uint32_t* order, uint64_t n, void* out, uint32_t* ctr, void* rec,
                          hipStream_t s) {
   const uint32_t lds = BalancedCfg<WPB, NB, W>::kLds;
-  auto kern = diag_desc_balanced<WPB, NB, kSplit, W, kHashOff, CP>;
+  auto kern = diag_desc_balanced<WPB, NB, kSplit, W, kHashOff, CP, kLong>;
   if (hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
     return -ENODEV;
@@ -1141,7 +1144,8 @@ int diag_launch_balanced(const void* base, const uint64_t* offs, const uint32_t*
 // policy instead of nt (lines stay in L2: a 16-B-aligned chunk's visit
 // boundaries share a 128-B line): 16 = 4/1/4, 17 = 4/1/4 loads only,
 // 18 = 4/1/2, 19 = 4/1/1 (the product's shape), 20 = 4/2/1, 21 = 8/1/1, 22 = 4/1/1 loads only,
-// 23 = 8/1/1 split queues.
+// 23 = 8/1/1 split queues; 24 / 25 = the product's shape with groups whose
+// longest chunk is >= 256 KiB / 1 MiB run lane-direct (HYBRID's long path).
 extern "C" int md5diag_desc_balanced(int kind, const void* base, const uint64_t* offs,
                                      const uint32_t* lens, const uint32_t* order, uint64_t n,
                                      void* out, void* rec, void* stream) {
@@ -1175,6 +1179,10 @@ extern "C" int md5diag_desc_balanced(int kind, const void* base, const uint64_t*
     case 21: return diag_launch_balanced<8, 1, false, 1, false, 0>(base, offs, lens, order, n, out, ctr, rec, s);
     case 22: return diag_launch_balanced<4, 1, false, 1, true, 0>(base, offs, lens, order, n, out, ctr, rec, s);
     case 23: return diag_launch_balanced<8, 1, true, 1, false, 0>(base, offs, lens, order, n, out, ctr, rec, s);
+    case 24: return diag_launch_balanced<4, 1, false, 1, false, 2, kHybridLongBlocks>(base, offs, lens, order, n, out,
+                                                                                     ctr, rec, s);
+    case 25: return diag_launch_balanced<4, 1, false, 1, false, 2, 4 * kHybridLongBlocks>(base, offs, lens, order, n,
+                                                                                         out, ctr, rec, s);
     default: return -EINVAL;
   }
 }

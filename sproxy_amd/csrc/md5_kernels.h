@@ -730,7 +730,8 @@ struct BalancedCfg {
 // latency), two long chains on one SIMD halve each other's speed.
 // ctr[0] long (all groups, unsplit), ctr[1] short, ctr[2] waves done.
 // Returns the number of groups this wave took (diagnostics).
-template <int WPB, int NB, bool kSplit, int W = 1, bool kHashOff = false, int CP = 2>
+template <int WPB, int NB, bool kSplit, int W = 1, bool kHashOff = false, int CP = 2,
+          uint32_t kLong = 0>
 __device__ __forceinline__ uint32_t balanced_body(const uint8_t* __restrict__ base,
                                                   const uint64_t* __restrict__ offs,
                                                   const uint32_t* __restrict__ lens,
@@ -777,8 +778,8 @@ __device__ __forceinline__ uint32_t balanced_body(const uint8_t* __restrict__ ba
       if (g == ~0ull) break;
     }
     ++taken;
-    desc_xpose_group<CP, Md5Hasher<true>, 0, 1, false, true, true, DescArrays, true, NB, W, kHashOff>(
-        h, base, src, n, g * 64u, out, img);
+    desc_xpose_group<CP, Md5Hasher<true>, kLong, 1, false, true, true, DescArrays, true, NB, W, kHashOff>(
+        h, base, src, n, g * 64u, out, img, 0xFFFFFFFFu);   // kLong: every long group lane-direct
   }
   if (lane == 0) {
     const uint32_t total = gridDim.x * (blockDim.x >> 6);
