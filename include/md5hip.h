@@ -222,6 +222,12 @@ int md5hip_batcher_get_digest(const md5hip_batcher *b, int *kind, uint32_t *fast
  * flight (1..nslots; default 2, or 1 with fewer than 3 slots).  1 coalesces
  * hardest; nslots never waits to coalesce. */
 int md5hip_batcher_set_inflight(md5hip_batcher *b, uint32_t target);
+/* Linger: with nothing in flight, an asynchronous submission's slot is held
+ * up to min(max_us, 1/8 of the recent launches' wall time) for more work to
+ * join it, so a burst of vectors goes out as one launch.  A wait, poll or
+ * flush on one of its tickets, a full slot or a synchronous submission still
+ * launches at once.  Default max_us 5000; 0 = launch at once. */
+int md5hip_batcher_set_linger(md5hip_batcher *b, uint32_t max_us);
 
 struct md5hip_batcher_stats {
     uint64_t submissions;             /* tickets issued */

@@ -195,6 +195,11 @@ struct slot {
     uint64_t fx_bytes, fx_stride;
     uint32_t fx_len;
     uint64_t tickets_in;              /* distinct tickets (stats) */
+    /* descriptors already on the device / the plan they were ordered by:
+     * prepared ahead while another slot's launch runs (slot_prepare) */
+    uint64_t copied_n, planned_n, seen_n;
+    int plan_var;
+    uint64_t opened_us, launched_us;  /* first chunk reserved / went in flight */
 };
 
 struct md5hip_batcher {
@@ -208,6 +213,8 @@ struct md5hip_batcher {
     uint64_t segcap;   /* gather segments per slot (zero-copy modes) */
     int gather;        /* enum md5hip_gather_mode */
     uint32_t target;   /* launch the open slot at once while fewer slots are in flight */
+    uint32_t linger_max_us;  /* idle pipeline: hold a slot up to this long for more work */
+    double launch_ema_us;    /* recent launches' wall time (submit to retire) */
     struct slot *s;
     int open;          /* index of the OPEN slot new chunks go to, -1 = none */
     uint32_t inflight;
@@ -226,6 +233,35 @@ struct md5hip_batcher {
 };
 
 #define CK(x) do { if ((x) != hipSuccess) { rc = -ENODEV; goto fail; } } while (0)
+
+static uint64_t now_us(void)
+{
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return (uint64_t)ts.tv_sec * 1000000u + (uint64_t)ts.tv_nsec / 1000u;
+}
+
+/* How long an idle pipeline holds an open slot for more work: 1/8 of the
+ * recent launches' wall time, at most linger_max_us.  A burst of vectors
+ * submitted back to back then goes out as one launch instead of its first
+ * vector alone (a mixed vector alone is bound by its longest chains, DESIGN.md
+ * §5.4), and the added latency stays a fraction of the work itself. */
+static uint64_t linger_us(const md5hip_batcher *b)
+{
+    const double l = b->launch_ema_us / 8.0;
+    return l < (double)b->linger_max_us ? (uint64_t)l : (uint64_t)b->linger_max_us;
+}
+
+/* pthread_cond_timedwait on work_cv until `us` microseconds from now (mu held) */
+static void wait_work_us(md5hip_batcher *b, uint64_t us)
+{
+    struct timespec ts;
+    clock_gettime(CLOCK_REALTIME, &ts);
+    ts.tv_sec += (time_t)(us / 1000000u);
+    ts.tv_nsec += (long)(us % 1000000u) * 1000;
+    if (ts.tv_nsec >= 1000000000L) { ts.tv_sec++; ts.tv_nsec -= 1000000000L; }
+    pthread_cond_timedwait(&b->work_cv, &b->mu, &ts);
+}
 
 static int tk_grow(md5hip_batcher *b)
 {
@@ -303,6 +339,34 @@ static int seg_has(const struct slot *sl, uint64_t t)
     return 0;
 }
 
+/* Descriptors in and the plan (mu held): the new descriptor entries
+ * [copied_n, n) go to the device, the whole slot is ordered longest-first
+ * (md5hip_plan_desc) and the order follows, all on the slot's own stream.
+ * Descriptors are final once reserved (append-only), so this may run while
+ * the slot is still OPEN -- the progress thread does it while another slot's
+ * launch keeps the device busy, and the launch then only enqueues the kernel.
+ * Chunks appended after it are copied and the slot re-planned at launch (an
+ * order copy still in flight is overwritten by the later one, same stream). */
+static int slot_prepare(md5hip_batcher *b, struct slot *sl)
+{
+    (void)b;
+    const uint64_t n = sl->n;
+    if (sl->planned_n == n) return 0;
+    if (n > sl->copied_n) {
+        const uint64_t c0 = sl->copied_n;
+        if (hipMemcpyAsync(sl->d_off + c0, sl->h_off + c0, 8 * (n - c0), hipMemcpyHostToDevice, sl->stream) ||
+            hipMemcpyAsync(sl->d_len + c0, sl->h_len + c0, 4 * (n - c0), hipMemcpyHostToDevice, sl->stream))
+            return -EIO;
+        sl->copied_n = n;
+    }
+    const int dvar = md5hip_plan_desc(sl->h_len, n, sl->h_ord);
+    if (dvar < 0) return dvar;
+    if (hipMemcpyAsync(sl->d_ord, sl->h_ord, 4 * n, hipMemcpyHostToDevice, sl->stream)) return -EIO;
+    sl->plan_var = dvar;
+    sl->planned_n = n;
+    return 0;
+}
+
 /* Enqueue slot `sl` (mu held, writers == 0): bytes in, kernel, digests out. */
 static int slot_enqueue(md5hip_batcher *b, struct slot *sl)
 {
@@ -317,12 +381,8 @@ static int slot_enqueue(md5hip_batcher *b, struct slot *sl)
                  : md5hip_digest_fixed(sl->d_data, n, sl->fx_len, sl->fx_stride, sl->d_dig, sl->stream);
         if (rc) return rc;
     } else {
-        const int dvar = md5hip_plan_desc(sl->h_len, n, sl->h_ord);
-        if (dvar < 0) return dvar;
-        if (hipMemcpyAsync(sl->d_off, sl->h_off, 8 * n, hipMemcpyHostToDevice, sl->stream) ||
-            hipMemcpyAsync(sl->d_len, sl->h_len, 4 * n, hipMemcpyHostToDevice, sl->stream) ||
-            hipMemcpyAsync(sl->d_ord, sl->h_ord, 4 * n, hipMemcpyHostToDevice, sl->stream))
-            return -EIO;
+        if ((rc = slot_prepare(b, sl))) return rc;
+        const int dvar = sl->plan_var;
         if (sl->mode == MODE_STAGED && sl->used) {
             if (hipMemcpyAsync(sl->d_data, sl->h_data, sl->used, hipMemcpyHostToDevice, sl->stream))
                 return -EIO;
@@ -385,6 +445,7 @@ static void slot_reset(struct slot *sl)
     sl->n = sl->used = sl->nseg = sl->ndma = sl->ndsc = 0;
     sl->nsegs = 0;
     sl->tickets_in = 0;
+    sl->copied_n = sl->planned_n = sl->seen_n = 0;
 }
 
 /* Deliver a finished (or failed) slot to its tickets and free it (mu held). */
@@ -396,7 +457,11 @@ static void slot_retire(md5hip_batcher *b, struct slot *sl, int err)
             memcpy(g->user, sl->h_dig + (size_t)sl->dsz * g->first, (size_t)sl->dsz * g->count);
         tk_put(b, g->ticket, err);
     }
-    if (sl->state == SLOT_INFLIGHT) b->inflight--;
+    if (sl->state == SLOT_INFLIGHT) {
+        b->inflight--;
+        const double d = (double)(now_us() - sl->launched_us);
+        b->launch_ema_us = b->launch_ema_us > 0 ? 0.75 * b->launch_ema_us + 0.25 * d : d;
+    }
     slot_reset(sl);
     pthread_cond_broadcast(&b->done_cv);
 }
@@ -411,6 +476,10 @@ static void slot_try_launch(md5hip_batcher *b, struct slot *sl)
         return;
     }
     if (!(sl->full || sl->flush || b->inflight < b->target)) return;
+    if (!sl->full && !sl->flush && b->inflight == 0 && now_us() - sl->opened_us < linger_us(b)) {
+        pthread_cond_broadcast(&b->work_cv);        /* the progress thread times the linger */
+        return;
+    }
     if (b->open == (int)(sl - b->s)) b->open = -1;
     const int rc = sl->err ? sl->err : slot_enqueue(b, sl);
     if (rc) {
@@ -418,6 +487,7 @@ static void slot_try_launch(md5hip_batcher *b, struct slot *sl)
         return;
     }
     sl->state = SLOT_INFLIGHT;
+    sl->launched_us = now_us();
     b->inflight++;
     b->st.launches++;
     b->st.chunks += sl->n;
@@ -499,9 +569,29 @@ static void *progress_main(void *arg)
             continue;
         }
         if (b->inflight == 0) {
-            pthread_cond_wait(&b->work_cv, &b->mu);
+            struct slot *o = b->open >= 0 ? &b->s[b->open] : NULL;
+            if (o && o->state == SLOT_OPEN && o->n > 0 && !o->writers) {
+                const uint64_t waited = now_us() - o->opened_us, l = linger_us(b);
+                if (waited >= l) slot_try_launch(b, o);    /* lingered long enough */
+                else wait_work_us(b, l - waited);
+            } else {
+                pthread_cond_wait(&b->work_cv, &b->mu);
+            }
             idle_us = 20;
         } else {
+            /* the device is busy: get the open slot's descriptors over and its
+             * plan made now, once no chunk arrived since the last poll, so
+             * its launch is only the kernel when the running one retires */
+            if (b->open >= 0) {
+                struct slot *o = &b->s[b->open];
+                if (o->state == SLOT_OPEN && o->mode != MODE_FIXED && o->n > o->planned_n) {
+                    if (o->n == o->seen_n) {
+                        const int e = slot_prepare(b, o);
+                        if (e && !o->err) o->err = e;
+                    }
+                    o->seen_n = o->n;
+                }
+            }
             struct timespec ts;
             clock_gettime(CLOCK_REALTIME, &ts);
             ts.tv_nsec += (long)idle_us * 1000;
@@ -591,6 +681,7 @@ static int batcher_new(int device, uint64_t slice_bytes, uint32_t nslots, uint64
     b->segcap = slice_bytes / 1024 < 4096 ? 4096 : slice_bytes / 1024;
     b->gather = MD5HIP_GATHER_AUTO;
     b->target = nslots > 2 ? 2 : 1;
+    b->linger_max_us = 5000;
     b->open = -1;
     b->tk_lo = b->tk_hi = 1;              /* ticket 0 = "nothing": complete at once */
     b->s = calloc(nslots, sizeof *b->s);
@@ -713,6 +804,16 @@ int md5hip_batcher_set_inflight(md5hip_batcher *b, uint32_t target)
     pthread_mutex_lock(&b->mu);
     b->target = target;
     if (b->open >= 0) slot_try_launch(b, &b->s[b->open]);
+    pthread_mutex_unlock(&b->mu);
+    return 0;
+}
+
+int md5hip_batcher_set_linger(md5hip_batcher *b, uint32_t max_us)
+{
+    if (!b) return -EINVAL;
+    pthread_mutex_lock(&b->mu);
+    b->linger_max_us = max_us;
+    pthread_cond_broadcast(&b->work_cv);
     pthread_mutex_unlock(&b->mu);
     return 0;
 }
@@ -865,6 +966,7 @@ static long reserve(md5hip_batcher *b, struct slot *sl, const struct chunk_src *
     const int dev = b->device;
     uint64_t j = i;
     if (zc) pthread_rwlock_rdlock(&g_reg_lock);
+    if (sl->n == 0 && i < n) sl->opened_us = now_us();
     while (j < n && sl->n < b->maxn) {
         const uint64_t L = src_len(src, j);
         if (src->dptrs) {                                      /* device-resident: no bytes */

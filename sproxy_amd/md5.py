@@ -336,7 +336,7 @@ class Batcher:
                wait="md5_batch_wait", poll="md5_batch_poll", flush="md5_batch_flush",
                submit_device_async="md5_batch_submit_device_async",
                submit_device="md5_batch_submit_device", set_inflight="md5hip_batcher_set_inflight",
-               stats="md5hip_batcher_get_stats")
+               set_linger="md5hip_batcher_set_linger", stats="md5hip_batcher_get_stats")
 
     def __init__(self, device: int = 0, slice_bytes: int = 0, nslots: int = 0,
                  kind: int = 0, fastcrc: int = 0):
@@ -505,6 +505,11 @@ class Batcher:
     def set_inflight(self, target: int):
         """Launch the open slot at once while fewer than `target` slots run."""
         check(*self._call("set_inflight", target))
+
+    def set_linger(self, max_us: int):
+        """Idle pipeline: hold an async submission's slot up to
+        min(max_us, 1/8 of recent launch time) for more work (0 = never)."""
+        check(*self._call("set_linger", max_us))
 
     def stats(self) -> dict:
         st = MD5HipBatcherStats()

@@ -239,3 +239,27 @@ def test_zero_copy_adjacent_registrations(cuda):
     finally:
         m.unregister_host(lo)
         m.unregister_host(hi)
+
+
+def test_queue_linger_turns_a_burst_into_one_launch(cuda):
+    """With nothing in flight, asynchronous submissions arriving back to back
+    are held for up to 1/8 of the recent launches' wall time (capped by
+    md5hip_batcher_set_linger) and go out as ONE launch; with linger 0 the
+    first of them is launched at once.  Digests per ticket either way."""
+    dl, pl, Ll, wl = _arena_batch([64 << 20] * 2, 21, cuda)      # ~0.6 s of serial chains
+    rng = np.random.default_rng(23)
+    small = [_arena_batch([int(x) for x in rng.integers(0, 70000, 100)], 300 + k, cuda) for k in range(5)]
+    with m.Queue(device=0, nslots=4) as q:
+        q.set_linger(200000)
+        assert np.array_equal(q.submit_device(pl, Ll), wl)        # sets the launch-time average
+        n0 = q.stats()["launches"]
+        pend = [q.submit_device_async(p, L) for _, p, L, _ in small]
+        for pn, (_, _, _, want) in zip(pend, small):
+            assert np.array_equal(pn.wait(), want)
+        n1 = q.stats()["launches"]
+        assert n1 == n0 + 1, (n0, n1)
+        q.set_linger(0)
+        pend = [q.submit_device_async(p, L) for _, p, L, _ in small]
+        for pn, (_, _, _, want) in zip(pend, small):
+            assert np.array_equal(pn.wait(), want)
+        assert q.stats()["launches"] >= n1 + 2
