@@ -24,6 +24,7 @@ template __global__ void crc32_desc<true>(const uint8_t*, const uint64_t*, const
 #include <string.h>
 #include <map>
 #include <mutex>
+#include <thread>
 #include <vector>
 
 #include "../../include/md5hip.h"
@@ -355,16 +356,45 @@ int md5hip_plan_order(const uint32_t* lens, uint64_t n, uint32_t* order) {
     if (b > maxb) maxb = b;
   }
   if (maxb <= (1u << 20)) {
-    uint32_t* cnt = (uint32_t*)calloc((size_t)maxb + 2, sizeof(uint32_t));
+    // T contiguous index ranges, one histogram each; range t's chunks of key
+    // k go after every earlier range's chunks of key k: stable, and the
+    // batcher's large coalesced slots (~1 M chunks) plan on several cores.
+    const uint64_t per = 1u << 17;
+    const uint32_t T = n >= 2 * per ? (uint32_t)(n / per < 8 ? n / per : 8) : 1u;
+    const size_t nb = (size_t)maxb + 1;
+    uint32_t* cnt = (uint32_t*)calloc(nb * T, sizeof(uint32_t));
     if (!cnt) return -ENOMEM;
-    for (uint64_t i = 0; i < n; ++i) cnt[maxb - ((lens[i] >> 6) + 1)]++;
+    auto range = [&](uint32_t t, uint64_t& lo, uint64_t& hi) {
+      lo = n * t / T;
+      hi = n * (t + 1) / T;
+    };
+    auto hist = [&](uint32_t t) {
+      uint64_t lo, hi;
+      range(t, lo, hi);
+      uint32_t* c = cnt + nb * t;
+      for (uint64_t i = lo; i < hi; ++i) c[maxb - ((lens[i] >> 6) + 1)]++;
+    };
+    auto scatter = [&](uint32_t t) {
+      uint64_t lo, hi;
+      range(t, lo, hi);
+      uint32_t* c = cnt + nb * t;
+      for (uint64_t i = lo; i < hi; ++i) order[c[maxb - ((lens[i] >> 6) + 1)]++] = (uint32_t)i;
+    };
+    std::vector<std::thread> th;
+    for (uint32_t t = 1; t < T; ++t) th.emplace_back(hist, t);
+    hist(0);
+    for (auto& x : th) x.join();
+    th.clear();
     uint32_t run = 0;
-    for (uint32_t k = 0; k <= maxb; ++k) {
-      const uint32_t c = cnt[k];
-      cnt[k] = run;
-      run += c;
-    }
-    for (uint64_t i = 0; i < n; ++i) order[cnt[maxb - ((lens[i] >> 6) + 1)]++] = (uint32_t)i;
+    for (size_t k = 0; k < nb; ++k)
+      for (uint32_t t = 0; t < T; ++t) {
+        const uint32_t c = cnt[nb * t + k];
+        cnt[nb * t + k] = run;
+        run += c;
+      }
+    for (uint32_t t = 1; t < T; ++t) th.emplace_back(scatter, t);
+    scatter(0);
+    for (auto& x : th) x.join();
     free(cnt);
     return 0;
   }
