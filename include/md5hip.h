@@ -284,10 +284,13 @@ int md5_batch_submit_device_async(md5hip_batcher *b, const uint64_t *d_ptrs, con
                                   uint64_t *ticket);
 int md5_batch_submit_device(md5hip_batcher *b, const uint64_t *d_ptrs, const uint32_t *lens,
                             uint64_t n, unsigned char *digests, int digests_on_device);
-/* Block until submission `ticket` has delivered its digests: 0 or -errno. */
+/* Block until submission `ticket` has delivered its digests: 0 or -errno.
+ * A ticket still coalescing in the open slot is launched at once when
+ * nothing is in flight (no linger); otherwise its slot goes out as soon as a
+ * running launch retires (it is never forced out beside one). */
 int md5_batch_wait(md5hip_batcher *b, uint64_t ticket);
 /* Non-blocking: 1 = `ticket` delivered, 0 = still running (its slot is
- * launched if it was waiting to coalesce), <0 = error. */
+ * hastened as by md5_batch_wait), <0 = error. */
 int md5_batch_poll(md5hip_batcher *b, uint64_t ticket);
 /* Launch the open slot now, whatever the in-flight count. */
 int md5_batch_flush(md5hip_batcher *b);

@@ -1105,7 +1105,7 @@ static int submit(md5hip_batcher *b, const struct chunk_src *src, uint64_t n, un
         while (!tk_done(b, t, &err)) {
             for (uint32_t k = 0; k < b->nslots; k++)
                 if (b->s[k].state == SLOT_OPEN && seg_has(&b->s[k], t)) {
-                    b->s[k].flush = 1;
+                    b->s[k].flush = 1;       /* a synchronous caller: at once */
                     slot_try_launch(b, &b->s[k]);
                 }
             pthread_cond_wait(&b->done_cv, &b->mu);
@@ -1115,6 +1115,21 @@ static int submit(md5hip_batcher *b, const struct chunk_src *src, uint64_t n, un
     pthread_mutex_unlock(&b->mu);
     dev_leave(&g);
     return rc;
+}
+
+/* A waiter or poller on `ticket` (mu held): if its chunks sit in the open
+ * slot and nothing is in flight, launch that slot now (no linger).  While
+ * launches are in flight the slot keeps coalescing and goes out as soon as
+ * one retires (the inflight target holds; its plan is made meanwhile) --
+ * forcing it out beside a running launch only splits the device between
+ * them. */
+static void hasten(md5hip_batcher *b, uint64_t ticket)
+{
+    for (uint32_t k = 0; k < b->nslots; k++)
+        if (b->s[k].state == SLOT_OPEN && seg_has(&b->s[k], ticket)) {
+            if (b->inflight == 0) b->s[k].flush = 1;
+            slot_try_launch(b, &b->s[k]);
+        }
 }
 
 int md5_batch_wait(md5hip_batcher *b, uint64_t ticket)
@@ -1127,11 +1142,7 @@ int md5_batch_wait(md5hip_batcher *b, uint64_t ticket)
         rc = -EINVAL;
     } else {
         while (!tk_done(b, ticket, &err)) {
-            for (uint32_t k = 0; k < b->nslots; k++)
-                if (b->s[k].state == SLOT_OPEN && seg_has(&b->s[k], ticket)) {
-                    b->s[k].flush = 1;
-                    slot_try_launch(b, &b->s[k]);
-                }
+            hasten(b, ticket);
             pthread_cond_wait(&b->done_cv, &b->mu);
         }
         rc = err;
@@ -1151,12 +1162,7 @@ int md5_batch_poll(md5hip_batcher *b, uint64_t ticket)
     } else if (tk_done(b, ticket, &err)) {
         rc = err ? err : 1;
     } else {
-        /* it must make progress without the caller blocking: launch its open slot */
-        for (uint32_t k = 0; k < b->nslots; k++)
-            if (b->s[k].state == SLOT_OPEN && seg_has(&b->s[k], ticket)) {
-                b->s[k].flush = 1;
-                slot_try_launch(b, &b->s[k]);
-            }
+        hasten(b, ticket);                   /* progress without the caller blocking */
         rc = 0;
     }
     pthread_mutex_unlock(&b->mu);
