@@ -505,7 +505,34 @@ def run_crc(a, rank, world, local, device, backend):
                         "traffic": traffic, "traffic_source": tnote, "kernel": "md5hip::" + kname,
                         "avg_launch_ms": round(dev_ms_max, 4), "alg_bytes_per_launch": int(alg_bytes),
                         "alg_bytes_note": f"{read} B read per block (+4 B CRC written)"}}
-    return per_rank_line(res, rank, world, local, device, backend, float(n) * L * a.steps, wall, None)
+    par = crc_sample(data, n, L, F, out, a.parity_sample, rank) if a.parity_sample else None
+    return per_rank_line(res, rank, world, local, device, backend, float(n) * L * a.steps, wall, par)
+
+
+def crc_sample(data, n, L, F, out, k, rank):
+    """Parity of the CRC line: the first, the last and seeded-random blocks
+    re-checksummed on the host after the timed region by the CRC-32
+    restatement (oracle/crc32_oracle.c, pinned to the reference crc32.c by
+    tests/test_oracle.py), blk_make_crc's fastcrc rule included."""
+    import numpy as np
+    lib = os.path.join(REPO, "oracle", "_build", "libmd5_oracle.so")
+    if not os.path.exists(lib):
+        return {"ok": None, "checker": "absent"}
+    O = ctypes.CDLL(lib)
+    O.oracle_crc32_batch.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                     ctypes.c_uint64, ctypes.c_uint32, ctypes.c_void_p]
+    idx = np.unique(np.concatenate([[0, n - 1], np.random.default_rng(77 + rank).integers(0, n, k)]))
+    rows = data.view(n, L)[torch.from_numpy(idx).to(data.device)].cpu().numpy()
+    offs = np.arange(idx.size, dtype=np.uint64) * np.uint64(L)
+    lens = np.full(idx.size, L, dtype=np.uint32)
+    want = np.empty(idx.size, dtype=np.uint32)
+    O.oracle_crc32_batch(rows.ctypes.data, offs.ctypes.data, lens.ctypes.data, idx.size, F,
+                         want.ctypes.data)
+    got = out.index_select(0, torch.from_numpy(idx).to(out.device)).cpu().numpy().view(np.uint32)
+    bad = int((got != want).sum())
+    return {"ok": bad == 0, "checked": int(idx.size), "mismatches": bad,
+            "checker": "CRC-32 restatement (oracle/crc32_oracle.c, pinned to crc32.c)",
+            "sample": "first + last + seeded-random blocks, re-checksummed on the host after the timed region"}
 
 
 def c3_lens(total_bytes, seed):
