@@ -223,3 +223,16 @@ def test_plan_desc_picks_balanced_for_coalesced_mixed_batches():
     big_uniform = np.full(1 << 20, 16384, np.uint32)
     big_uniform[::8] = 100
     assert m.plan_desc(big_uniform)[1] == "xdma"
+
+
+def test_plan_order_stable_across_thread_split():
+    """md5hip_plan_order: longest-first by 64-B block count, ties in index
+    order (a stable counting sort), also where it splits the index range over
+    several threads (>= 2^18 chunks) and for block counts past 2^20 (the
+    comparison-sort fallback)."""
+    for n, hi in ((0, 10), (1, 10), (1000, 1 << 21), (262143, 1 << 21), (262144, 1 << 21),
+                  (1 << 20, 1 << 22), (300001, 1 << 16), (5000, 1 << 31)):
+        x = np.random.default_rng(n + hi).integers(0, hi, n).astype(np.uint32)
+        got = m.plan_order(x)
+        want = np.argsort(-(x.astype(np.int64) >> 6), kind="stable")
+        assert np.array_equal(got, want), (n, hi)
