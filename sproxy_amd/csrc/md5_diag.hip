@@ -921,6 +921,33 @@ extern "C" int md5diag_crc_fast_lane(const void* d_base, uint64_t n, uint32_t le
   return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }
 
+// fastcrc F = 64 / 128 with D window groups in flight per wave
+namespace md5hip {
+template <int D, int T>
+__global__ void __launch_bounds__(T)
+diag_crc_fast_pipe(const uint8_t* __restrict__ base, uint64_t n, uint64_t stride, uint32_t flen,
+                   uint32_t F, uint32_t* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds[Crc32PermHasher::kLdsBytes];
+  fast_pipe_body<D>(base, nullptr, nullptr, n, stride, flen, F, out, lds);
+}
+}  // namespace md5hip
+
+extern "C" int md5diag_crc_fast_pipe(int depth, const void* d_base, uint64_t n, uint32_t len,
+                                     uint64_t stride, uint32_t fastcrc, uint32_t* d_out, void* stream) {
+  if (n == 0) return 0;
+  if (fastcrc != 64 && fastcrc != 128) return -EINVAL;
+  const dim3 g((uint32_t)(diag_cus() < (int)((2 * n + 63) / 64) ? diag_cus() : (2 * n + 63) / 64));
+  hipStream_t s = (hipStream_t)stream;
+  const uint8_t* p = (const uint8_t*)d_base;
+  // waves per CU so that the D buffers fit the register file: 16 / 12 / 8
+  if (depth == 2) hipLaunchKernelGGL((diag_crc_fast_pipe<2, 1024>), g, dim3(1024), 0, s, p, n, stride, len, fastcrc, d_out);
+  else if (depth == 3) hipLaunchKernelGGL((diag_crc_fast_pipe<3, 768>), g, dim3(768), 0, s, p, n, stride, len, fastcrc, d_out);
+  else if (depth == 4) hipLaunchKernelGGL((diag_crc_fast_pipe<4, 512>), g, dim3(512), 0, s, p, n, stride, len, fastcrc, d_out);
+  else if (depth == 13) hipLaunchKernelGGL((diag_crc_fast_pipe<2, 768>), g, dim3(768), 0, s, p, n, stride, len, fastcrc, d_out);
+  else return -EINVAL;
+  return hipGetLastError() == hipSuccess ? 0 : -EIO;
+}
+
 extern "C" int md5diag_variant_fixed(int v, const void* d_base, uint64_t n, uint32_t len,
                                      uint64_t stride, void* d_out, void* stream) {
   if (n == 0) return 0;

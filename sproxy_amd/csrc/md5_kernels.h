@@ -890,11 +890,13 @@ crc32_fast_xdma16(const uint8_t* __restrict__ base, const uint64_t* __restrict__
 // ragged tail window) is hashed lane-direct (lane_range) with nothing in
 // flight beside it.  Persistent: one 1024-thread workgroup per CU, groups
 // wave-major, grid-stride.
-__global__ void __launch_bounds__(1024)
-crc32_fast_pipe(const uint8_t* __restrict__ base, const uint64_t* __restrict__ offs,
-                const uint32_t* __restrict__ lens, uint64_t n, uint64_t stride, uint32_t flen,
-                uint32_t F, uint32_t* __restrict__ out) {
-  __shared__ __attribute__((aligned(16))) uint8_t lds[Crc32PermHasher::kLdsBytes];
+// D: window groups in flight per wave (D-1 loaded ahead of the one hashed).
+template <int D>
+__device__ __forceinline__ void fast_pipe_body(const uint8_t* __restrict__ base,
+                                               const uint64_t* __restrict__ offs,
+                                               const uint32_t* __restrict__ lens, uint64_t n,
+                                               uint64_t stride, uint32_t flen, uint32_t F,
+                                               uint32_t* __restrict__ out, uint8_t* lds) {
   Crc32PermHasher h;
   h.setup(lds);
   const FastWindows src{offs, lens, stride, flen, F};
@@ -935,29 +937,45 @@ crc32_fast_pipe(const uint8_t* __restrict__ base, const uint64_t* __restrict__ o
     }
     if (w.live) emit<FastWindows>(h, out, gi * 64u + lane, st);
   };
-  uint64_t gi = (uint64_t)wave * gridDim.x + blockIdx.x;
-  if (gi >= ngroups) return;
-  uint4 A[2][4], B[2][4];
-  Win a = locate(gi);
-  if (a.pipe) fetch(a, A);
-  for (;;) {                                             // two groups per trip: A, then B
-    const uint64_t g1 = gi + step;
-    Win b{};
-    if (g1 < ngroups) {
-      b = locate(g1);
-      if (b.pipe) fetch(b, B);
+  uint64_t g0 = (uint64_t)wave * gridDim.x + blockIdx.x;
+  if (g0 >= ngroups) return;
+  // a ring of D window buffers, indices fixed at compile time (unrolled)
+  uint4 buf[D][2][4];
+  Win win[D];
+#pragma unroll
+  for (int j = 0; j < D - 1; ++j) {
+    const uint64_t g = g0 + (uint64_t)j * step;
+    win[j] = Win{};
+    if (g < ngroups) {
+      win[j] = locate(g);
+      if (win[j].pipe) fetch(win[j], buf[j]);
     }
-    hash(a, gi, A);
-    if (g1 >= ngroups) break;
-    const uint64_t g2 = g1 + step;
-    if (g2 < ngroups) {
-      a = locate(g2);
-      if (a.pipe) fetch(a, A);
-    }
-    hash(b, g1, B);
-    if (g2 >= ngroups) break;
-    gi = g2;
   }
+  for (;;) {
+#pragma unroll
+    for (int j = 0; j < D; ++j) {
+      constexpr int kD = D;
+      const int pj = (j + kD - 1) % kD;                 // the slot freed one group ago
+      const uint64_t gp = g0 + (uint64_t)(j + kD - 1) * step;
+      win[pj] = Win{};
+      if (gp < ngroups) {
+        win[pj] = locate(gp);
+        if (win[pj].pipe) fetch(win[pj], buf[pj]);
+      }
+      const uint64_t g = g0 + (uint64_t)j * step;
+      if (g < ngroups) hash(win[j], g, buf[j]);
+    }
+    g0 += (uint64_t)D * step;
+    if (g0 >= ngroups) break;
+  }
+}
+
+__global__ void __launch_bounds__(1024)
+crc32_fast_pipe(const uint8_t* __restrict__ base, const uint64_t* __restrict__ offs,
+                const uint32_t* __restrict__ lens, uint64_t n, uint64_t stride, uint32_t flen,
+                uint32_t F, uint32_t* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds[Crc32PermHasher::kLdsBytes];
+  fast_pipe_body<2>(base, offs, lens, n, stride, flen, F, out, lds);
 }
 
 template <bool kImplicit>
