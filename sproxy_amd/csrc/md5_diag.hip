@@ -948,6 +948,85 @@ extern "C" int md5diag_crc_fast_pipe(int depth, const void* d_base, uint64_t n, 
   return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }
 
+// C2 energy per byte: fewer LDS round trips per byte --
+// W 128-B stages per DMA round (W x 8 KiB image per wave: one vmcnt wait,
+// one lgkmcnt wait and one DMA issue per W stages) -- against xdma1nt (W = 1).
+// kPad: W = 1 with the LDS of W = 2 (the occupancy control).
+namespace md5hip {
+template <int W, bool kPad = false>
+__global__ void __launch_bounds__(256)
+diag_fixed_xdma_wide(const uint8_t* __restrict__ base, uint64_t n, uint32_t len, uint64_t stride,
+                     uint4* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds[4 * (kPad ? 2 : W) * 8192];
+  Md5Hasher<false> h;
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint64_t wave_first = (uint64_t)blockIdx.x * blockDim.x + wave * 64u;
+  if (wave_first >= n) return;
+  uint8_t* img = lds + wave * (kPad ? 2 : W) * 8192u;
+  const uint64_t left = n - wave_first;
+  const uint32_t rows = left < 64 ? (uint32_t)left : 64u;
+  const __amdgpu_buffer_rsrc_t rsrc = uniform_rsrc(base + wave_first * stride);
+  uint32_t voff[8];
+#pragma unroll
+  for (int r = 0; r < 8; ++r) {
+    const uint32_t row = (uint32_t)r * 8u + (lane >> 3);
+    const uint32_t rc = row < rows ? row : rows - 1u;
+    const uint32_t part = (lane & 7u) ^ ((row >> 1) & 7u);
+    voff[r] = rc * (uint32_t)stride + part * 16u;
+  }
+  const uint32_t g = (lane >> 1) & 7u;
+  const uint32_t nfull = len >> 6;
+  const uint32_t nstage = nfull >> 1;
+  const uint32_t nws = (nstage + W - 1) / W;
+  typename Md5Hasher<false>::State st = h.init();
+  auto issue = [&](uint32_t ws) __attribute__((always_inline)) {
+#pragma unroll
+    for (int r = 0; r < 8; ++r)
+#pragma unroll
+      for (int j = 0; j < W; ++j) {
+        const uint32_t stg = ws * W + j;
+        if (W == 1 || stg < nstage)
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, img + j * 8192 + r * 1024, 16, voff[r],
+                                                   stg * 128u, 0, 2);
+      }
+  };
+  if (nstage) {
+    issue(0);
+    for (uint32_t ws = 0; ws < nws; ++ws) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      uint4 w[W][2][4];
+#pragma unroll
+      for (int j = 0; j < W; ++j)
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          const u32x4 v = *reinterpret_cast<const u32x4*>(img + j * 8192 + lane * 128 + ((q ^ g) * 16));
+          w[j][q >> 2][q & 3] = make_uint4(v.x, v.y, v.z, v.w);
+        }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if (ws + 1 < nws) issue(ws + 1);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int j = 0; j < W; ++j)
+        if (ws * W + j < nstage) {
+          h.block(st, w[j][0]);
+          h.block(st, w[j][1]);
+        }
+    }
+  }
+  const uint64_t i = wave_first + lane;
+  const uint64_t ci = lane < rows ? i : n - 1;
+  const uint8_t* chunk = base + ci * stride;
+  if (nfull & 1u) {
+    uint4 w[4];
+    load_block(w, reinterpret_cast<const uint4*>(chunk + ((uint64_t)(nfull - 1) << 6)));
+    h.block(st, w);
+  }
+  h.finish(st, chunk + ((uint64_t)nfull << 6), len & 63u, len);
+  if (lane < rows) h.store(out, i, st);
+}
+}  // namespace md5hip
+
 extern "C" int md5diag_variant_fixed(int v, const void* d_base, uint64_t n, uint32_t len,
                                      uint64_t stride, void* d_out, void* stream) {
   if (n == 0) return 0;
@@ -970,6 +1049,10 @@ extern "C" int md5diag_variant_fixed(int v, const void* d_base, uint64_t n, uint
     case 7: k = md5_fixed_xpose1nt; break;
     case 8: k = md5_fixed_xpose2nt; break;
     case 10: k = md5_fixed_xdma1nt; break;
+    case 70: k = diag_fixed_xdma_wide<2>; break;
+    case 71: k = diag_fixed_xdma_wide<1, true>; break;
+    case 72: k = diag_fixed_xdma_wide<4>; break;
+    case 73: k = diag_fixed_xdma_wide<1>; break;
     default: return -EINVAL;
   }
   hipLaunchKernelGGL(k, grid, blk, 0, s, b, n, len, stride, o);
