@@ -263,3 +263,72 @@ def test_queue_linger_turns_a_burst_into_one_launch(cuda):
         for pn, (_, _, _, want) in zip(pend, small):
             assert np.array_equal(pn.wait(), want)
         assert q.stats()["launches"] >= n1 + 2
+
+
+def test_queue_concurrency_stress(cuda):
+    """Eight threads on one queue for a few seconds: device-resident and host
+    submissions, synchronous and asynchronous, tickets waited / polled in
+    random order, while another thread keeps changing the inflight target
+    and the linger -- every ticket's digests equal the oracle and every
+    ticket completes (the coalescing, linger, plan-ahead and wait paths of
+    md5_submit.c under contention)."""
+    import time
+    rng0 = np.random.default_rng(99)
+    pool = []
+    for k in range(6):
+        lens = [int(x) for x in rng0.integers(0, 150000, int(rng0.integers(1, 120)))]
+        pool.append(_arena_batch(lens, 900 + k, cuda, align=int(rng0.choice([1, 16, 128]))))
+    hosts = []
+    for k in range(4):
+        lens = [int(x) for x in rng0.integers(0, 90000, int(rng0.integers(1, 60)))]
+        blob = gen.xorshift_bytes(sum(lens) + 1, seed=950 + k)
+        bufs, cur = [], 0
+        for x in lens:
+            bufs.append(blob[cur:cur + x])
+            cur += x
+        want = gen.oracle_digests(np.frombuffer(blob, dtype=np.uint8), np.cumsum([0] + lens[:-1]), lens)
+        hosts.append((bufs, want))
+    errs, done = [], []
+    stop = time.time() + 6.0
+    with m.Queue(device=0, nslots=4) as q:
+        def worker(seed):
+            rng = np.random.default_rng(seed)
+            try:
+                while time.time() < stop:
+                    held = []
+                    for _ in range(int(rng.integers(1, 6))):
+                        if rng.random() < 0.7:
+                            _, p, L, want = pool[int(rng.integers(0, len(pool)))]
+                            if rng.random() < 0.2:
+                                assert np.array_equal(q.submit_device(p, L), want)
+                                done.append(1)
+                            else:
+                                held.append((q.submit_device_async(p, L), want))
+                        else:
+                            bufs, want = hosts[int(rng.integers(0, len(hosts)))]
+                            held.append((q.submit_async(bufs), want))
+                    rng.shuffle(held)
+                    for pn, want in held:
+                        if rng.random() < 0.3:
+                            while not pn.poll():
+                                time.sleep(0.0002)
+                        assert np.array_equal(pn.wait(), want)
+                        done.append(1)
+            except Exception as e:  # pragma: no cover - surfaced below
+                errs.append(repr(e))
+
+        def knobs():
+            rng = np.random.default_rng(5)
+            while time.time() < stop:
+                q.set_inflight(int(rng.integers(1, 5)))
+                q.set_linger(int(rng.choice([0, 200, 5000])))
+                time.sleep(0.05)
+
+        th = [threading.Thread(target=worker, args=(s,)) for s in range(8)] + [threading.Thread(target=knobs)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join(timeout=120)
+        st = q.stats()
+    assert not errs, errs[:3]
+    assert len(done) > 50 and st["submissions"] >= len(done), (len(done), st)
