@@ -380,11 +380,22 @@ int md5hip_plan_order(const uint32_t* lens, uint64_t n, uint32_t* order) {
       uint32_t* c = cnt + nb * t;
       for (uint64_t i = lo; i < hi; ++i) order[c[maxb - ((lens[i] >> 6) + 1)]++] = (uint32_t)i;
     };
-    std::vector<std::thread> th;
-    for (uint32_t t = 1; t < T; ++t) th.emplace_back(hist, t);
-    hist(0);
-    for (auto& x : th) x.join();
-    th.clear();
+    // ranges 1..T-1 on helper threads; a range whose thread cannot be
+    // started runs here (no exception leaves this extern "C" entry)
+    auto fan_out = [&](auto&& fn) {
+      std::vector<std::thread> th;
+      std::vector<uint32_t> mine{0u};
+      for (uint32_t t = 1; t < T; ++t) {
+        try {
+          th.emplace_back(fn, t);
+        } catch (...) {
+          mine.push_back(t);
+        }
+      }
+      for (uint32_t t : mine) fn(t);
+      for (auto& x : th) x.join();
+    };
+    fan_out(hist);
     uint32_t run = 0;
     for (size_t k = 0; k < nb; ++k)
       for (uint32_t t = 0; t < T; ++t) {
@@ -392,9 +403,7 @@ int md5hip_plan_order(const uint32_t* lens, uint64_t n, uint32_t* order) {
         cnt[nb * t + k] = run;
         run += c;
       }
-    for (uint32_t t = 1; t < T; ++t) th.emplace_back(scatter, t);
-    scatter(0);
-    for (auto& x : th) x.join();
+    fan_out(scatter);
     free(cnt);
     return 0;
   }
