@@ -174,6 +174,21 @@ int md5hip_arena_free(void *d_ptr);
  */
 int md5hip_plan_desc(const uint32_t *lens, uint64_t n, uint32_t *order);
 
+/* Planning without sorting on the host, for producers that count lengths as
+ * chunks arrive (the batcher does): hist[k] = number of chunks whose key
+ * k = (len >> 6) + 1, for k in [1, kmax] (kmax <= MD5HIP_HIST_KMAX, chunks
+ * up to 8 MiB).  Returns md5hip_plan_desc's variant for such a batch and, if
+ * bucket_start is not NULL, fills bucket_start[kmax - k] with the first
+ * position of key k in the longest-first order (kmax + 1 entries).
+ * md5hip_order_device then builds that order on the device: with
+ * d_bucket_next holding bucket_start, d_order[d_bucket_next[kmax - k]++] = i
+ * for every chunk i of key k (positions within one key in no fixed order;
+ * the kernels do not care).  Asynchronous on `stream`; 0 or -errno. */
+#define MD5HIP_HIST_KMAX (1u << 17)
+int md5hip_plan_hist(const uint32_t *hist, uint32_t kmax, uint64_t n, uint32_t *bucket_start);
+int md5hip_order_device(const uint32_t *d_lens, uint64_t n, uint32_t kmax, uint32_t *d_bucket_next,
+                        uint32_t *d_order, void *stream);
+
 /*
  * Synthetic-data generator for benches/tests: fills nbytes (multiple of 16)
  * of device memory with word i = mix32(seed, i) (md5hip_kernels.hip).

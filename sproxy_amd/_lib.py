@@ -85,6 +85,8 @@ def lib():
         "md5hip_queue_create": (i, [i, u64, u32, ctypes.POINTER(vp)]),
         "md5hip_batcher_set_inflight": (i, [vp, u32]),
         "md5hip_batcher_set_linger": (i, [vp, u32]),
+        "md5hip_plan_hist": (i, [vp, u32, u64, vp]),
+        "md5hip_order_device": (i, [vp, u64, u32, vp, vp, vp]),
         "md5hip_batcher_get_stats": (i, [vp, ctypes.POINTER(MD5HipBatcherStats)]),
         "md5_batch_submit_device_async": (i, [vp, vp, vp, u64, vp, i, vp]),
         "md5_batch_submit_device": (i, [vp, vp, vp, u64, vp, i]),
@@ -154,7 +156,8 @@ EXPORTS = ["MD5Init", "MD5Update", "MD5Final", "nc_MD5Init", "nc_MD5Update", "nc
            "nc_crc32", "nc_header_crc", "nc_header_seal", "nc_header_verify",
            "md5hip_batch_verify_headers", "md5hip_host_register", "md5hip_host_unregister",
            "md5hip_batcher_set_gather", "md5hip_pool_set_gather", "md5hip_queue_create",
-           "md5hip_batcher_set_inflight", "md5hip_batcher_set_linger", "md5hip_batcher_get_stats", "md5_batch_submit_device_async",
+           "md5hip_batcher_set_inflight", "md5hip_batcher_set_linger", "md5hip_plan_hist", "md5hip_order_device",
+           "md5hip_batcher_get_stats", "md5_batch_submit_device_async",
            "md5_batch_submit_device", "md5_batch_flush", "md5hip_init_ctx", "md5hip_update_ctx",
            "md5hip_final_ctx"]
 

@@ -1175,6 +1175,35 @@ md5_init_ctx(uint32_t* __restrict__ ctxs, uint64_t n) {  // md5.c:153-163 (in[] 
 }
 
 // ---------------------------------------------------------------------------
+// The longest-first order of a descriptor batch on the device (the batcher's
+// planner, md5_submit.c): a counting sort whose bucket starts the host took
+// from the histogram it keeps while chunks are reserved.  One atomic per
+// distinct key per wave: the lanes of one key take consecutive positions.
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256)
+order_scatter(const uint32_t* __restrict__ lens, uint64_t n, uint32_t kmax,
+              uint32_t* __restrict__ next, uint32_t* __restrict__ order) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t lane = threadIdx.x & 63u;
+  const bool live = i < n;
+  const uint32_t key = live ? (lens[i] >> 6) + 1u : 0u;
+  uint64_t todo = __ballot(live);
+  while (todo) {                                       // wave-uniform
+    const uint32_t leader = (uint32_t)__builtin_ctzll(todo);
+    const uint32_t lk = (uint32_t)__shfl((int)key, (int)leader, 64);
+    const uint64_t same = __ballot(live && key == lk);
+    uint32_t base = 0;
+    if (lane == leader) base = atomicAdd(&next[kmax - lk], (uint32_t)__popcll(same));
+    base = (uint32_t)__shfl((int)base, (int)leader, 64);
+    if (live && key == lk) {
+      const uint32_t pos = base + (uint32_t)__popcll(same & ((1ull << lane) - 1ull));
+      if (pos < n) order[pos] = (uint32_t)i;           // bound: a torn bucket table stays in range
+    }
+    todo &= ~same;
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Device-side gather for the batcher's zero-copy path: segment k of a slice
 // is read from registered (pinned, device-mapped) host memory over PCIe and
 // written to its packed place in the slice's HBM buffer.  One workgroup per

@@ -93,6 +93,17 @@ bool dyn_lds_ready(const void* kern, uint32_t lds) {
   return ok;
 }
 
+// md5hip_plan_desc's decision from four order statistics of the batch: the
+// longest chunk's blocks, the median group's first key, the summed first
+// keys of all groups (work), and the blocks of the chunk two waves per CU deep.
+int plan_choice(uint32_t bmax, uint64_t median, uint64_t total, uint32_t probe_blocks) {
+  if (8u * median <= (uint64_t)bmax + 1) {
+    const uint64_t simds = 4ull * (uint64_t)cu_count();
+    if (10u * total >= 4u * simds * ((uint64_t)bmax + 1)) return MD5HIP_DESC_BALANCED;
+  }
+  return 4ull * probe_blocks <= bmax ? MD5HIP_DESC_HYBRID : MD5HIP_DESC_XDMA;
+}
+
 // One workgroup of `threads` per CU, grid-stride over 64-chunk groups.
 uint32_t per_cu_grid(uint64_t n) {
   const uint64_t need = (n + 63) / 64;
@@ -528,16 +539,52 @@ int md5hip_plan_desc(const uint32_t* lens, uint64_t n, uint32_t* order) {
   if (bmax < kHybridLongBlocks) return MD5HIP_DESC_XDMA;
   const uint64_t ngroups = (n + 63) / 64;
   const uint64_t median = (uint64_t)(lens[order[(ngroups / 2) * 64]] >> 6) + 1;
-  if (8u * median <= (uint64_t)bmax + 1) {
-    // work in block-steps: each group runs as long as its first (longest) lane
-    uint64_t total = 0;
-    for (uint64_t g = 0; g < ngroups; ++g) total += (uint64_t)(lens[order[g * 64]] >> 6) + 1;
-    const uint64_t simds = 4ull * (uint64_t)cu_count();
-    if (10u * total >= 4u * simds * ((uint64_t)bmax + 1)) return MD5HIP_DESC_BALANCED;
-  }
+  uint64_t total = 0;           // work in block-steps: a group runs as long as its first lane
+  for (uint64_t g = 0; g < ngroups; ++g) total += (uint64_t)(lens[order[g * 64]] >> 6) + 1;
   const uint64_t depth = (uint64_t)cu_count() * 128u;
   const uint64_t p = depth < n - 1 ? depth : n - 1;
-  return 4ull * (lens[order[p]] >> 6) <= bmax ? MD5HIP_DESC_HYBRID : MD5HIP_DESC_XDMA;
+  return plan_choice(bmax, median, total, lens[order[p]] >> 6);
+}
+
+int md5hip_plan_hist(const uint32_t* hist, uint32_t kmax, uint64_t n, uint32_t* bucket_start) {
+  if (!hist || kmax > MD5HIP_HIST_KMAX) return -EINVAL;
+  // walk the keys longest-first; rank r of the sorted order holds key k for
+  // r in [start(k), start(k) + hist[k])
+  const uint64_t ngroups = (n + 63) / 64;
+  const uint64_t rmed = (ngroups / 2) * 64;
+  const uint64_t depth = (uint64_t)cu_count() * 128u;
+  const uint64_t rprobe = n ? (depth < n - 1 ? depth : n - 1) : 0;
+  uint64_t r = 0, total = 0, median = 0, probe = 0;
+  uint32_t top = 0;
+  for (uint32_t k = kmax; k >= 1; --k) {
+    const uint64_t c = hist[k];
+    if (bucket_start) bucket_start[kmax - k] = (uint32_t)r;
+    if (!c) continue;
+    if (!top) top = k;
+    // group firsts 64 g in [r, r + c)
+    const uint64_t g0 = (r + 63) / 64, g1 = (r + c - 1) / 64;
+    if (g1 >= g0) total += (g1 - g0 + 1) * (uint64_t)k;
+    if (rmed >= r && rmed < r + c) median = k;
+    if (rprobe >= r && rprobe < r + c) probe = k;
+    r += c;
+  }
+  if (bucket_start) bucket_start[kmax] = (uint32_t)r;   // key 0 (never used): the end
+  if (n == 0 || !top) return MD5HIP_DESC_XDMA;
+  const uint32_t bmax = top - 1;
+  if (bmax < kHybridLongBlocks) return MD5HIP_DESC_XDMA;
+  return plan_choice(bmax, median, total, (uint32_t)(probe - 1));
+}
+
+int md5hip_order_device(const uint32_t* d_lens, uint64_t n, uint32_t kmax, uint32_t* d_next,
+                        uint32_t* d_order, void* stream) {
+  if (n == 0) return 0;
+  if (!d_lens || !d_next || !d_order || kmax > MD5HIP_HIST_KMAX) return -EINVAL;
+  if (int e = device_ok()) return e;
+  const uint64_t g = (n + 255) / 256;
+  if (g > 0x7fffffffull) return -EINVAL;
+  hipLaunchKernelGGL(order_scatter, dim3((uint32_t)g), dim3(256), 0, (hipStream_t)stream, d_lens, n,
+                     kmax, d_next, d_order);
+  return launched();
 }
 
 }  // extern "C"

@@ -199,6 +199,11 @@ struct slot {
      * prepared ahead while another slot's launch runs (slot_prepare) */
     uint64_t copied_n, planned_n, seen_n;
     int plan_var;
+    /* key histogram of the reserved chunks (k = (len >> 6) + 1, md5hip.h
+     * md5hip_plan_hist): the plan is made from counts and the order built on
+     * the device; hovf = a chunk past MD5HIP_HIST_KMAX (host sort instead) */
+    uint32_t *hh, hkmax, *h_bkt, *d_bkt;
+    int hovf;
     uint64_t opened_us, launched_us;  /* first chunk reserved / went in flight */
 };
 
@@ -359,9 +364,21 @@ static int slot_prepare(md5hip_batcher *b, struct slot *sl)
             return -EIO;
         sl->copied_n = n;
     }
-    const int dvar = md5hip_plan_desc(sl->h_len, n, sl->h_ord);
-    if (dvar < 0) return dvar;
-    if (hipMemcpyAsync(sl->d_ord, sl->h_ord, 4 * n, hipMemcpyHostToDevice, sl->stream)) return -EIO;
+    int dvar;
+    if (!sl->hovf) {
+        /* from the histogram: O(keys) on the host, the order on the device */
+        dvar = md5hip_plan_hist(sl->hh, sl->hkmax, n, sl->h_bkt);
+        if (dvar < 0) return dvar;
+        if (hipMemcpyAsync(sl->d_bkt, sl->h_bkt, 4 * ((size_t)sl->hkmax + 1), hipMemcpyHostToDevice,
+                           sl->stream))
+            return -EIO;
+        const int e = md5hip_order_device(sl->d_len, n, sl->hkmax, sl->d_bkt, sl->d_ord, sl->stream);
+        if (e) return e;
+    } else {
+        dvar = md5hip_plan_desc(sl->h_len, n, sl->h_ord);
+        if (dvar < 0) return dvar;
+        if (hipMemcpyAsync(sl->d_ord, sl->h_ord, 4 * n, hipMemcpyHostToDevice, sl->stream)) return -EIO;
+    }
     sl->plan_var = dvar;
     sl->planned_n = n;
     return 0;
@@ -446,6 +463,9 @@ static void slot_reset(struct slot *sl)
     sl->nsegs = 0;
     sl->tickets_in = 0;
     sl->copied_n = sl->planned_n = sl->seen_n = 0;
+    if (sl->hh) memset(sl->hh, 0, sizeof(uint32_t) * ((size_t)sl->hkmax + 1));
+    sl->hkmax = 0;
+    sl->hovf = 0;
 }
 
 /* Deliver a finished (or failed) slot to its tickets and free it (mu held). */
@@ -622,6 +642,8 @@ static void batcher_free(md5hip_batcher *b)
         hipHostFree(sl->h_dsc); hipFree(sl->d_dsc);
         free(sl->b_dst); free(sl->b_src); free(sl->b_len); free(sl->b_reg);
         free(sl->segs);
+        free(sl->hh);
+        hipHostFree(sl->h_bkt); hipFree(sl->d_bkt);
     }
     free(b->s);
     free(b->tk_pending);
@@ -708,7 +730,11 @@ static int batcher_new(int device, uint64_t slice_bytes, uint32_t nslots, uint64
         sl->b_src = malloc(sizeof(void *) * b->segcap);
         sl->b_len = malloc(sizeof(size_t) * b->segcap);
         sl->b_reg = malloc(sizeof(long) * b->segcap);
-        if (!sl->b_dst || !sl->b_src || !sl->b_len || !sl->b_reg) { rc = -ENOMEM; goto fail; }
+        sl->hh = calloc((size_t)MD5HIP_HIST_KMAX + 2, sizeof(uint32_t));
+        CK(hipHostMalloc((void **)&sl->h_bkt, sizeof(uint32_t) * ((size_t)MD5HIP_HIST_KMAX + 2),
+                         hipHostMallocDefault));
+        CK(hipMalloc((void **)&sl->d_bkt, sizeof(uint32_t) * ((size_t)MD5HIP_HIST_KMAX + 2)));
+        if (!sl->b_dst || !sl->b_src || !sl->b_len || !sl->b_reg || !sl->hh) { rc = -ENOMEM; goto fail; }
     }
     if (pthread_create(&b->progress, NULL, progress_main, b) != 0) { rc = -EAGAIN; goto fail; }
     b->progress_started = 1;
@@ -1023,6 +1049,15 @@ static long reserve(md5hip_batcher *b, struct slot *sl, const struct chunk_src *
             sl->used += sz;
         }
         sl->h_len[sl->n] = (uint32_t)L;
+        {
+            const uint64_t k = (L >> 6) + 1;
+            if (k > MD5HIP_HIST_KMAX) {
+                sl->hovf = 1;
+            } else {
+                sl->hh[k]++;
+                if (k > sl->hkmax) sl->hkmax = (uint32_t)k;
+            }
+        }
         sl->n++;
         j++;
     }

@@ -236,3 +236,34 @@ def test_plan_order_stable_across_thread_split():
         got = m.plan_order(x)
         want = np.argsort(-(x.astype(np.int64) >> 6), kind="stable")
         assert np.array_equal(got, want), (n, hi)
+
+
+def test_plan_hist_matches_plan_desc():
+    """md5hip_plan_hist (planning from a histogram of keys, as the batcher
+    keeps while chunks arrive) makes md5hip_plan_desc's choice on the same
+    batch, and its bucket starts are where each key begins in the
+    longest-first order."""
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    L = _lib.lib()
+    names = {v: k for k, v in m.DESC_VARIANTS.items()}
+    rng = np.random.default_rng(8)
+    cases = [bench.c3_lens(16 << 30, 1000),
+             np.concatenate([bench.c3_lens(16 << 30, 3000 + 31 * j) for j in range(3)]),
+             np.full(1 << 16, 16384), rng.integers(0, 1 << 20, 5000), rng.integers(0, 4096, 100),
+             np.array([1 << 20] * 10 + [4096] * 100000)]
+    for lens in cases:
+        lens = lens.astype(np.uint32)
+        keys = (lens >> 6) + 1
+        kmax = int(keys.max())
+        hist = np.bincount(keys, minlength=kmax + 1).astype(np.uint32)
+        start = np.zeros(kmax + 1, np.uint32)
+        v = L.md5hip_plan_hist(hist.ctypes.data, kmax, lens.size, start.ctypes.data)
+        order, want = m.plan_desc(lens)
+        assert names[v] == want, (names[v], want)
+        sk = keys[order]                                   # keys in longest-first order
+        for k in np.unique(keys):
+            assert start[kmax - k] == np.argmax(sk == k), k
+        assert start[kmax] == lens.size
+    assert L.md5hip_plan_hist(None, 1, 1, None) == -errno.EINVAL
