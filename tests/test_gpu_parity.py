@@ -628,3 +628,40 @@ def test_zero_copy_gather_modes(cuda):
         m.unregister_host(heap)
     with pytest.raises(m.MD5HipError):
         m.unregister_host(heap)
+
+
+@pytest.mark.gpu
+def test_order_device_is_a_longest_first_permutation(cuda):
+    """md5hip_plan_hist + md5hip_order_device (the batcher's planner): the
+    device-built order is a permutation, keys non-increasing along it, bucket
+    by bucket where md5hip_plan_hist put them; a descriptor launch with it
+    gives the oracle digests."""
+    import ctypes
+    import torch
+    from sproxy_amd import _lib
+    L = _lib.lib()
+    rng = np.random.default_rng(2024)
+    for n in (1, 63, 64, 1000, 200003):
+        lens = rng.integers(0, 300000, n).astype(np.uint32)
+        lens[rng.integers(0, n, max(1, n // 10))] = 16384          # a popular key
+        keys = (lens >> 6) + 1
+        kmax = int(keys.max())
+        hist = np.bincount(keys, minlength=kmax + 1).astype(np.uint32)
+        start = np.zeros(kmax + 1, np.uint32)
+        v = L.md5hip_plan_hist(hist.ctypes.data, kmax, n, start.ctypes.data)
+        assert v >= 0
+        d_len = torch.from_numpy(lens.view(np.int32)).to(cuda)
+        d_next = torch.from_numpy(start.view(np.int32)).to(cuda)
+        d_ord = torch.full((n,), -1, dtype=torch.int32, device=cuda)
+        s = torch.cuda.current_stream().cuda_stream
+        assert L.md5hip_order_device(d_len.data_ptr(), n, kmax, d_next.data_ptr(), d_ord.data_ptr(), s) == 0
+        order = d_ord.cpu().numpy().view(np.uint32)
+        assert np.array_equal(np.sort(order), np.arange(n, dtype=np.uint32)), n
+        assert np.all(np.diff(keys[order].astype(np.int64)) <= 0), n
+        if n <= 1000:
+            offs, total = gen.pack_offsets([int(x) for x in lens], align=16)
+            host = gen.xorshift_array(total + 64, seed=n)
+            dev = torch.from_numpy(host).to(cuda)
+            got = m.digest_desc(dev, torch.tensor(offs, dtype=torch.int64, device=cuda), d_len, d_ord,
+                                variant=v)
+            assert np.array_equal(got.cpu().numpy(), gen.oracle_digests(host, offs, [int(x) for x in lens]))
