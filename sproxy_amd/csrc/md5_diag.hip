@@ -291,6 +291,28 @@ diag_chain(uint32_t nblocks, uint4* __restrict__ out) {
   out[i] = make_uint4(st.a, st.b, st.c, st.d);
 }
 
+// The same chain with pre-summed addends (md5_core.h compress_fed): 4 VALU
+// per step, the 64 addends of a block read from LDS (16 ds_read_b128 per
+// block from one of four 16 KiB tables).  kind 80.
+__global__ void __launch_bounds__(64)
+diag_chain_fed(uint32_t nblocks, uint4* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) uint4 tab[4][16][64];
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t i = blockIdx.x * 64u + lane;
+  for (int b = 0; b < 4; ++b)
+    for (int t = 0; t < 16; ++t)
+      tab[b][t][lane] = make_uint4(i * 2654435761u + 4 * t + b, i * 40503u + t, i ^ (0x9E37u * t), i + 77u * t);
+  __syncthreads();
+  State st = initial_state();
+  for (uint32_t b = 0; b < nblocks; ++b) {
+    uint4 q[16];
+#pragma unroll
+    for (int t = 0; t < 16; ++t) q[t] = tab[b & 3][t][lane];
+    compress_fed(st, q);
+  }
+  out[i] = make_uint4(st.a, st.b, st.c, st.d);
+}
+
 // 64-B-stage candidates at 8 waves per SIMD (fixed_x64_body above).
 template <int CP, bool kDma>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8)))
@@ -720,6 +742,9 @@ extern "C" int md5diag_run(int kind, const void* base, uint64_t n, uint32_t len,
       if (kind == 33) hipLaunchKernelGGL((diag_chain<32, true>), g1, dim3(64), 0, s, nb, o);
       break;
     }
+    case 80:   // n = workgroups, len = bytes per chain: the fed chain
+      hipLaunchKernelGGL(diag_chain_fed, dim3((uint32_t)n), dim3(64), 0, s, len >> 6, o);
+      break;
     case 13: case 14: {
       // single-chain latency: n lanes (one wave per CU at n = 16384), each
       // hashing `len` bytes; 64-thread workgroups so every CU gets one wave
@@ -1063,6 +1088,18 @@ extern "C" int md5diag_variant_desc(int v, const void* d_base, const uint64_t* o
                                     const uint32_t* lens, const uint32_t* order, uint64_t n,
                                     void* d_out, void* stream) {
   if (n == 0) return 0;
+  if (v >= 4 && v <= 8) {   // HYBRID with fed chains (md5_kernels.h), one long group per CU:
+    // 4 / 5 = two addend tables, ring of 4 / 8 blocks; 6 = two tables, feeder
+    // off (barriers only; timing); 7 = one table, ring 4; 8 = one table, feeder off
+    const uint32_t nlong = (uint32_t)diag_cus();
+    auto k = v == 4 ? md5_desc_hybrid_fed<4, 2> : v == 5 ? md5_desc_hybrid_fed<8, 2>
+           : v == 6 ? md5_desc_hybrid_fed<4, 2, true> : v == 7 ? md5_desc_hybrid_fed<4, 1>
+           : md5_desc_hybrid_fed<4, 1, true>;
+    hipLaunchKernelGGL(k, dim3((uint32_t)hybrid_fed_grid(n, nlong)), dim3(128), 0,
+                       (hipStream_t)stream, (const uint8_t*)d_base, offs, lens, order, n,
+                       (uint4*)d_out, nlong);
+    return hipGetLastError() == hipSuccess ? 0 : -EIO;
+  }
   if (v != 2) return -EINVAL;
   hipLaunchKernelGGL(md5_desc_xpose, dim3((uint32_t)((n + 63) / 64)), dim3(64), 0, (hipStream_t)stream,
                      (const uint8_t*)d_base, offs, lens, order, n, (uint4*)d_out);

@@ -152,6 +152,42 @@ def test_desc_long_and_short_waves(cuda, dv):
         assert np.array_equal(got, want), order is None
 
 
+def test_hybrid_long_group_edges(cuda):
+    """HYBRID's long groups (longest chunk >= 256 KiB, one per CU, run
+    lane-direct): long chunks at every residue mod 64 and 128 beside lanes
+    with no whole block, a lone partial group, twenty full long groups, and a
+    group with one unaligned start."""
+    rng = np.random.default_rng(4242)
+    K = 4096 * 64                                       # 256 KiB: HYBRID's long threshold
+    cases = {
+        "residues": [K + r for r in (0, 1, 55, 56, 63, 64, 65, 127, 128, 129)] +
+                    [int(x) for x in rng.integers(K, 3 * K, 40)] + [0, 1, 63, 64, 100, 4096] +
+                    [int(x) for x in rng.integers(0, 64, 8)],
+        "lone_partial": [K + 77] * 3 + [5, 0],
+        "twenty_groups": [int(x) for x in rng.integers(K, K + 4000, 64 * 20)],
+    }
+    for name, lens in cases.items():
+        offs, total = gen.pack_offsets(lens, align=16)
+        buf = gen.xorshift_array(total + 64, seed=len(lens))
+        want = gen.oracle_digests(buf, offs, lens)
+        order = m.plan_order(lens).astype(np.int32)
+        got = m.digest_desc(_dev(buf, cuda), torch.tensor(offs, dtype=torch.int64, device=cuda),
+                            torch.tensor(lens, dtype=torch.int32, device=cuda), _dev(order, cuda),
+                            variant="hybrid").cpu().numpy()
+        assert np.array_equal(got, want), name
+    # one chunk start off 16 B inside the first (long) group
+    lens = [K + 5] * 20 + [300] * 30
+    offs, total = gen.pack_offsets(lens, align=16)
+    offs = list(offs)
+    offs[3] += 4
+    buf = gen.xorshift_array(total + 64, seed=77)
+    want = gen.oracle_digests(buf, offs, lens)
+    got = m.digest_desc(_dev(buf, cuda), torch.tensor(offs, dtype=torch.int64, device=cuda),
+                        torch.tensor(lens, dtype=torch.int32, device=cuda),
+                        _dev(m.plan_order(lens).astype(np.int32), cuda), variant="hybrid").cpu().numpy()
+    assert np.array_equal(got, want)
+
+
 @pytest.mark.parametrize("dv", DESC)
 def test_desc_offsets_beyond_4gib(cuda, dv):
     """Descriptor offsets past 2^32 (64-bit row pointers): chunks scattered
