@@ -1171,6 +1171,7 @@ diag_desc_x(const uint8_t* __restrict__ base, const uint64_t* __restrict__ offs,
   if constexpr (kVPad == 127) asm volatile("" ::: "v127");
   else if constexpr (kVPad == 167) asm volatile("" ::: "v167");
   else if constexpr (kVPad == 255) asm volatile("" ::: "v255");
+  else if constexpr (kVPad == 511) asm volatile("" ::: "v255", "a255");   // the whole file
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
   Md5Hasher<true> h;
   const uint64_t first = (uint64_t)blockIdx.x * 64u;
@@ -1222,6 +1223,12 @@ extern "C" int md5diag_desc_x(int kind, const void* base, const uint64_t* offs, 
   else if (kind == 10)
     hipLaunchKernelGGL((diag_desc_x<0, true, 2, 255>), g, b, 0, s, bs, offs, lens, order, n,
                        (uint4*)out, nlong, r);
+  else if (kind == 11)       // HYBRID at 2 / 1 waves per SIMD by registers (a chain's SIMD
+    hipLaunchKernelGGL((diag_desc_x<kHybridLongBlocks, true, 2, 255>), g, b, 0, s, bs, offs, lens,
+                       order, n, (uint4*)out, nlong, r);   // shared with one / no other wave)
+  else if (kind == 12)
+    hipLaunchKernelGGL((diag_desc_x<kHybridLongBlocks, true, 2, 511>), g, b, 0, s, bs, offs, lens,
+                       order, n, (uint4*)out, nlong, r);
   else if (kind >= 5 && kind <= 7) {   // XDMA at 16 / 12 / 8 waves per CU (dynamic LDS pad)
     const uint32_t waves = kind == 5 ? 16u : kind == 6 ? 12u : 8u;
     const uint32_t pad = (160u * 1024u) / waves - 8192u + 64u;
