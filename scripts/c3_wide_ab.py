@@ -30,8 +30,9 @@ NAMES = {0: "w4_nb1_s1", 1: "w4_nb2_s1", 5: "w4_nb1_s2", 6: "w4_nb1_s4", 7: "w4_
          12: "loads_w4_nb2_s1", 13: "loads_w8_nb1_s1", 14: "w4_nb1_s5", 15: "loads_w4_nb1_s5",
          16: "w4_nb1_s4_cached", 17: "loads_w4_nb1_s4_cached", 18: "w4_nb1_s2_cached", 19: "w4_nb1_s1_cached",
          20: "w4_nb2_s1_cached", 21: "w8_nb1_s1_cached", 22: "loads_w4_nb1_s1_cached",
-         23: "w8_split_s1_cached", 24: "product_shape_long_lane_256k", 25: "product_shape_long_lane_1m"}
-HASHING = (0, 1, 5, 6, 7, 14, 16, 18, 19, 20, 21, 23, 24, 25)
+         23: "w8_split_s1_cached", 24: "product_shape_long_lane_256k", 25: "product_shape_long_lane_1m",
+         26: "product_shape_3_images_regpipe"}
+HASHING = (0, 1, 5, 6, 7, 14, 16, 18, 19, 20, 21, 23, 24, 25, 26)
 PRODUCT = ("balanced", "hybrid", "xdma")
 
 

@@ -1299,7 +1299,8 @@ int diag_launch_balanced(const void* base, const uint64_t* offs, const uint32_t*
 // boundaries share a 128-B line): 16 = 4/1/4, 17 = 4/1/4 loads only,
 // 18 = 4/1/2, 19 = 4/1/1 (the product's shape), 20 = 4/2/1, 21 = 8/1/1, 22 = 4/1/1 loads only,
 // 23 = 8/1/1 split queues; 24 / 25 = the product's shape with groups whose
-// longest chunk is >= 256 KiB / 1 MiB run lane-direct (HYBRID's long path).
+// longest chunk is >= 256 KiB / 1 MiB run lane-direct (HYBRID's long path);
+// 26 = the product's shape with three images, stages register-pipelined.
 extern "C" int md5diag_desc_balanced(int kind, const void* base, const uint64_t* offs,
                                      const uint32_t* lens, const uint32_t* order, uint64_t n,
                                      void* out, void* rec, void* stream) {
@@ -1337,6 +1338,7 @@ extern "C" int md5diag_desc_balanced(int kind, const void* base, const uint64_t*
                                                                                      ctr, rec, s);
     case 25: return diag_launch_balanced<4, 1, false, 1, false, 2, 4 * kHybridLongBlocks>(base, offs, lens, order, n,
                                                                                          out, ctr, rec, s);
+    case 26: return diag_launch_balanced<4, 3, false, 1, false, 2>(base, offs, lens, order, n, out, ctr, rec, s);
     default: return -EINVAL;
   }
 }
