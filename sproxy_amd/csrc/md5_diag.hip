@@ -313,6 +313,33 @@ diag_chain_fed(uint32_t nblocks, uint4* __restrict__ out) {
   out[i] = make_uint4(st.a, st.b, st.c, st.d);
 }
 
+// Two independent chains per lane in one instruction stream (kind 81): does
+// a lone wave issue faster when it has a second chain to interleave?  Same
+// message words as diag_chain (xor with the block index), kLat step.
+__global__ void __launch_bounds__(64)
+diag_chain2(uint32_t nblocks, uint4* __restrict__ out) {
+  const uint32_t i = blockIdx.x * 64u + threadIdx.x;
+  uint4 w0[4], w1[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    w0[k] = make_uint4(i * 2654435761u + 4 * k, i * 40503u + 4 * k + 1, i ^ (0x9E37u * k), i + 77u * k);
+    w1[k] = make_uint4(i * 97u + 4 * k, i * 1013u + 3 * k + 1, i ^ (0x51EDu * k), i + 31u * k);
+  }
+  State s0 = initial_state(), s1 = initial_state();
+  s1.a ^= i;
+  for (uint32_t b = 0; b < nblocks; ++b) {
+    uint4 x[4], y[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      x[k] = make_uint4(w0[k].x ^ b, w0[k].y ^ b, w0[k].z ^ b, w0[k].w ^ b);
+      y[k] = make_uint4(w1[k].x ^ b, w1[k].y ^ b, w1[k].z ^ b, w1[k].w ^ b);
+    }
+    compress_regs<true>(s0, x);
+    compress_regs<true>(s1, y);
+  }
+  out[i] = make_uint4(s0.a ^ s1.a, s0.b ^ s1.b, s0.c ^ s1.c, s0.d ^ s1.d);
+}
+
 // 64-B-stage candidates at 8 waves per SIMD (fixed_x64_body above).
 template <int CP, bool kDma>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8)))
@@ -742,6 +769,9 @@ extern "C" int md5diag_run(int kind, const void* base, uint64_t n, uint32_t len,
       if (kind == 33) hipLaunchKernelGGL((diag_chain<32, true>), g1, dim3(64), 0, s, nb, o);
       break;
     }
+    case 81:   // n = workgroups, len = bytes per chain: two chains per lane, interleaved
+      hipLaunchKernelGGL(diag_chain2, dim3((uint32_t)n), dim3(64), 0, s, len >> 6, o);
+      break;
     case 80:   // n = workgroups, len = bytes per chain: the fed chain
       hipLaunchKernelGGL(diag_chain_fed, dim3((uint32_t)n), dim3(64), 0, s, len >> 6, o);
       break;

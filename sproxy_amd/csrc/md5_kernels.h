@@ -783,8 +783,9 @@ struct BalancedCfg {
 // 4-7 SHORT ones, each falling back to the other queue when its own is empty.
 // So every SIMD runs one serial chain at a time at s_setprio 3, and the short
 // groups fill the chain's issue gaps at a lower priority instead of slowing it
-// -- a lone MD5 chain issues only ~80 % of a SIMD's VALU rate (the dependent
-// latency), two long chains on one SIMD halve each other's speed.
+// (measured slower: a lone wave already issues VALU at the SIMD's full rate,
+// profiles/r02_chain_ilp_probe.json; two long chains on one SIMD halve each
+// other's speed).
 // ctr[0] long (all groups, unsplit), ctr[1] short, ctr[2] waves done.
 // Returns the number of groups this wave took (diagnostics).
 template <int WPB, int NB, bool kSplit, int W = 1, bool kHashOff = false, int CP = 2,
