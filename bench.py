@@ -353,7 +353,20 @@ def load_traffic(path, kernel, workload):
     h = m.kernel_code_hash(kernel)
     if ent.get("code_hash") != h:
         return None, f"stale: {kernel} code {h[:16]} != measured {str(ent.get('code_hash'))[:16]}"
-    return ent["bytes"], f"rocprofv3 PMC FETCH_SIZE/WRITE_SIZE, kernel code {h[:16]}; {ent.get('source', '')}"
+    note = f"rocprofv3 PMC FETCH_SIZE/WRITE_SIZE, kernel code {h[:16]}; {ent.get('source', '')}"
+    return ent["bytes"], note
+
+
+def load_valu_busy(path, kernel, workload):
+    """VALUBusy of `kernel` on `workload` (the secondary ceiling
+    beside HBM) from the same code-hash-checked PMC entry, or None."""
+    try:
+        ent = json.load(open(path)).get("entries", {}).get(f"{kernel}@{workload}")
+    except Exception:  # pragma: no cover
+        return None
+    if not ent or ent.get("code_hash") != m.kernel_code_hash(kernel):
+        return None
+    return ent.get("valu_busy")
 
 
 # --------------------------------------------------------------------------- configs
@@ -449,6 +462,7 @@ def run_c2(a, rank, world, local, device, backend):
     vname = m.variant_name(m.resolve_variant(variant))
     kname = "md5_fixed_" + vname
     traffic, tnote = load_traffic(a.traffic, kname, f"c2@{n}x{L}")
+    vbusy = load_valu_busy(a.traffic, kname, f"c2@{n}x{L}")
     res = {
         "metric": METRIC, "value": round(value, 2), "unit": "GiB/s", "n_gpus": world,
         "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(wall_max / a.steps * 1e3, 4),
@@ -460,7 +474,7 @@ def run_c2(a, rank, world, local, device, backend):
                    "parallelism": f"dp{world} (independent chunk shards, no collective)"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                     "traffic": traffic, "traffic_source": tnote,
+                     "traffic": traffic, "traffic_source": tnote, "valu_busy_pmc": vbusy,
                      "kernel": "md5hip::" + kname, "avg_launch_ms": round(dev_ms_max, 4),
                      "alg_bytes_per_launch": int(alg_bytes)},
     }
@@ -488,6 +502,7 @@ def run_crc(a, rank, world, local, device, backend):
     kname = m.crc_kernel_name(L, F)
     achieved = alg_bytes / (dev_ms_max * 1e-3) / 1e9
     traffic, tnote = load_traffic(a.traffic, kname, f"crc@{n}x{L}f{F}")
+    vbusy = load_valu_busy(a.traffic, kname, f"crc@{n}x{L}f{F}")
     res = {"metric": ("device-resident CRC-32 (netcache blk_make_crc) GiB/s on batched 16 KiB chunks"
                       if not fast else
                       f"device-resident fastcrc={F} CRC-32 (netcache blk_make_crc) blocks/s"),
@@ -502,7 +517,7 @@ def run_crc(a, rank, world, local, device, backend):
                       "block_payload_gib_s": round(float(n) * L * world * a.steps / wall_max / GIB, 2)},
            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                        "traffic": traffic, "traffic_source": tnote, "kernel": "md5hip::" + kname,
+                        "traffic": traffic, "traffic_source": tnote, "valu_busy_pmc": vbusy, "kernel": "md5hip::" + kname,
                         "avg_launch_ms": round(dev_ms_max, 4), "alg_bytes_per_launch": int(alg_bytes),
                         "alg_bytes_note": f"{read} B read per block (+4 B CRC written)"}}
     par = crc_sample(data, n, L, F, out, a.parity_sample, rank) if a.parity_sample else None
@@ -595,6 +610,7 @@ def c3_coalesced(a, lens, rank, world):
     pay = float(L_all.sum())
     kname = "md5_desc_" + ("balanced_t" if varK == "balanced" else varK)
     traffic, tnote = load_traffic(a.traffic, kname, f"c3k{K}@{a.c3_bytes}s{1000 + rank}")
+    vbusy = load_valu_busy(a.traffic, kname, f"c3k{K}@{a.c3_bytes}s{1000 + rank}")
     par = sample_desc(big, O_all, L_all, outK, c3_sample(L_all, ordK, a.parity_sample // 2, 191 + rank)) \
         if a.parity_sample else None
     alg = pay + 16 * L_all.size
@@ -604,7 +620,7 @@ def c3_coalesced(a, lens, rank, world):
             "roofline": {"bound": "hbm", "achieved": round(alg / (k_ms * 1e-3) / 1e9, 1),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(alg / (k_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-                         "traffic": traffic, "traffic_source": tnote, "kernel": "md5hip::" + kname,
+                         "traffic": traffic, "traffic_source": tnote, "valu_busy_pmc": vbusy, "kernel": "md5hip::" + kname,
                          "alg_bytes_per_launch": int(alg)},
             "parity": par,
             "note": "K C3 batches coalesced into one planned descriptor launch (distinct bytes)"}
@@ -702,6 +718,7 @@ def run_c3(a, rank, world, local, device, backend):
     del dig1
     kname = "md5_desc_" + dvar
     traffic, tnote = load_traffic(a.traffic, kname, f"c3@{a.c3_bytes}s{1000 + rank}")
+    vbusy = load_valu_busy(a.traffic, kname, f"c3@{a.c3_bytes}s{1000 + rank}")
     achieved = payload / (dev_ms * 1e-3) / 1e9
     res = {"metric": "device-resident MD5 GiB/s, mixed 4 KiB-1 MiB chunks (C3)",
            "value": round(value, 2), "unit": "GiB/s", "n_gpus": world, "steps": a.steps,
@@ -716,7 +733,7 @@ def run_c3(a, rank, world, local, device, backend):
            "roofline": {"bound": "hbm", "achieved": round(achieved, 1),
                         "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": round(achieved / HBM_PEAK_GBS, 4),
-                        "traffic": traffic, "traffic_source": tnote, "kernel": "md5hip::" + kname,
+                        "traffic": traffic, "traffic_source": tnote, "valu_busy_pmc": vbusy, "kernel": "md5hip::" + kname,
                         "avg_launch_ms": round(dev_ms, 4),
                         "alg_bytes_per_launch": int(payload + 16 * lens.size),
                         "chain_bound": {"longest_alone_ms": round(chain_ms, 4), "n_longest": int(il.size),
@@ -862,6 +879,7 @@ def run_ctx(a, rank, world, local, device, backend):
     alg = float(n) * (L + 2 * 88)
     achieved = alg / (dev_ms_max * 1e-3) / 1e9
     traffic, tnote = load_traffic(a.traffic, "md5_update_ctx", f"ctx@{n}x{L}")
+    vbusy = load_valu_busy(a.traffic, "md5_update_ctx", f"ctx@{n}x{L}")
     res = {"metric": "device-resident batched MD5Update GiB/s (md5hip_update_ctx, 16 KiB per context per call)",
            "value": round(float(n) * L * world * a.steps / wall_max / GIB, 2), "unit": "GiB/s",
            "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
@@ -872,7 +890,7 @@ def run_ctx(a, rank, world, local, device, backend):
                         "frac": round(achieved / HBM_PEAK_GBS, 4), "kernel": "md5hip::md5_update_ctx",
                         "avg_launch_ms": round(dev_ms_max, 4), "alg_bytes_per_launch": int(alg),
                         "alg_bytes_note": "block bytes + the 88-B context read and written",
-                        "traffic": traffic, "traffic_source": tnote}}
+                        "traffic": traffic, "traffic_source": tnote, "valu_busy_pmc": vbusy}}
     return per_rank_line(res, rank, world, local, device, backend, float(n) * L * a.steps, wall, par)
 
 

@@ -4,10 +4,13 @@ kernel@workload, with the SHA-256 of that kernel's machine code in the
 library that ran (sproxy_amd._lib.kernel_code_hash), so bench.py reports
 counter bytes only while the kernel's code is the code that was measured.
 
-usage: traffic_json.py FETCH_DIR WRITE_DIR WORKLOAD [--out profiles/traffic.json]
+usage: traffic_json.py FETCH_DIR WRITE_DIR WORKLOAD [--valu VALU_DIR] [--out profiles/traffic.json]
   FETCH_DIR / WRITE_DIR: `rocprofv3 --pmc FETCH_SIZE` / `--pmc WRITE_SIZE`
   output dirs (csv) of the same bench command; WORKLOAD: the bench line's
-  config tag the bytes belong to (e.g. c2@1048576x16384).
+  config tag the bytes belong to (e.g. c2@1048576x16384).  VALU_DIR: a pass
+  of SQ_ACTIVE_INST_VALU SQ_INSTS_VALU GRBM_GUI_ACTIVE (SURVEY §8(d) asks for
+  VALUBusy beside the HBM roofline): valu_busy = SQ_ACTIVE_INST_VALU quad-
+  cycles over (1024 SIMDs x GRBM_GUI_ACTIVE / 8 XCDs / 4), as pmc_summary.py.
 HBM bytes per launch (MI355X_MICROARCH.md HBM section, gfx950): read =
 2 x 1024 x FETCH_SIZE, write = 1024 x WRITE_SIZE, mean over the kernel's
 dispatches."""
@@ -48,14 +51,19 @@ def main():
     p.add_argument("workload")
     p.add_argument("--out", default=os.path.join(REPO, "profiles", "traffic.json"))
     p.add_argument("--source", default="")
+    p.add_argument("--valu", default=None)
     a = p.parse_args()
     from sproxy_amd._lib import kernel_code_hash
     fs, nf = per_kernel(a.fetch, "FETCH_SIZE")
     ws, _ = per_kernel(a.write, "WRITE_SIZE")
+    va, vi, gr = ({}, {}, {}) if not a.valu else (per_kernel(a.valu, "SQ_ACTIVE_INST_VALU")[0],
+                                                   per_kernel(a.valu, "SQ_INSTS_VALU")[0],
+                                                   per_kernel(a.valu, "GRBM_GUI_ACTIVE")[0])
     d = json.load(open(a.out)) if os.path.exists(a.out) else {}
     d["_note"] = ("HBM bytes per launch from rocprofv3 PMC (read = 2*1024*FETCH_SIZE, write = "
                   "1024*WRITE_SIZE; MI355X_MICROARCH.md HBM section), per kernel@workload, with "
-                  "the SHA-256 of the kernel's machine code that was measured")
+                  "the SHA-256 of the kernel's machine code that was measured; valu_busy = "
+                  "SQ_ACTIVE_INST_VALU / (1024 SIMDs x GRBM_GUI_ACTIVE/8 / 4) from a separate pass")
     ent = d.setdefault("entries", {})
     new = {}
     for k, v in fs.items():
@@ -65,6 +73,10 @@ def main():
             "bytes": int(2 * 1024 * v + 1024 * ws.get(k, 0.0)),
             "read_bytes": int(2 * 1024 * v), "write_bytes": int(1024 * ws.get(k, 0.0)),
             "dispatches": nf[k], "code_hash": kernel_code_hash(k), "source": a.source}
+        if k in va and gr.get(k):
+            new[f"{k}@{a.workload}"].update({
+                "valu_busy": round(va[k] / (1024 * gr[k] / 8 / 4), 4),
+                "valu_insts": int(vi.get(k, 0)), "gpu_cycles": int(gr[k] / 8)})
     ent.update(new)
     json.dump(d, open(a.out, "w"), indent=1, sort_keys=True)
     print(json.dumps(new, indent=1))
