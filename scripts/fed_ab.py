@@ -53,6 +53,7 @@ def main():
     D = ctypes.CDLL(DIAG)
     D.md5diag_run.argtypes = [ci, vp, u64, u32, u64, vp, vp]
     D.md5diag_variant_desc.argtypes = [ci, vp, vp, vp, vp, u64, vp, vp]
+    D.md5diag_fed_split.argtypes = [ci, vp, vp, vp, vp, u64, vp, vp]
     st = torch.cuda.current_stream().cuda_stream
     res = {}
 
@@ -71,6 +72,9 @@ def main():
     print(json.dumps({"chain_probe": probe}), flush=True)
 
     def fed(base, dO, dL, dR, n, dig, v=4):
+        if v >= 100:   # split launches: 100 = fed pairs + XDMA, 101 = HYBRID part + XDMA
+            return D.md5diag_fed_split(v - 100, base.data_ptr(), dO.data_ptr(), dL.data_ptr(),
+                                       dR.data_ptr(), n, dig.data_ptr(), st)
         return D.md5diag_variant_desc(v, base.data_ptr(), dO.data_ptr(), dL.data_ptr(), dR.data_ptr(), n,
                                       dig.data_ptr(), st)
 
@@ -89,7 +93,7 @@ def main():
     ref = m.digest_desc(buf, dO, dL, dR, variant="hybrid")
     dig = torch.empty((n, 16), dtype=torch.uint8, device="cuda")
     eqs = []
-    for v in (4, 5, 7):
+    for v in (4, 100, 101):
         assert fed(buf, dO, dL, dR, n, dig, v) == 0
         torch.cuda.synchronize()
         eqs.append(bool(torch.equal(dig, ref)))
@@ -107,14 +111,14 @@ def main():
         dig = torch.empty((n, 16), dtype=torch.uint8, device="cuda")
         ref = m.digest_desc(big, dO, dL, dR, variant="hybrid")
         eq = []
-        for v in (4, 5, 7):
+        for v in (4, 100, 101):
             assert fed(big, dO, dL, dR, n, dig, v) == 0
             torch.cuda.synchronize()
             eq.append(bool(torch.equal(dig, ref)))
         legs = {"hybrid": lambda: m.digest_desc(big, dO, dL, dR, out=dig, variant="hybrid"),
-                "fed_2tab_wg4": lambda: fed(big, dO, dL, dR, n, dig, 4),
-                "fed_2tab_wg2": lambda: fed(big, dO, dL, dR, n, dig, 5),
-                "fed_1tab_wg2": lambda: fed(big, dO, dL, dR, n, dig, 7)}
+                "fed_one_launch": lambda: fed(big, dO, dL, dR, n, dig, 4),
+                "fed_split": lambda: fed(big, dO, dL, dR, n, dig, 100),
+                "hybrid_split": lambda: fed(big, dO, dL, dR, n, dig, 101)}
         if K > 1:
             legs["balanced"] = lambda: m.digest_desc(big, dO, dL, dR, out=dig, variant="balanced")
         ms = {k: [] for k in legs}
@@ -130,9 +134,8 @@ def main():
             sR = torch.arange(sel.size, dtype=torch.int32, device="cuda")
             sd = torch.empty((sel.size, 16), dtype=torch.uint8, device="cuda")
             fl = {"hybrid": lambda: m.digest_desc(big, sO, sL, sR, out=sd, variant="hybrid"),
-                  "fed_2tab_wg4": lambda: fed(big, sO, sL, sR, sel.size, sd, 4),
-                  "fed_2tab_wg2": lambda: fed(big, sO, sL, sR, sel.size, sd, 5),
-                  "fed_2tab_wg4_feeder_off": lambda: fed(big, sO, sL, sR, sel.size, sd, 6)}
+                  "fed_one_launch": lambda: fed(big, sO, sL, sR, sel.size, sd, 4),
+                  "fed_split": lambda: fed(big, sO, sL, sR, sel.size, sd, 100)}
             fms = {k: [] for k in fl}
             for _ in range(a.rounds):
                 for k, f in fl.items():

@@ -1136,6 +1136,47 @@ extern "C" int md5diag_variant_desc(int v, const void* d_base, const uint64_t* o
   return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }
 
+// Fed chains as a split launch (kind 0) or the same split with plain HYBRID
+// lane-direct long waves in the first part (kind 1, control): groups
+// [0, L = min(CUs, groups)) as md5_desc_fed_pairs on a high-priority stream,
+// groups [L, ...) as md5_desc_xdma on `stream`, joined by events.  Needs an
+// order (the split is by position in it).
+extern "C" int md5diag_fed_split(int kind, const void* d_base, const uint64_t* offs,
+                                 const uint32_t* lens, const uint32_t* order, uint64_t n,
+                                 void* d_out, void* stream) {
+  if (n == 0) return 0;
+  if (!order) return -EINVAL;
+  static hipStream_t hs = nullptr;
+  static hipEvent_t e0 = nullptr, e1 = nullptr;
+  if (!hs) {
+    int lo = 0, hi = 0;
+    if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess ||
+        hipStreamCreateWithPriority(&hs, hipStreamNonBlocking, hi) != hipSuccess ||
+        hipEventCreateWithFlags(&e0, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&e1, hipEventDisableTiming) != hipSuccess)
+      return -ENODEV;
+  }
+  hipStream_t s = (hipStream_t)stream;
+  const uint64_t groups = (n + 63) / 64;
+  const uint64_t L = groups < (uint64_t)diag_cus() ? groups : (uint64_t)diag_cus();
+  const uint8_t* b = (const uint8_t*)d_base;
+  if (hipEventRecord(e0, s) != hipSuccess || hipStreamWaitEvent(hs, e0, 0) != hipSuccess) return -EIO;
+  const uint64_t nfirst = L * 64 < n ? L * 64 : n;
+  if (kind == 0)
+    hipLaunchKernelGGL((md5_desc_fed_pairs<4, 2>), dim3((uint32_t)L), dim3(128), 0, hs, b, offs, lens,
+                       order, nfirst, (uint4*)d_out);
+  else
+    hipLaunchKernelGGL(md5_desc_hybrid, dim3((uint32_t)L), dim3(64), 0, hs, b, offs, lens, order, nfirst,
+                       (uint4*)d_out, (uint32_t)L);
+  if (hipGetLastError() != hipSuccess) return -EIO;
+  if (n > nfirst)
+    hipLaunchKernelGGL(md5_desc_xdma, dim3((uint32_t)(groups - L)), dim3(64), 0, s, b, offs, lens,
+                       order + nfirst, n - nfirst, (uint4*)d_out);
+  if (hipGetLastError() != hipSuccess) return -EIO;
+  if (hipEventRecord(e1, hs) != hipSuccess || hipStreamWaitEvent(s, e1, 0) != hipSuccess) return -EIO;
+  return 0;
+}
+
 extern "C" int md5diag_variant_crc(int v, const void* d_base, uint64_t n, uint32_t len,
                                    uint64_t stride, uint32_t* d_out, void* stream) {
   if (n == 0) return 0;

@@ -766,6 +766,38 @@ md5_desc_hybrid_fed(const uint8_t* __restrict__ base, const uint64_t* __restrict
                                                                 lds + wave * 8192u);
 }
 
+// Only the first min(L, groups) groups of md5_desc_hybrid_fed (the pair
+// workgroups), for a split launch: the rest goes to md5_desc_xdma on the
+// caller's stream while this kernel runs on a high-priority stream, so the
+// XDMA waves get the ordinary one-wave workgroups and 8 KiB images and the
+// pairs their 32 KiB (md5diag_fed_split).
+template <int D = 4, int NT = 2>
+__global__ void __launch_bounds__(128)
+md5_desc_fed_pairs(const uint8_t* __restrict__ base, const uint64_t* __restrict__ offs,
+                   const uint32_t* __restrict__ lens, const uint32_t* __restrict__ order, uint64_t n,
+                   uint4* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds[NT * kFedTable];
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const DescArrays src{offs, lens, order};
+  Md5Hasher<true> h;
+  const uint64_t first = (uint64_t)blockIdx.x * 64u;
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint64_t i = first + lane;
+  const bool live = i < n;
+  const uint64_t c = src.index(live ? i : first);
+  const uint64_t off = src.off(c);
+  const uint32_t len = live ? src.len(c) : 0u;
+  const uint32_t nfull = len >> 6;
+  const uint32_t bmax = wave_max(nfull);
+  const bool unaligned = __ballot(live && ((((uintptr_t)base + off) & 15u) != 0)) != 0;
+  if (bmax >= kHybridLongBlocks && !unaligned) {
+    fed_long_group<D, NT>(base, out, lds, wave == 1, nfull, bmax, off, len, c, live);
+    return;
+  }
+  if (wave == 0)
+    desc_xpose_group<2, Md5Hasher<true>, 0, 1, false, true, true>(h, base, src, n, first, out, lds);
+}
+
 // grid of md5_desc_hybrid_fed
 __host__ __device__ inline uint64_t hybrid_fed_grid(uint64_t n, uint32_t nlong) {
   const uint64_t groups = (n + 63) / 64;
