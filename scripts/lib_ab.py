@@ -1,0 +1,126 @@
+#!/usr/bin/env python3
+"""In-process A/B of two builds of libmd5hip.so on the same device buffers:
+OLD (build/ab/libmd5hip_old.so, the library before a change) against NEW
+(sproxy_amd/lib/libmd5hip.so).  Both are loaded with ctypes side by side;
+every workload runs both, interleaved, and their outputs are compared.
+
+Workloads (the descriptor LDS-DMA loader's users):
+  ctx       md5hip_update_ctx on 1,048,576 contexts x 16 KiB (bench --config ctx)
+  ragged16  md5hip_digest_desc_variant XDMA, netcache blocks packed at 16 B
+  c3k3      BALANCED on 3 coalesced C3 batches (bench --config c3 coalesced leg)
+Prints one JSON object (ms per launch, hipEvent, interleaved rounds).
+usage: lib_ab.py [--rounds R]"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+sys.path.insert(0, os.path.join(REPO, "scripts"))
+from c3_trace_x import batch  # noqa: E402
+from sproxy_amd import md5 as m  # noqa: E402
+
+vp, u64, ci = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int
+
+
+def load(path):
+    L = ctypes.CDLL(path, mode=ctypes.RTLD_LOCAL)
+    L.md5hip_update_ctx.argtypes = [vp, vp, vp, u64, vp]
+    L.md5hip_init_ctx.argtypes = [vp, u64, vp]
+    L.md5hip_digest_desc_variant.argtypes = [vp, vp, vp, vp, u64, vp, vp, ci]
+    return L
+
+
+def timed(f):
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    rc = f()
+    e1.record()
+    torch.cuda.synchronize()
+    assert rc == 0, rc
+    return e0.elapsed_time(e1)
+
+
+def ab(libs, run, out, rounds):
+    """run(lib) -> rc; out() -> tensor to compare; returns ms lists and equality"""
+    res = {}
+    for name, L in libs.items():
+        assert run(L) == 0
+        torch.cuda.synchronize()
+        res[name] = out().clone()
+    eq = bool(torch.equal(res["old"], res["new"]))
+    ms = {k: [] for k in libs}
+    for _ in range(rounds):
+        for k, L in libs.items():
+            ms[k].append(round(timed(lambda: run(L)), 4))
+    return {"ms": ms, "equal": eq, "best_new_vs_old": round(min(ms["old"]) / min(ms["new"]), 4),
+            "median_new_vs_old": round(sorted(ms["old"])[rounds // 2] / sorted(ms["new"])[rounds // 2], 4)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rounds", type=int, default=9)
+    a = ap.parse_args()
+    libs = {"old": load(os.path.join(REPO, "build", "ab", "libmd5hip_old.so")),
+            "new": load(os.path.join(REPO, "sproxy_amd", "lib", "libmd5hip.so"))}
+    st = torch.cuda.current_stream().cuda_stream
+    res = {}
+
+    # ctx: 1 M contexts x 16 KiB (one update launch; contexts re-initialised per run)
+    n, L = 1 << 20, 16384
+    data = torch.empty(n * L, dtype=torch.uint8, device="cuda")
+    m.fill_synthetic(data, seed=0xC7)
+    ctx = torch.zeros((n, 88), dtype=torch.uint8, device="cuda")
+    ptrs = torch.arange(n, dtype=torch.int64, device="cuda") * L + data.data_ptr()
+    lens = torch.full((n,), L, dtype=torch.int32, device="cuda")
+
+    def run_ctx(Lb):
+        rc = Lb.md5hip_init_ctx(ctx.data_ptr(), n, st)
+        return rc or Lb.md5hip_update_ctx(ctx.data_ptr(), ptrs.data_ptr(), lens.data_ptr(), n, st)
+    res["ctx"] = ab(libs, run_ctx, lambda: ctx, a.rounds)
+    print(json.dumps({"ctx": res["ctx"]}), flush=True)
+    del data, ctx, ptrs, lens
+    torch.cuda.empty_cache()
+
+    # ragged netcache blocks packed at 16 B (descriptor XDMA)
+    rng = np.random.default_rng(5)
+    S, nb = 16384, 983040                       # ~15 GiB
+    bl = np.full(nb, S, dtype=np.int64)
+    tail = rng.integers(0, 8, nb) == 0
+    bl[tail] = rng.integers(1, S, int(tail.sum()))
+    offs = np.concatenate([[0], np.cumsum((bl + 15) // 16 * 16)[:-1]]).astype(np.int64)
+    arena = m.arena_empty(int(offs[-1] + bl[-1] + 64))
+    m.fill_synthetic(arena, seed=0x16)
+    order, _ = m.plan_desc(bl.astype(np.uint32))
+    dO = torch.from_numpy(offs).cuda()
+    dL = torch.from_numpy(bl.astype(np.int32)).cuda()
+    dR = torch.from_numpy(order.astype(np.int32)).cuda()
+    dig = torch.empty((nb, 16), dtype=torch.uint8, device="cuda")
+    run_r = lambda Lb: Lb.md5hip_digest_desc_variant(arena.data_ptr(), dO.data_ptr(), dL.data_ptr(),  # noqa
+                                                     dR.data_ptr(), nb, dig.data_ptr(), st, 4)
+    res["ragged16"] = ab(libs, run_r, lambda: dig, a.rounds)
+    print(json.dumps({"ragged16": res["ragged16"]}), flush=True)
+    del arena, dO, dL, dR, dig
+    torch.cuda.empty_cache()
+
+    # 3 coalesced C3 batches, BALANCED
+    big, Lk, O, order, var = batch(3, 1000)
+    nk = Lk.size
+    dO = torch.from_numpy(O).cuda()
+    dL = torch.from_numpy(Lk.astype(np.int32)).cuda()
+    dR = torch.from_numpy(order.astype(np.int32)).cuda()
+    dig = torch.empty((nk, 16), dtype=torch.uint8, device="cuda")
+    run_b = lambda Lb: Lb.md5hip_digest_desc_variant(big.data_ptr(), dO.data_ptr(), dL.data_ptr(),  # noqa
+                                                     dR.data_ptr(), nk, dig.data_ptr(), st, 5)
+    res["c3k3_balanced"] = ab(libs, run_b, lambda: dig, a.rounds)
+    print(json.dumps({"c3k3_balanced": res["c3k3_balanced"]}), flush=True)
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    sys.exit(main())
