@@ -9,7 +9,7 @@ Workloads (the descriptor LDS-DMA loader's users):
   ragged16  md5hip_digest_desc_variant XDMA, netcache blocks packed at 16 B
   c3k3      BALANCED on 3 coalesced C3 batches (bench --config c3 coalesced leg)
 Prints one JSON object (ms per launch, hipEvent, interleaved rounds).
-usage: lib_ab.py [--rounds R]"""
+usage: lib_ab.py [--rounds R] [--extra name=path ...]"""
 import argparse
 import ctypes
 import json
@@ -53,7 +53,11 @@ def ab(libs, run, out, rounds):
         assert run(L) == 0
         torch.cuda.synchronize()
         res[name] = out().clone()
-    eq = bool(torch.equal(res["old"], res["new"]))
+    eq = all(bool(torch.equal(res["old"], v)) for v in res.values())
+    for _ in range(3):                   # clocks settle
+        for L in libs.values():
+            run(L)
+    torch.cuda.synchronize()
     ms = {k: [] for k in libs}
     for _ in range(rounds):
         for k, L in libs.items():
@@ -65,9 +69,13 @@ def ab(libs, run, out, rounds):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rounds", type=int, default=9)
+    ap.add_argument("--extra", nargs="*", default=[], help="name=path of more builds to compare")
     a = ap.parse_args()
-    libs = {"old": load(os.path.join(REPO, "build", "ab", "libmd5hip_old.so")),
-            "new": load(os.path.join(REPO, "sproxy_amd", "lib", "libmd5hip.so"))}
+    libs = {"old": load(os.path.join(REPO, "build", "ab", "libmd5hip_old.so"))}
+    for extra in a.extra:               # name=path, between old and new
+        k, v = extra.split("=", 1)
+        libs[k] = load(os.path.join(REPO, v))
+    libs["new"] = load(os.path.join(REPO, "sproxy_amd", "lib", "libmd5hip.so"))
     st = torch.cuda.current_stream().cuda_stream
     res = {}
 
@@ -119,6 +127,20 @@ def main():
                                                      dR.data_ptr(), nk, dig.data_ptr(), st, 5)
     res["c3k3_balanced"] = ab(libs, run_b, lambda: dig, a.rounds)
     print(json.dumps({"c3k3_balanced": res["c3k3_balanced"]}), flush=True)
+    del big, dO, dL, dR, dig
+    torch.cuda.empty_cache()
+
+    # the single C3 batch, HYBRID (its short-chunk waves use the same loader)
+    big, Lk, O, order, var = batch(1, 1000)
+    nk = Lk.size
+    dO = torch.from_numpy(O).cuda()
+    dL = torch.from_numpy(Lk.astype(np.int32)).cuda()
+    dR = torch.from_numpy(order.astype(np.int32)).cuda()
+    dig = torch.empty((nk, 16), dtype=torch.uint8, device="cuda")
+    run_h = lambda Lb: Lb.md5hip_digest_desc_variant(big.data_ptr(), dO.data_ptr(), dL.data_ptr(),  # noqa
+                                                     dR.data_ptr(), nk, dig.data_ptr(), st, 3)
+    res["c3_hybrid"] = ab(libs, run_h, lambda: dig, a.rounds)
+    print(json.dumps({"c3_hybrid": res["c3_hybrid"]}), flush=True)
     print(json.dumps(res))
 
 
