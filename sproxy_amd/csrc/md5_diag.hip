@@ -1313,6 +1313,44 @@ extern "C" int md5diag_desc_x(int kind, const void* base, const uint64_t* offs, 
   return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }
 
+// Descriptor XDMA with two LDS-DMA images per wave (stage s+2's DMA issued as
+// stage s is read), default cache policy: for 16-B-packed ragged batches the
+// line two stages share is then fetched twice within one stage instead of a
+// compression apart.  16 KiB LDS per one-wave workgroup.
+// md5diag_desc_x2: kind 0 = this, kind 1 = the same with one image (16 KiB
+// allocated, so occupancy matches).
+namespace md5hip {
+template <int NB>
+__global__ void __launch_bounds__(64)
+diag_desc_x2(const uint8_t* __restrict__ base, const uint64_t* __restrict__ offs,
+             const uint32_t* __restrict__ lens, const uint32_t* __restrict__ order, uint64_t n,
+             uint4* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) uint8_t img[16384];
+  asm volatile("" ::: "v127");
+  Md5Hasher<true> h;
+  const uint64_t first = (uint64_t)blockIdx.x * 64u;
+  if (first < n)
+    desc_xpose_group<0, Md5Hasher<true>, 0, 1, false, true, true, DescArrays, true, NB>(
+        h, base, DescArrays{offs, lens, order}, n, first, out, img);
+}
+}  // namespace md5hip
+
+extern "C" int md5diag_desc_x2(int kind, const void* base, const uint64_t* offs, const uint32_t* lens,
+                               const uint32_t* order, uint64_t n, void* out, void* stream) {
+  if (n == 0) return 0;
+  const dim3 g((uint32_t)((n + 63) / 64)), b(64);
+  hipStream_t s = (hipStream_t)stream;
+  if (kind == 0)
+    hipLaunchKernelGGL(md5hip::diag_desc_x2<2>, g, b, 0, s, (const uint8_t*)base, offs, lens, order, n,
+                       (uint4*)out);
+  else if (kind == 1)
+    hipLaunchKernelGGL(md5hip::diag_desc_x2<1>, g, b, 0, s, (const uint8_t*)base, offs, lens, order, n,
+                       (uint4*)out);
+  else
+    return -EINVAL;
+  return hipGetLastError() == hipSuccess ? 0 : -EIO;
+}
+
 // md5_desc_balanced_t with the per-wave record of md5diag_desc_x (one record
 // per persistent wave: its whole run over the groups it took, and how many)
 // for WPB waves per workgroup, NB LDS-DMA images per wave, split queues (A/B).
