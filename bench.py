@@ -824,6 +824,9 @@ def run_c3q(a, rank, world, local, device, backend):
             ps.append(sample_desc(big, starts[j] + ok_[j], lk[j], subs[j][2], idx))
         par = {"checked": sum(p["checked"] for p in ps), "mismatches": sum(p.get("mismatches", 0) for p in ps),
                "ok": all(p["ok"] for p in ps), "checker": ps[0]["checker"]}
+    # PMC of the queue's BALANCED launches (one per pipelined step: K vectors)
+    traffic, tnote = load_traffic(a.traffic, "md5_desc_balanced_t", f"c3q{K}@{a.c3_bytes}")
+    vbusy = load_valu_busy(a.traffic, "md5_desc_balanced_t", f"c3q{K}@{a.c3_bytes}")
     res = {"metric": "device-resident MD5 GiB/s, mixed 4 KiB-1 MiB chunks (C3) through md5hip_queue",
            "value": round(value, 2), "unit": "GiB/s", "n_gpus": world, "steps": a.steps,
            "warmup": a.warmup, "ms_per_step": round(wall_max / a.steps * 1e3, 4),
@@ -836,8 +839,11 @@ def run_c3q(a, rank, world, local, device, backend):
            "roofline": {"bound": "hbm", "achieved": round(payload / (wall_max / a.steps) / 1e9, 1),
                         "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": round(payload / (wall_max / a.steps) / 1e9 / HBM_PEAK_GBS, 4),
-                        "traffic": None, "kernel": "md5hip::md5_desc_* (queue launches)",
-                        "note": "wall-clock per step (submit + wait), several launches per step"},
+                        "traffic": traffic, "traffic_source": tnote, "valu_busy_pmc": vbusy,
+                        "kernel": "md5hip::md5_desc_balanced_t (queue launches)",
+                        "note": "achieved: wall-clock per step (submit + wait); traffic: HBM bytes "
+                                "per BALANCED launch, mean over a profiled run's launches (about "
+                                "one per step of K vectors)"},
            "drained": {"value": round(payload * world * a.steps / wall_d_max / GIB, 2), "unit": "GiB/s",
                        "ms_per_step": round(wall_d_max / a.steps * 1e3, 4),
                        "note": "every step's tickets waited for before the next step submits: each "

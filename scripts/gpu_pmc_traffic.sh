@@ -24,6 +24,7 @@ run crc128 crc@1048576x16384f128 --config crc --fastcrc 128 && \
 run c3 c3@17179869184s1000 --config c3 --c3-legs main && \
 run c3k3 c3k3@17179869184s1000 --config c3 --c3-legs coalesced && \
 run ctx ctx@1048576x16384 --config ctx && \
+run c3q c3q6@17179869184 --config c3q && \
 python3 - "$O/traffic.json" <<'PY'
 import json, sys
 d = json.load(open(sys.argv[1]))["entries"]
