@@ -44,6 +44,7 @@ CPU_SHARE = 16                 # host cores a one-GPU box grants a job (the box'
 
 torch = m = None               # imported after the launcher decision (see main)
 COLL_DEVICE = "cuda"           # where the control-plane scalars live (cpu under gloo)
+COLL_ON = False                # a process group is up (world > 1, or --dist-always)
 
 
 # --------------------------------------------------------------------------- launch
@@ -65,6 +66,9 @@ def parse_args(argv):
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--parity-sample", type=int, default=4096,
                    help="chunks per rank re-digested by the host reference after timing (0 = off)")
+    p.add_argument("--dist-always", action="store_true",
+                   help="bring the process group up even at WORLD_SIZE 1 (a one-GPU rehearsal "
+                        "of the RCCL control plane: init, barrier, MAX, object gathers)")
     p.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                    help="control-plane backend for N > 1 (barrier + scalar MAX + gathers only)")
     p.add_argument("--dry-run", action="store_true",
@@ -123,7 +127,7 @@ def dist_setup(a):
     """One process per GPU.  The collectives are a barrier, scalar MAX/SUM
     reductions and small object gathers, so gloo (CPU) serves as well as RCCL;
     it lets N ranks share one GPU for a rehearsal on a one-GPU box."""
-    global COLL_DEVICE
+    global COLL_DEVICE, COLL_ON
     rank, world, local = env_rank()
     if world != a.gpus:
         raise SystemExit(f"bench.py: --gpus {a.gpus} but WORLD_SIZE={world}")
@@ -137,25 +141,30 @@ def dist_setup(a):
             raise SystemExit(f"bench.py: LOCAL_RANK {local} but only {ndev} GPUs visible")
         device = local % ndev
         torch.cuda.set_device(device)
-    if world > 1:
+    if world > 1 or a.dist_always:
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if world == 1:                   # a one-rank group without a launcher
+            os.environ.setdefault("RANK", "0")
+            os.environ.setdefault("WORLD_SIZE", "1")
+            os.environ.setdefault("MASTER_PORT", str(free_port()))
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", device))
         else:
             dist.init_process_group("gloo")
         COLL_DEVICE = "cuda" if backend == "nccl" else "cpu"
+        COLL_ON = True
     return rank, world, local, device, backend
 
 
 def barrier(world):
-    if world > 1:
+    if COLL_ON:
         import torch.distributed as dist
         dist.barrier()
 
 
 def max_over_ranks(x, world):
-    if world == 1:
+    if not COLL_ON:
         return float(x)
     import torch.distributed as dist
     t = torch.tensor([float(x)], dtype=torch.float64, device=COLL_DEVICE)
@@ -164,7 +173,7 @@ def max_over_ranks(x, world):
 
 
 def gather_objects(obj, world):
-    if world == 1:
+    if not COLL_ON:
         return [obj]
     import torch.distributed as dist
     out = [None] * world
@@ -377,7 +386,7 @@ def per_rank_line(res, rank, world, local, device, backend, rank_bytes, rank_wal
     allr = gather_objects(mine, world)
     res["per_gpu"] = [r["gib_s"] for r in allr]
     devs = [r["dev"] for r in allr]
-    res["ranks_seen"] = {"world": world, "backend": backend if world > 1 else None,
+    res["ranks_seen"] = {"world": world, "backend": backend if COLL_ON else None,
                          "distinct_devices": len({(d["host"], d.get("uuid") or d["device"]) for d in devs
                                                   if d["device"] is not None}),
                          "ranks": devs}
@@ -979,7 +988,7 @@ def main(argv=None):
             res["cpu_baseline"] = cpu_baseline_crc()
     if rank == 0:
         print(json.dumps(res), flush=True)
-    if world > 1:
+    if COLL_ON:
         import torch.distributed as dist
         dist.barrier()
         dist.destroy_process_group()

@@ -50,3 +50,13 @@ def test_world_size_mismatch_fails():
     assert r.returncode != 0
     assert "WORLD_SIZE=3" in r.stderr
     assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+
+
+def test_dist_always_brings_up_a_one_rank_group():
+    """--dist-always: the control plane (init, barrier, MAX, object gathers)
+    runs even at one rank -- the rehearsal of the RCCL path on a one-GPU box."""
+    r = _run(["--gpus", "1", "--dist-always", "--dist-backend", "gloo", "--dry-run", "--steps", "1",
+              "--warmup", "0", "--chunks", "16"])
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = _line(r.stdout)
+    assert d["n_gpus"] == 1 and d["ranks_seen"]["backend"] == "gloo" and d["ranks_seen"]["world"] == 1
