@@ -235,6 +235,7 @@ struct md5hip_batcher {
     pthread_cond_t work_cv;   /* a slot went in flight / stop */
     pthread_t progress;
     int progress_started, stop;
+    int waiters;              /* threads blocked on a ticket: poll the launches fast */
 };
 
 #define CK(x) do { if ((x) != hipSuccess) { rc = -ENODEV; goto fail; } } while (0)
@@ -612,9 +613,13 @@ static void *progress_main(void *arg)
                     o->seen_n = o->n;
                 }
             }
+            /* poll interval: 20 -> 200 us while nobody waits; a blocked
+             * waiter pins it at 10 us, so a short launch is not delivered up
+             * to 200 us late */
+            const unsigned us = b->waiters ? 10u : idle_us;
             struct timespec ts;
             clock_gettime(CLOCK_REALTIME, &ts);
-            ts.tv_nsec += (long)idle_us * 1000;
+            ts.tv_nsec += (long)us * 1000;
             if (ts.tv_nsec >= 1000000000L) { ts.tv_sec++; ts.tv_nsec -= 1000000000L; }
             pthread_cond_timedwait(&b->work_cv, &b->mu, &ts);
             if (idle_us < 200) idle_us += 20;
@@ -1137,6 +1142,8 @@ static int submit(md5hip_batcher *b, const struct chunk_src *src, uint64_t n, un
     if (ticket) *ticket = t;
     if (!async || rc) {
         int err = 0;
+        b->waiters++;
+        pthread_cond_broadcast(&b->work_cv);        /* the progress thread polls fast now */
         while (!tk_done(b, t, &err)) {
             for (uint32_t k = 0; k < b->nslots; k++)
                 if (b->s[k].state == SLOT_OPEN && seg_has(&b->s[k], t)) {
@@ -1145,6 +1152,7 @@ static int submit(md5hip_batcher *b, const struct chunk_src *src, uint64_t n, un
                 }
             pthread_cond_wait(&b->done_cv, &b->mu);
         }
+        b->waiters--;
         if (!rc) rc = err;
     }
     pthread_mutex_unlock(&b->mu);
@@ -1176,10 +1184,13 @@ int md5_batch_wait(md5hip_batcher *b, uint64_t ticket)
     if (ticket >= b->tk_hi) {
         rc = -EINVAL;
     } else {
+        b->waiters++;
+        pthread_cond_broadcast(&b->work_cv);        /* the progress thread polls fast now */
         while (!tk_done(b, ticket, &err)) {
             hasten(b, ticket);
             pthread_cond_wait(&b->done_cv, &b->mu);
         }
+        b->waiters--;
         rc = err;
     }
     pthread_mutex_unlock(&b->mu);
@@ -1354,7 +1365,10 @@ int md5hip_batch_host_fixed(md5hip_batcher *b, const void *h_base, uint64_t n, u
     }
     tk_put(b, t, rc);
     int err = 0;
+    b->waiters++;
+    pthread_cond_broadcast(&b->work_cv);
     while (!tk_done(b, t, &err)) pthread_cond_wait(&b->done_cv, &b->mu);
+    b->waiters--;
     if (!rc) rc = err;
     pthread_mutex_unlock(&b->mu);
     dev_leave(&g);
