@@ -180,6 +180,7 @@ struct slot {
     uint32_t *h_len, *d_len;
     uint32_t *h_ord, *d_ord;
     unsigned char *h_dig, *d_dig;     /* 16 * maxn */
+    int direct;                       /* the kernel wrote the one device segment in place */
     struct md5hip_seg *h_seg, *d_seg; /* zero-copy gather table, `segcap` entries */
     void **b_dst, **b_src;            /* DMA-batch gather arrays (plain host memory) */
     size_t *b_len;
@@ -424,17 +425,26 @@ static int slot_enqueue(md5hip_batcher *b, struct slot *sl)
                         return -EIO;
             }
         }
+        /* one submission whose digests stay on the device and fill the slot
+         * in order: the kernel writes them in place (no scatter launch) */
+        const struct seg *g0 = sl->nsegs == 1 ? &sl->segs[0] : NULL;
+        unsigned char *dst = sl->d_dig;
+        if (g0 && g0->on_device && g0->first == 0 && g0->count == n &&
+            ((uintptr_t)g0->user & 15u) == 0) {
+            dst = g0->user;
+            sl->direct = 1;
+        }
         rc = sl->kind == MD5HIP_DIGEST_CRC32
                  ? crc32hip_desc(sl->d_data, sl->d_off, sl->d_len, sl->d_ord, n, sl->fastcrc,
-                                 (uint32_t *)sl->d_dig, sl->stream)
+                                 (uint32_t *)dst, sl->stream)
                  : md5hip_digest_desc_variant(sl->d_data, sl->d_off, sl->d_len, sl->d_ord, n,
-                                              sl->d_dig, sl->stream, dvar);
+                                              dst, sl->stream, dvar);
         if (rc) return rc;
     }
     /* digests out: one D2H for the host segments, one scatter for the device ones */
     int any_host = 0;
     sl->ndsc = 0;
-    for (uint32_t k = 0; k < sl->nsegs; k++) {
+    for (uint32_t k = 0; k < sl->nsegs && !sl->direct; k++) {
         const struct seg *g = &sl->segs[k];
         if (!g->on_device) { any_host = 1; continue; }
         sl->h_dsc[sl->ndsc++] = (struct md5hip_seg){
@@ -459,7 +469,7 @@ static void slot_reset(struct slot *sl)
 {
     sl->state = SLOT_FREE;
     sl->mode = MODE_NONE;
-    sl->writers = sl->full = sl->flush = sl->err = 0;
+    sl->writers = sl->full = sl->flush = sl->err = sl->direct = 0;
     sl->n = sl->used = sl->nseg = sl->ndma = sl->ndsc = 0;
     sl->nsegs = 0;
     sl->tickets_in = 0;
