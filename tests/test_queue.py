@@ -37,6 +37,34 @@ def test_queue_device_chunks_host_and_device_digests(cuda):
     assert np.array_equal(out.cpu().numpy(), want)
 
 
+def test_queue_device_digests_in_place_and_scattered(cuda):
+    """Device-side digests: a slot holding one in-order submission is written
+    in place by the kernel (16-B-aligned output, also slot by slot when the
+    submission spans several slots); an unaligned output, or several
+    submissions sharing a slot, go through the scatter kernel."""
+    rng = np.random.default_rng(17)
+    lens = [int(x) for x in rng.integers(0, 70000, 1000)] + [0, 1, 63, 64, 65]
+    dev, ptrs, L, want = _arena_batch(lens, 171, cuda)
+    n = len(lens)
+    with m.Queue(device=0, max_chunks=256) as q:                      # 4+ slots' worth
+        out = torch.empty((n, 16), dtype=torch.uint8, device=cuda)
+        q.submit_device(ptrs, L, out=out)
+        torch.cuda.synchronize()
+        assert np.array_equal(out.cpu().numpy(), want)
+        raw = torch.zeros(n * 16 + 4, dtype=torch.uint8, device=cuda)
+        odd = raw[4:].view(n, 16)                                     # not 16-B aligned
+        q.submit_device(ptrs, L, out=odd)
+        torch.cuda.synchronize()
+        assert np.array_equal(odd.cpu().numpy(), want)
+        halves = [torch.empty((k, 16), dtype=torch.uint8, device=cuda) for k in (100, 150)]
+        p1 = q.submit_device_async(ptrs[:100], L[:100], out=halves[0])
+        p2 = q.submit_device_async(ptrs[100:250], L[100:250], out=halves[1])
+        p1.wait()
+        p2.wait()
+        torch.cuda.synchronize()
+        assert np.array_equal(torch.cat(halves).cpu().numpy(), want[:250])
+
+
 def test_queue_tickets_complete_out_of_order(cuda):
     """A submission of four 64 MiB chunks (each a ~0.6 s serial chain) and a
     later one of short chunks: the short ticket completes while the long one
