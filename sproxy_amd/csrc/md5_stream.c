@@ -127,8 +127,15 @@ void MD5Update(struct MD5Context *ctx, const void *buf, unsigned len)
         src += room;
         len -= room;
     }
-    md5_blocks(ctx->buf, src, len >> 6);
+    const unsigned whole = len >> 6;
+    md5_blocks(ctx->buf, src, whole);
     src += len & ~63u;
+    /* md5.c:204-214 copies every whole block through ctx->in before it is
+     * transformed, so in[] ends as the last whole block with the tail copied
+     * over its first bytes.  Hashing straight from the source and copying that
+     * block once leaves the same 88 bytes. */
+    if (whole)
+        memcpy(ctx->in, src - 64, 64);
     memcpy(ctx->in, src, len & 63u);
 }
 

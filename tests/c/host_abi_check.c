@@ -10,6 +10,9 @@
  *   hdr <hex> <ok>       nc_header_crc / nc_header_verify of a sealed header
  *   plan <G> <first...>  md5hip_pool_plan over a fixed length list
  *   arr <rc...>          nc_digest_update / verify bound cases
+ *   ctx <seq> <off> <n> <hex88>  the whole context after each MD5Update of
+ *                        buf[off:off+n] (stale in[] preset to 0x5a), for the
+ *                        test to replay through the reference md5.c
  */
 #include <stdint.h>
 #include <stdio.h>
@@ -77,6 +80,19 @@ int main(void)
     h[500] ^= 1;
     printf("hdrbad %d\n", nc_header_verify(h));
     free(h);
+    /* call-by-call context bytes (md5.c:204-214 leaves the last whole block in in[]) */
+    for (int seq = 0; seq < 40; seq++) {
+        struct MD5Context ctx;
+        MD5Init(&ctx);
+        memset(ctx.in, 0x5a, sizeof ctx.in);
+        for (int call = 0; call < 6; call++) {
+            rng ^= rng << 13; rng ^= rng >> 7; rng ^= rng << 17;
+            const unsigned n = (unsigned)(rng % (call & 1 ? 300u : 5000u));
+            const unsigned off = (unsigned)((rng >> 20) % (maxlen - n));
+            MD5Update(&ctx, buf + off, n);
+            printf("ctx %d %u %u ", seq, off, n); hex((const unsigned char *)&ctx, sizeof ctx); printf("\n");
+        }
+    }
     /* pool split */
     uint32_t pl[100];
     for (int i = 0; i < 100; i++) pl[i] = (uint32_t)((i * 7919u) % 5000u);

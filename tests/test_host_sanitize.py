@@ -73,6 +73,24 @@ def test_host_entries_under_asan(asan_run, golden):
             assert r[1:] == ["0", "-34", "-7", "1", "0"]      # ok, ERANGE, E2BIG, equal, differs
             seen.add("arr")
     assert seen == {"md5", "crc", "hdr", "plan", "arr"}
+    ctx_rows = [r for r in rows if r[0] == "ctx"]
+    assert len(ctx_rows) == 240
+    ref = os.path.join(gen.REPO, "oracle", "_ref", "libmd5_ref.so")
+    if os.path.exists(ref):                  # replay through the reference md5.c
+        import ctypes
+        R = ctypes.CDLL(ref)
+        R.MD5Init.argtypes = [ctypes.c_void_p]
+        R.MD5Update.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint]
+        src = np.frombuffer(big, np.uint8)
+        ctx = np.zeros(88, np.uint8)
+        for r in ctx_rows:
+            seq, off, n = int(r[1]), int(r[2]), int(r[3])
+            if r is ctx_rows[0] or seq != prev:
+                R.MD5Init(ctx.ctypes.data)
+                ctx[24:] = 0x5A
+            prev = seq
+            R.MD5Update(ctx.ctypes.data, src.ctypes.data + off, n)
+            assert ctx.tobytes().hex() == r[4], (seq, off, n)
     ncm = {int(r[1]): r[2] for r in rows if r[0] == "ncmd5"}
     assert len(ncm) == 16
     for L, hx in ncm.items():
