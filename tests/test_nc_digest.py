@@ -144,18 +144,24 @@ def test_gpu_batch_verify_headers(cuda):
 
 
 def test_header_layout_against_reference_probe():
-    """include/nc_digest.h's header offsets against offsetof() in the
-    reference netcache.h compiled as is (oracle/nc_header_probe.c, `make -C
-    oracle probe`).  netcache.h needs <uuid/uuid.h>, absent in this image and
-    not stubbed, so without the probe's output this row is parity unpinned
-     and the test says so."""
+    """include/nc_digest.h's header offsets, magic and canned-array size
+    against the reference netcache.h compiled as is
+    (oracle/nc_header_probe.c with the image's libuuid 1.0.3 header;
+    tests/golden/make_nc_layout.py wrote the fixture).  When the probe builds
+    here, its live output must equal the committed fixture too."""
     import re
-    path = os.path.join(gen.REPO, "oracle", "_ref", "nc_header_layout.json")
-    if not os.path.exists(path):
-        pytest.skip("parity unpinned: netcache.h does not compile here without <uuid/uuid.h>")
-    lay = json.load(open(path))
+    lay = json.load(open(os.path.join(gen.REPO, "tests", "golden", "nc_header_layout.json")))
+    live = os.path.join(gen.REPO, "oracle", "_ref", "nc_header_layout.json")
+    if os.path.exists(live):
+        got = json.load(open(live))
+        assert all(lay[k] == v for k, v in got.items()), got
     hdr = open(os.path.join(gen.REPO, "include", "nc_digest.h")).read()
     off = {k: int(v) for k, v in re.findall(r"#define NC_HDR_OFF_(\w+) (\d+)", hdr)}
     assert off["MAGIC"] == lay["magic"] and off["DISK_HEADER_SIZE"] == lay["disk_header_size"]
     assert off["HEADER_SIZE"] == lay["header_size"] and off["FLAG"] == lay["flag"]
     assert off["CRC"] == lay["crc"] and lay["sizeof_nc_crc_t"] == 4
+    assert lay["sizeof_fc_common_header_t"] == 16 and lay["block_size"] == off["CRC"] + 4
+    assert nd.HDR_MIN_SIZE == lay["crc"] + lay["sizeof_nc_crc_t"]
+    assert nd.NC_MAGIC_V30 == lay["NC_MAGIC_V30"]
+    for bl, size in lay["NC_CANNED_CRC_SIZE"]:
+        assert nd.canned_digest_size(bl, 4) == size, bl
