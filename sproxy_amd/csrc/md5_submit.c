@@ -48,6 +48,7 @@
 
 #include "../../include/md5hip.h"
 #include "md5_internal.h"
+#include "md5_tickets.h"
 
 /* ------------------------------------------------------------------------
  * Registered host ranges (zero-copy input).  netcache allocates its cache
@@ -224,12 +225,7 @@ struct md5hip_batcher {
     struct slot *s;
     int open;          /* index of the OPEN slot new chunks go to, -1 = none */
     uint32_t inflight;
-    /* tickets: ring of ids [tk_lo, tk_hi); id t at tk[t & (tkcap - 1)] */
-    uint64_t tk_lo, tk_hi;
-    uint32_t *tk_pending;
-    int *tk_err;
-    uint64_t tkcap;
-    int broken;        /* sticky first error of a ticket that has left the ring */
+    struct tk_ring tk; /* tickets: live ids, their references and errors (md5_tickets.h) */
     struct md5hip_batcher_stats st;
     pthread_mutex_t mu;
     pthread_cond_t done_cv;   /* a slot retired / a ticket completed */
@@ -270,58 +266,10 @@ static void wait_work_us(md5hip_batcher *b, uint64_t us)
     pthread_cond_timedwait(&b->work_cv, &b->mu, &ts);
 }
 
-static int tk_grow(md5hip_batcher *b)
-{
-    const uint64_t nc = b->tkcap ? 2 * b->tkcap : 1024;
-    uint32_t *p = malloc(nc * sizeof *p);
-    int *e = malloc(nc * sizeof *e);
-    if (!p || !e) { free(p); free(e); return -ENOMEM; }
-    for (uint64_t t = b->tk_lo; t < b->tk_hi; t++) {
-        p[t & (nc - 1)] = b->tk_pending[t & (b->tkcap - 1)];
-        e[t & (nc - 1)] = b->tk_err[t & (b->tkcap - 1)];
-    }
-    free(b->tk_pending);
-    free(b->tk_err);
-    b->tk_pending = p;
-    b->tk_err = e;
-    b->tkcap = nc;
-    return 0;
-}
-
-/* a new ticket holding one "submission in progress" reference (mu held) */
-static int tk_new(md5hip_batcher *b, uint64_t *t)
-{
-    if (b->tk_hi - b->tk_lo == b->tkcap) {
-        const int rc = tk_grow(b);
-        if (rc) return rc;
-    }
-    const uint64_t id = b->tk_hi++;
-    b->tk_pending[id & (b->tkcap - 1)] = 1;
-    b->tk_err[id & (b->tkcap - 1)] = 0;
-    *t = id;
-    return 0;
-}
-
-/* 1 = complete, 0 = pending; *err = its error (mu held) */
-static int tk_done(const md5hip_batcher *b, uint64_t t, int *err)
-{
-    if (t < b->tk_lo) { *err = b->broken; return 1; }
-    *err = b->tk_err[t & (b->tkcap - 1)];
-    return b->tk_pending[t & (b->tkcap - 1)] == 0;
-}
-
-static void tk_put(md5hip_batcher *b, uint64_t t, int err)
-{
-    if (t < b->tk_lo) return;
-    const uint64_t k = t & (b->tkcap - 1);
-    if (err && !b->tk_err[k]) b->tk_err[k] = err;
-    if (b->tk_pending[k]) b->tk_pending[k]--;
-    while (b->tk_lo < b->tk_hi && b->tk_pending[b->tk_lo & (b->tkcap - 1)] == 0) {
-        const int e = b->tk_err[b->tk_lo & (b->tkcap - 1)];
-        if (e && !b->broken) b->broken = e;
-        b->tk_lo++;
-    }
-}
+/* ticket table (md5_tickets.h), all under b->mu */
+static int tk_new(md5hip_batcher *b, uint64_t *t) { return tk_ring_new(&b->tk, t); }
+static int tk_done(const md5hip_batcher *b, uint64_t t, int *err) { return tk_ring_done(&b->tk, t, err); }
+static void tk_put(md5hip_batcher *b, uint64_t t, int err) { tk_ring_put(&b->tk, t, err); }
 
 /* One segment per (ticket, slot): a submission fills a slot until it is full
  * before it moves on, so its chunks in one slot are one contiguous run. */
@@ -661,8 +609,7 @@ static void batcher_free(md5hip_batcher *b)
         hipHostFree(sl->h_bkt); hipFree(sl->d_bkt);
     }
     free(b->s);
-    free(b->tk_pending);
-    free(b->tk_err);
+    tk_ring_free(&b->tk);
     pthread_mutex_destroy(&b->mu);
     pthread_cond_destroy(&b->done_cv);
     pthread_cond_destroy(&b->work_cv);
@@ -720,9 +667,9 @@ static int batcher_new(int device, uint64_t slice_bytes, uint32_t nslots, uint64
     b->target = nslots > 2 ? 2 : 1;
     b->linger_max_us = 5000;
     b->open = -1;
-    b->tk_lo = b->tk_hi = 1;              /* ticket 0 = "nothing": complete at once */
     b->s = calloc(nslots, sizeof *b->s);
-    if (!b->s || tk_grow(b)) { rc = -ENOMEM; goto fail; }
+    /* ticket 0 = "nothing": complete at once */
+    if (!b->s || tk_ring_init(&b->tk, 1)) { rc = -ENOMEM; goto fail; }
     for (uint32_t k = 0; k < nslots; k++) {
         struct slot *sl = &b->s[k];
         CK(hipStreamCreateWithFlags(&sl->stream, hipStreamNonBlocking));
@@ -1135,7 +1082,7 @@ static int submit(md5hip_batcher *b, const struct chunk_src *src, uint64_t n, un
             sl->err = rc;                    /* its reserved chunks have no segment */
             break;
         }
-        b->tk_pending[t & (b->tkcap - 1)]++;
+        tk_ring_ref(&b->tk, t);
         if (mode == MODE_STAGED && hi > lo) {
             /* copy outside the lock: other submitters may reserve behind us */
             sl->writers++;
@@ -1191,7 +1138,7 @@ int md5_batch_wait(md5hip_batcher *b, uint64_t ticket)
     if (ticket == 0) return 0;               /* "nothing submitted" */
     pthread_mutex_lock(&b->mu);
     int rc = 0, err = 0;
-    if (ticket >= b->tk_hi) {
+    if (ticket >= b->tk.hi) {
         rc = -EINVAL;
     } else {
         b->waiters++;
@@ -1213,7 +1160,7 @@ int md5_batch_poll(md5hip_batcher *b, uint64_t ticket)
     if (ticket == 0) return 1;
     pthread_mutex_lock(&b->mu);
     int rc, err = 0;
-    if (ticket >= b->tk_hi) {
+    if (ticket >= b->tk.hi) {
         rc = -EINVAL;
     } else if (tk_done(b, ticket, &err)) {
         rc = err ? err : 1;
@@ -1370,7 +1317,7 @@ int md5hip_batch_host_fixed(md5hip_batcher *b, const void *h_base, uint64_t n, u
             slot_retire(b, sl, rc);
             break;
         }
-        b->tk_pending[t & (b->tkcap - 1)]++;
+        tk_ring_ref(&b->tk, t);
         slot_try_launch(b, sl);
     }
     tk_put(b, t, rc);
