@@ -430,7 +430,8 @@ def run_dry(a, rank, world, local, device, backend):
            "ms_per_step": round(wall_max / a.steps * 1e3, 4), "higher_is_better": True,
            "scaling": "weak", "vs_baseline": None, "dtype": "u32", "dry_run": True,
            "data": "synthetic host buffers (CPU dry run: product host MD5, no GPU)",
-           "config": {"workload": f"dry run: {n} x {L} B host chunks per rank",
+           "config": {"workload": f"dry run: {n} x {L} B host chunks per rank, standing in for "
+                                  f"{c2_workload(*c2_shape_gpu(a, world), L, world, bool(a.total_chunks))}",
                       "chunks_per_gpu": n, "chunk_bytes": L,
                       "parallelism": f"dp{world} (independent chunk shards, no collective)"}}
     return per_rank_line(res, rank, world, local, device, backend, n * L * a.steps, wall, par)
@@ -442,6 +443,15 @@ def c2_shape(a, rank, world):
         hi = a.total_chunks * (rank + 1) // world
         return hi - lo, a.total_chunks
     n = a.chunks or ((1 << 20) if world == 1 else (1 << 21))
+    return n, n * world
+
+
+def c2_shape_gpu(a, world):
+    """(chunks per GPU, chunks in all) of the device run these flags select
+    (the dry run names it; --chunks sizes only the dry run's host batch)."""
+    if a.total_chunks:
+        return a.total_chunks // world, a.total_chunks
+    n = (1 << 20) if world == 1 else (1 << 21)
     return n, n * world
 
 
@@ -775,6 +785,7 @@ def run_c3q(a, rank, world, local, device, backend):
     starts = np.concatenate([[0], np.cumsum(spans)[:-1]]).astype(np.int64)
     big = m.arena_empty(int(sum(spans)))
     m.fill_synthetic(big, seed=0xC3D + rank)
+    torch.cuda.synchronize()           # the queue also orders itself after torch's stream
     base = big.data_ptr()
     subs = []
     for j in range(K):

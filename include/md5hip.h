@@ -299,6 +299,17 @@ int md5_batch_submit_device_async(md5hip_batcher *b, const uint64_t *d_ptrs, con
                                   uint64_t *ticket);
 int md5_batch_submit_device(md5hip_batcher *b, const uint64_t *d_ptrs, const uint32_t *lens,
                             uint64_t n, unsigned char *digests, int digests_on_device);
+/* The two forms above run on the batcher's own streams with NO ordering
+ * against the caller's: the chunks must be written (and the digest memory
+ * free to overwrite) before the call, e.g. after hipStreamSynchronize on the
+ * producer's stream.  This form takes the producer's stream instead: the
+ * kernel that reads the chunks (and writes device digests) runs after all
+ * work enqueued on `producer_stream` before the call, with no host sync.
+ * producer_stream NULL = no ordering; it must belong to the batcher's device
+ * (-EINVAL otherwise).  ticket NULL = synchronous, else as the _async form. */
+int md5_batch_submit_device_on(md5hip_batcher *b, const uint64_t *d_ptrs, const uint32_t *lens,
+                               uint64_t n, unsigned char *digests, int digests_on_device,
+                               void *producer_stream, uint64_t *ticket);
 /* Block until submission `ticket` has delivered its digests: 0 or -errno.
  * A ticket still coalescing in the open slot is launched at once when
  * nothing is in flight (no linger); otherwise its slot goes out as soon as a
@@ -348,22 +359,32 @@ int md5hip_batch_host_fixed(md5hip_batcher *b, const void *h_base, uint64_t n, u
                             uint64_t stride, unsigned char *digests);
 
 /*
- * Multi-GPU host pool.  Chunks are independent, so a batch
- * shards with no collective: the pool owns one batcher per listed device
- * (a device may be listed twice) and cuts every call into contiguous chunk
- * ranges, one per device, balanced by bytes; a host thread per device drives
- * its range and writes the digests straight into its slice of `digests`.
- * Same results and errors as the batcher entries; calls are synchronous and
- * serialized by an internal lock, so one pool may be shared by threads.
+ * Multi-GPU host pool: a router over one coalescing batcher
+ * per listed device (a device may be listed more than once).  Chunks are
+ * independent, so no collective is needed.  Each submission goes WHOLE to
+ * the device whose batcher holds the least outstanding work (bytes reserved
+ * and not yet delivered), so a netcache vector keeps its one launch and
+ * coalesces there with other threads' vectors.  Only a submission larger than
+ * the split threshold (default: one batcher slice) is cut into contiguous
+ * byte-balanced ranges (md5hip_pool_plan) over the least-loaded devices.
+ * No pool-wide lock is held across device work and no thread is created per
+ * call: any number of threads (the ASIO pool, asio_mgr.c:205, :1050-1057)
+ * may submit concurrently.  Same results and errors as the batcher entries.
  */
 typedef struct md5hip_pool md5hip_pool;
 
 int md5hip_pool_create(const int *devices, uint32_t ndev, uint64_t slice_bytes, uint32_t nslots,
                        md5hip_pool **out);
+/* Waits for everything in flight, then frees. */
 void md5hip_pool_destroy(md5hip_pool *p);
 int md5hip_pool_ndev(const md5hip_pool *p);
+/* The digest kind of later submissions (submissions already made keep
+ * theirs); MD5 or CRC32 with a fastcrc window as md5hip_batcher_set_digest. */
 int md5hip_pool_set_digest(md5hip_pool *p, int kind, uint32_t fastcrc);
 int md5hip_pool_set_gather(md5hip_pool *p, int mode);
+/* Submissions above `bytes` (sum of chunk lengths) are split over devices;
+ * 0 = one batcher slice (the default). */
+int md5hip_pool_set_split(md5hip_pool *p, uint64_t bytes);
 int md5hip_pool_submit(md5hip_pool *p, const void *const *ptrs, const uint32_t *lens, uint64_t n,
                        unsigned char *digests);
 int md5hip_pool_submit_iov(md5hip_pool *p, const struct md5hip_iov *segs,
@@ -373,6 +394,30 @@ int md5hip_pool_verify_iov(md5hip_pool *p, const struct md5hip_iov *segs,
                            unsigned char *ok);
 int md5hip_pool_host_fixed(md5hip_pool *p, const void *h_base, uint64_t n, uint32_t len,
                            uint64_t stride, unsigned char *digests);
+/* Asynchronous forms, ticket semantics as md5_batch_submit_async: the call
+ * returns once the chunks are staged, *ticket (0 for an empty submission)
+ * completes when every device holding its chunks has delivered them, and
+ * `digests` must stay valid until then.  A pool ticket is only meaningful to
+ * the pool that issued it. */
+int md5hip_pool_submit_async(md5hip_pool *p, const void *const *ptrs, const uint32_t *lens,
+                             uint64_t n, unsigned char *digests, uint64_t *ticket);
+int md5hip_pool_submit_iov_async(md5hip_pool *p, const struct md5hip_iov *segs,
+                                 const uint64_t *seg_first, uint64_t n, unsigned char *digests,
+                                 uint64_t *ticket);
+/* 0 or the ticket's own -errno (first failing part); -EINVAL if unknown. */
+int md5hip_pool_wait(md5hip_pool *p, uint64_t ticket);
+/* 1 = delivered, 0 = running, <0 = its error. */
+int md5hip_pool_poll(md5hip_pool *p, uint64_t ticket);
+
+struct md5hip_pool_stats {
+    uint64_t submissions;             /* non-empty submissions */
+    uint64_t routed_whole;            /* went whole to one device */
+    uint64_t split;                   /* cut over several devices */
+    uint64_t parts;                   /* device submissions made in all */
+};
+int md5hip_pool_get_stats(md5hip_pool *p, struct md5hip_pool_stats *out);
+/* Device g's batcher counters (launches, coalesced launches, ...). */
+int md5hip_pool_device_stats(md5hip_pool *p, uint32_t g, struct md5hip_batcher_stats *out);
 
 /* The pool's split, exposed for callers and tests (host only, synchronous):
  * first[0..nparts] such that part g is chunks [first[g], first[g+1]).

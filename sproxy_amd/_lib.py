@@ -46,6 +46,11 @@ class MD5HipBatcherStats(ctypes.Structure):
         "max_chunks_per_slot")]
 
 
+class MD5HipPoolStats(ctypes.Structure):
+    """struct md5hip_pool_stats (include/md5hip.h)."""
+    _fields_ = [(n, ctypes.c_uint64) for n in ("submissions", "routed_whole", "split", "parts")]
+
+
 class MD5HipError(RuntimeError):
     def __init__(self, fn, rc):
         name = errno.errorcode.get(-rc, str(rc))
@@ -118,6 +123,14 @@ def lib():
         "md5hip_host_unregister": (i, [vp]),
         "md5hip_batcher_set_gather": (i, [vp, i]),
         "md5hip_pool_set_gather": (i, [vp, i]),
+        "md5hip_pool_set_split": (i, [vp, u64]),
+        "md5hip_pool_submit_async": (i, [vp, vp, vp, u64, vp, vp]),
+        "md5hip_pool_submit_iov_async": (i, [vp, vp, vp, u64, vp, vp]),
+        "md5hip_pool_wait": (i, [vp, u64]),
+        "md5hip_pool_poll": (i, [vp, u64]),
+        "md5hip_pool_get_stats": (i, [vp, ctypes.POINTER(MD5HipPoolStats)]),
+        "md5hip_pool_device_stats": (i, [vp, u32, ctypes.POINTER(MD5HipBatcherStats)]),
+        "md5_batch_submit_device_on": (i, [vp, vp, vp, u64, vp, i, vp, vp]),
         "nc_canned_digest_size": (u64, [u32, u32]),
         "nc_digest_update": (i, [vp, u64, u32, u64, u64, vp]),
         "nc_digest_verify": (i, [vp, u64, u32, u64, vp]),
@@ -159,7 +172,9 @@ EXPORTS = ["MD5Init", "MD5Update", "MD5Final", "nc_MD5Init", "nc_MD5Update", "nc
            "md5hip_batcher_set_inflight", "md5hip_batcher_set_linger", "md5hip_plan_hist", "md5hip_order_device",
            "md5hip_batcher_get_stats", "md5_batch_submit_device_async",
            "md5_batch_submit_device", "md5_batch_flush", "md5hip_init_ctx", "md5hip_update_ctx",
-           "md5hip_final_ctx"]
+           "md5hip_final_ctx", "md5hip_pool_set_split", "md5hip_pool_submit_async",
+           "md5hip_pool_submit_iov_async", "md5hip_pool_wait", "md5hip_pool_poll",
+           "md5hip_pool_get_stats", "md5hip_pool_device_stats", "md5_batch_submit_device_on"]
 
 
 def check(fn, rc):

@@ -1,16 +1,29 @@
 /*
- * md5_pool.c -- multi-GPU host pool (include/md5hip.h).
+ * md5_pool.c -- multi-GPU host pool (include/md5hip.h): a
+ * router over one coalescing batcher (md5_submit.c) per listed device.
  *
- * Chunks are independent, so a batch shards with no collective: the pool cuts
- * it into contiguous chunk ranges, one per device, and a host thread per
- * device drives that device's batcher (md5_submit.c), which writes its
- * digests straight into its own slice of the caller's digest array.  Ranges
- * are balanced by bytes (md5hip_pool_plan) because a netcache batch mixes
- * block sizes (chunk_size 4 KiB-1 MiB, httpd.c:7968) and last-block tails
- * (blk_io.c:377); fixed-length batches reduce to [g*n/G, (g+1)*n/G).
+ * The reference calls its chunk checksum (blk_make_crc, blk_io.c:354) from
+ * every ASIO pool thread at once, without a lock (asio_mgr.c:205,
+ * :1050-1057), one vector of 64-1,024 blocks at a time, and completes the
+ * vector as a unit (asio_read_vector_done_LOCK, asio_mgr.c:1414).  So the
+ * pool keeps a vector whole: a submission goes to the device whose batcher
+ * has the least outstanding weight, where it coalesces with the other
+ * threads' vectors into that device's next launch.  Cutting a 64-block
+ * vector eight ways would make eight launches, each bound by one 16 KiB
+ * chunk's serial chain.  Only a submission heavier than the split threshold
+ * (one batcher slice by default) is cut into contiguous byte-balanced ranges
+ * (md5hip_pool_plan) over the least-loaded devices.
  *
- * A pool serializes its callers with a mutex, so the ASIO pool threads that
- * call blk_make_crc concurrently (asio_mgr.c:1054-1057) may share one.
+ * Concurrency: routing reads each batcher's load lock-free and reserves the
+ * submission's weight on the chosen device (`claim`) until the batcher has
+ * taken the chunks, so concurrent callers spread instead of piling onto the
+ * same idle device.  p->mu guards only the pool's own fields (digest kind,
+ * counters, the multi-part ticket table) and is never held across a batcher
+ * call that waits for the device.  No thread is created per call.
+ *
+ * Tickets: a submission routed whole is (batcher ticket << 6) | device; a
+ * split one is bit 63 | id, its parts kept in `mt` (ascending ids) until all
+ * of them have completed, then dropped (an error is kept in `failed`).
  */
 #include <errno.h>
 #include <pthread.h>
@@ -19,14 +32,40 @@
 #include <string.h>
 
 #include "../../include/md5hip.h"
+#include "md5_internal.h"
 
 #define POOL_MAX_DEV 64
+#define MT_BIT (1ull << 63)
+#define FAILED_MAX (1u << 16)
+
+struct mt_part {
+    uint32_t dev;
+    uint64_t t;
+};
+
+struct mt_entry {                      /* one split submission */
+    uint64_t id;
+    uint32_t nparts;
+    struct mt_part part[];
+};
 
 struct md5hip_pool {
     uint32_t ndev;
-    uint32_t dsz;                        /* digest bytes per chunk */
     md5hip_batcher *b[POOL_MAX_DEV];
-    pthread_mutex_t lock;
+    uint64_t claim[POOL_MAX_DEV];     /* weight routed to a device, not yet taken by its batcher */
+    pthread_mutex_t mu;
+    int kind;
+    uint32_t fastcrc;
+    uint64_t split_bytes;             /* 0 = one batcher slice */
+    uint32_t rr;                      /* rotating start for ties */
+    struct md5hip_pool_stats st;
+    /* split tickets still running, ascending ids; [mt_lo, mt_lo + mt_n) of a ring */
+    struct mt_entry **mt;
+    uint64_t mt_cap, mt_lo, mt_n, mt_next;
+    /* split tickets that completed with an error: (id, err), ascending */
+    uint64_t *failed_id;
+    int *failed_err;
+    uint64_t nfailed, capfailed;
 };
 
 /* Per-chunk weight for the byte balance: payload plus a fixed cost per chunk
@@ -58,7 +97,11 @@ void md5hip_pool_destroy(md5hip_pool *p)
 {
     if (!p) return;
     for (uint32_t g = 0; g < p->ndev; g++) md5hip_batcher_destroy(p->b[g]);
-    pthread_mutex_destroy(&p->lock);
+    for (uint64_t k = 0; k < p->mt_n; k++) free(p->mt[(p->mt_lo + k) % p->mt_cap]);
+    free(p->mt);
+    free(p->failed_id);
+    free(p->failed_err);
+    pthread_mutex_destroy(&p->mu);
     free(p);
 }
 
@@ -70,8 +113,9 @@ int md5hip_pool_create(const int *devices, uint32_t ndev, uint64_t slice_bytes, 
     if (!devices || ndev == 0 || ndev > POOL_MAX_DEV) return -EINVAL;
     md5hip_pool *p = calloc(1, sizeof *p);
     if (!p) return -ENOMEM;
-    pthread_mutex_init(&p->lock, NULL);
-    p->dsz = 16;
+    pthread_mutex_init(&p->mu, NULL);
+    p->kind = MD5HIP_DIGEST_MD5;
+    p->mt_next = 1;
     for (uint32_t g = 0; g < ndev; g++) {
         int rc = md5hip_batcher_create(devices[g], slice_bytes, nslots, &p->b[g]);
         if (rc) {
@@ -90,93 +134,456 @@ int md5hip_pool_ndev(const md5hip_pool *p) { return p ? (int)p->ndev : -EINVAL; 
 int md5hip_pool_set_digest(md5hip_pool *p, int kind, uint32_t fastcrc)
 {
     if (!p) return -EINVAL;
-    pthread_mutex_lock(&p->lock);
-    int rc = 0;
-    for (uint32_t g = 0; g < p->ndev && rc == 0; g++)
-        rc = md5hip_batcher_set_digest(p->b[g], kind, fastcrc);
-    if (rc == 0) p->dsz = kind == MD5HIP_DIGEST_CRC32 ? 4 : 16;
-    pthread_mutex_unlock(&p->lock);
-    return rc;
+    if (kind == MD5HIP_DIGEST_MD5 ? fastcrc != 0
+        : kind == MD5HIP_DIGEST_CRC32 ? (fastcrc & 3u) != 0 : 1)   /* cfs_apix.c:2222-2236 */
+        return -EINVAL;
+    pthread_mutex_lock(&p->mu);
+    p->kind = kind;
+    p->fastcrc = fastcrc;
+    pthread_mutex_unlock(&p->mu);
+    return 0;
 }
 
 int md5hip_pool_set_gather(md5hip_pool *p, int mode)
 {
     if (!p) return -EINVAL;
-    pthread_mutex_lock(&p->lock);
     int rc = 0;
     for (uint32_t g = 0; g < p->ndev && rc == 0; g++) rc = md5hip_batcher_set_gather(p->b[g], mode);
-    pthread_mutex_unlock(&p->lock);
     return rc;
 }
 
-/* One device's share of a call. */
-enum job_kind { JOB_PTRS, JOB_IOV, JOB_FIXED };
-struct job {
-    enum job_kind kind;
-    md5hip_batcher *b;
-    uint64_t lo, hi;                     /* chunk range */
-    const void *const *ptrs;             /* JOB_PTRS */
-    const uint32_t *lens;
-    const struct md5hip_iov *segs;       /* JOB_IOV */
-    const uint64_t *seg_first;
-    uint64_t *rebased;                   /* JOB_IOV: seg_first[lo..hi] - seg_first[lo] */
-    const unsigned char *h_base;         /* JOB_FIXED */
-    uint32_t len;
-    uint64_t stride;
-    unsigned char *digests;              /* already offset to chunk lo */
-    int rc;
-};
-
-static void *job_run(void *arg)
+int md5hip_pool_set_split(md5hip_pool *p, uint64_t bytes)
 {
-    struct job *j = arg;
-    const uint64_t m = j->hi - j->lo;
-    if (m == 0) { j->rc = 0; return NULL; }
-    switch (j->kind) {
-    case JOB_PTRS:
-        j->rc = md5_batch_submit(j->b, j->ptrs + j->lo, j->lens + j->lo, m, j->digests);
-        break;
-    case JOB_IOV:
-        j->rc = md5_batch_submit_iov(j->b, j->segs + j->seg_first[j->lo], j->rebased, m, j->digests);
-        break;
-    case JOB_FIXED:
-        j->rc = md5hip_batch_host_fixed(j->b, j->h_base + j->lo * j->stride, m, j->len, j->stride,
-                                        j->digests);
-        break;
+    if (!p) return -EINVAL;
+    pthread_mutex_lock(&p->mu);
+    p->split_bytes = bytes;
+    pthread_mutex_unlock(&p->mu);
+    return 0;
+}
+
+int md5hip_pool_get_stats(md5hip_pool *p, struct md5hip_pool_stats *out)
+{
+    if (!p || !out) return -EINVAL;
+    pthread_mutex_lock(&p->mu);
+    *out = p->st;
+    pthread_mutex_unlock(&p->mu);
+    return 0;
+}
+
+int md5hip_pool_device_stats(md5hip_pool *p, uint32_t g, struct md5hip_batcher_stats *out)
+{
+    if (!p || !out || g >= p->ndev) return -EINVAL;
+    return md5hip_batcher_get_stats(p->b[g], out);
+}
+
+/* ------------------------------------------------------------------------
+ * Routing
+ * ------------------------------------------------------------------------ */
+static uint64_t dev_load(md5hip_pool *p, uint32_t g)
+{
+    return md5hip_batcher_load(p->b[g]) + __atomic_load_n(&p->claim[g], __ATOMIC_RELAXED);
+}
+
+/* The k least-loaded devices (ties from a rotating start), their weight w
+ * claimed on each; into sel[0..k). */
+static void route(md5hip_pool *p, uint32_t k, const uint64_t *w, uint32_t *sel)
+{
+    const uint32_t G = p->ndev;
+    const uint32_t r0 = __atomic_fetch_add(&p->rr, 1, __ATOMIC_RELAXED);
+    uint64_t load[POOL_MAX_DEV];
+    int used[POOL_MAX_DEV] = {0};
+    for (uint32_t g = 0; g < G; g++) load[g] = dev_load(p, g);
+    for (uint32_t j = 0; j < k; j++) {
+        uint32_t best = G;
+        for (uint32_t q = 0; q < G; q++) {
+            const uint32_t g = (r0 + q) % G;
+            if (!used[g] && (best == G || load[g] < load[best])) best = g;
+        }
+        used[best] = 1;
+        sel[j] = best;
+        __atomic_fetch_add(&p->claim[best], w[j], __ATOMIC_RELAXED);
+    }
+}
+
+static void unclaim(md5hip_pool *p, uint32_t g, uint64_t w)
+{
+    __atomic_fetch_sub(&p->claim[g], w, __ATOMIC_RELAXED);
+}
+
+/* ------------------------------------------------------------------------
+ * Split-ticket table (p->mu held)
+ * ------------------------------------------------------------------------ */
+static void failed_add(md5hip_pool *p, uint64_t id, int err)
+{
+    if (p->nfailed == p->capfailed) {
+        if (p->capfailed >= FAILED_MAX) {                 /* keep the newest half */
+            const uint64_t keep = p->nfailed / 2;
+            memmove(p->failed_id, p->failed_id + p->nfailed - keep, keep * sizeof *p->failed_id);
+            memmove(p->failed_err, p->failed_err + p->nfailed - keep, keep * sizeof *p->failed_err);
+            p->nfailed = keep;
+        } else {
+            const uint64_t nc = p->capfailed ? 2 * p->capfailed : 64;
+            uint64_t *fi = realloc(p->failed_id, nc * sizeof *fi);
+            if (fi) p->failed_id = fi;
+            int *fe = realloc(p->failed_err, nc * sizeof *fe);
+            if (fe) p->failed_err = fe;
+            if (!fi || !fe) return;
+            p->capfailed = nc;
+        }
+    }
+    p->failed_id[p->nfailed] = id;
+    p->failed_err[p->nfailed] = err;
+    p->nfailed++;
+}
+
+static int failed_find(const md5hip_pool *p, uint64_t id)
+{
+    uint64_t a = 0, z = p->nfailed;
+    while (a < z) {
+        const uint64_t mid = (a + z) / 2;
+        if (p->failed_id[mid] < id) a = mid + 1;
+        else z = mid;
+    }
+    return a < p->nfailed && p->failed_id[a] == id ? p->failed_err[a] : 0;
+}
+
+/* 1 = every part done (*err = the first part error), 0 = running */
+static int mt_state(md5hip_pool *p, const struct mt_entry *e, int *err)
+{
+    *err = 0;
+    for (uint32_t j = 0; j < e->nparts; j++) {
+        int pe = 0;
+        const int s = md5hip_batcher_ticket_state(p->b[e->part[j].dev], e->part[j].t, &pe);
+        if (s < 0) pe = s;
+        else if (s == 0) return 0;
+        if (pe && !*err) *err = pe;
+    }
+    return 1;
+}
+
+/* Drop completed entries from the low end (they are looked up by failed_find
+ * from then on). */
+static void mt_reap(md5hip_pool *p)
+{
+    while (p->mt_n) {
+        struct mt_entry *e = p->mt[p->mt_lo % p->mt_cap];
+        int err;
+        if (!mt_state(p, e, &err)) break;
+        if (err) failed_add(p, e->id, err);
+        free(e);
+        p->mt_lo++;
+        p->mt_n--;
+    }
+}
+
+static int mt_push(md5hip_pool *p, struct mt_entry *e)
+{
+    if (p->mt_n == p->mt_cap) {
+        const uint64_t nc = p->mt_cap ? 2 * p->mt_cap : 64;
+        struct mt_entry **m = malloc(nc * sizeof *m);
+        if (!m) return -ENOMEM;
+        for (uint64_t k = 0; k < p->mt_n; k++) m[k] = p->mt[(p->mt_lo + k) % p->mt_cap];
+        free(p->mt);
+        p->mt = m;
+        p->mt_cap = nc;
+        p->mt_lo = 0;
+    }
+    p->mt[(p->mt_lo + p->mt_n) % p->mt_cap] = e;
+    p->mt_n++;
+    return 0;
+}
+
+/* the live entry with this id, or NULL (completed and dropped, or unknown) */
+static struct mt_entry *mt_find(md5hip_pool *p, uint64_t id)
+{
+    uint64_t a = 0, z = p->mt_n;
+    while (a < z) {
+        const uint64_t mid = (a + z) / 2;
+        if (p->mt[(p->mt_lo + mid) % p->mt_cap]->id < id) a = mid + 1;
+        else z = mid;
+    }
+    if (a < p->mt_n) {
+        struct mt_entry *e = p->mt[(p->mt_lo + a) % p->mt_cap];
+        if (e->id == id) return e;
     }
     return NULL;
 }
 
-/* Run jobs[0..G) -- job 0 on the calling thread, the rest on their own. */
-static int run_jobs(struct job *jobs, uint32_t G)
+/* ------------------------------------------------------------------------
+ * Submission
+ * ------------------------------------------------------------------------ */
+enum src_kind { SRC_PTRS, SRC_IOV, SRC_FIXED };
+struct pool_src {
+    enum src_kind kind;
+    const void *const *ptrs;             /* SRC_PTRS */
+    const uint32_t *lens;
+    const struct md5hip_iov *segs;       /* SRC_IOV */
+    const uint64_t *seg_first;
+    const unsigned char *h_base;         /* SRC_FIXED */
+    uint32_t len;
+    uint64_t stride;
+};
+
+/* chunks [lo, hi) of `s` to device g's batcher */
+static int part_submit(md5hip_pool *p, uint32_t g, int kind, uint32_t fastcrc,
+                       const struct pool_src *s, uint64_t lo, uint64_t hi, unsigned char *digests,
+                       uint64_t *ticket)
 {
-    pthread_t th[POOL_MAX_DEV];
-    int started[POOL_MAX_DEV] = {0};
-    for (uint32_t g = 1; g < G; g++) {
-        if (jobs[g].hi == jobs[g].lo) { jobs[g].rc = 0; continue; }
-        if (pthread_create(&th[g], NULL, job_run, &jobs[g]) == 0) started[g] = 1;
-        else job_run(&jobs[g]);          /* no thread: run it inline */
+    const uint64_t m = hi - lo;
+    switch (s->kind) {
+    case SRC_PTRS:
+        return md5hip_submit_as(p->b[g], kind, fastcrc, s->ptrs + lo, s->lens + lo, NULL, NULL, m,
+                                digests, ticket);
+    case SRC_IOV: {
+        /* the batcher reads seg_first[0..m] re-based to 0; it has taken the
+         * chunks when the call returns, so a temporary copy will do */
+        uint64_t local[65];
+        uint64_t *sf = m + 1 <= 65 ? local : malloc(8 * (m + 1));
+        if (!sf) return -ENOMEM;
+        for (uint64_t i = 0; i <= m; i++) sf[i] = s->seg_first[lo + i] - s->seg_first[lo];
+        const int rc = md5hip_submit_as(p->b[g], kind, fastcrc, NULL, NULL, s->segs + s->seg_first[lo],
+                                        sf, m, digests, ticket);
+        if (sf != local) free(sf);
+        return rc;
     }
-    job_run(&jobs[0]);
-    int rc = 0;
-    for (uint32_t g = 0; g < G; g++) {
-        if (g && started[g]) pthread_join(th[g], NULL);
-        if (rc == 0 && jobs[g].rc) rc = jobs[g].rc;
+    case SRC_FIXED:
+        return md5hip_host_fixed_as(p->b[g], kind, fastcrc, s->h_base + lo * s->stride, m, s->len,
+                                    s->stride, digests, ticket);
+    }
+    return -EINVAL;
+}
+
+static uint64_t src_weight(const struct pool_src *s, uint64_t i)
+{
+    if (s->kind == SRC_PTRS) return chunk_weight(s->lens[i]);
+    if (s->kind == SRC_FIXED) return chunk_weight(s->len);
+    uint64_t L = 0;
+    for (uint64_t j = s->seg_first[i]; j < s->seg_first[i + 1]; j++) L += s->segs[j].len;
+    return chunk_weight(L);
+}
+
+/* ticket NULL = synchronous; kind < 0 = the pool's current digest kind */
+static int pool_submit(md5hip_pool *p, const struct pool_src *s, uint64_t n, unsigned char *digests,
+                       uint64_t *ticket, int kind, uint32_t fastcrc)
+{
+    if (ticket) *ticket = 0;
+    if (n == 0) return 0;
+    pthread_mutex_lock(&p->mu);
+    if (kind < 0) {
+        kind = p->kind;
+        fastcrc = p->fastcrc;
+    }
+    uint64_t split = p->split_bytes;
+    p->st.submissions++;
+    pthread_mutex_unlock(&p->mu);
+    if (split == 0) split = md5hip_batcher_slice(p->b[0]);
+    const uint32_t dsz = kind == MD5HIP_DIGEST_CRC32 ? 4 : 16;
+    uint64_t total = 0;
+    if (s->kind == SRC_FIXED) {
+        total = n * chunk_weight(s->len);
+    } else {
+        for (uint64_t i = 0; i < n; i++) total += src_weight(s, i);
+    }
+    uint32_t k = 1;
+    if (total > split && p->ndev > 1) {
+        const uint64_t want = (total + split - 1) / split;
+        k = want < p->ndev ? (uint32_t)want : p->ndev;
+        if (k > n) k = (uint32_t)n;
+    }
+    if (k == 1) {                                     /* the common case: whole */
+        uint32_t g;
+        route(p, 1, &total, &g);
+        /* asynchronous even for a synchronous caller, so the claim ends as
+         * soon as the batcher holds the chunks (its own load counts them) */
+        uint64_t t = 0;
+        int rc = part_submit(p, g, kind, fastcrc, s, 0, n, digests, &t);
+        unclaim(p, g, total);
+        pthread_mutex_lock(&p->mu);
+        p->st.routed_whole++;
+        p->st.parts++;
+        pthread_mutex_unlock(&p->mu);
+        if (rc == 0 && !ticket) rc = md5_batch_wait(p->b[g], t);
+        if (ticket && rc == 0 && t) *ticket = (t << 6) | g;
+        return rc;
+    }
+    /* split: contiguous byte-balanced ranges over the k least-loaded devices */
+    uint64_t first[POOL_MAX_DEV + 1], w[POOL_MAX_DEV];
+    if (s->kind == SRC_FIXED) {
+        md5hip_pool_plan(NULL, n, k, first);
+    } else {
+        uint32_t *lens = malloc(4 * n);
+        if (!lens) return -ENOMEM;
+        for (uint64_t i = 0; i < n; i++) {
+            const uint64_t L = src_weight(s, i) - 64;
+            lens[i] = L > 0xffffffffull ? 0xffffffffu : (uint32_t)L;   /* the batcher rejects it */
+        }
+        md5hip_pool_plan(lens, n, k, first);
+        free(lens);
+    }
+    for (uint32_t j = 0; j < k; j++) {
+        w[j] = 0;
+        if (s->kind == SRC_FIXED) w[j] = (first[j + 1] - first[j]) * chunk_weight(s->len);
+        else for (uint64_t i = first[j]; i < first[j + 1]; i++) w[j] += src_weight(s, i);
+    }
+    uint32_t sel[POOL_MAX_DEV];
+    route(p, k, w, sel);
+    struct mt_entry *e = malloc(sizeof *e + k * sizeof(struct mt_part));
+    int rc = e ? 0 : -ENOMEM;
+    uint32_t np = 0;
+    for (uint32_t j = 0; j < k; j++) {
+        if (rc == 0 && first[j + 1] > first[j]) {
+            uint64_t t = 0;
+            rc = part_submit(p, sel[j], kind, fastcrc, s, first[j], first[j + 1],
+                             digests + (size_t)dsz * first[j], &t);
+            if (rc == 0 && t) e->part[np++] = (struct mt_part){sel[j], t};
+        }
+        unclaim(p, sel[j], w[j]);
+    }
+    pthread_mutex_lock(&p->mu);
+    p->st.split++;
+    p->st.parts += np;
+    pthread_mutex_unlock(&p->mu);
+    if (!e) return rc;
+    e->nparts = np;
+    if (rc || !ticket) {
+        /* synchronous, or a part failed: the submitted parts finish before
+         * the caller may reuse its buffers */
+        for (uint32_t j = 0; j < np; j++) {
+            const int r = md5_batch_wait(p->b[e->part[j].dev], e->part[j].t);
+            if (r && !rc) rc = r;
+        }
+        free(e);
+        return rc;
+    }
+    pthread_mutex_lock(&p->mu);
+    mt_reap(p);
+    e->id = p->mt_next++;
+    rc = mt_push(p, e);
+    if (rc == 0) *ticket = MT_BIT | e->id;
+    pthread_mutex_unlock(&p->mu);
+    if (rc) {                                         /* no table space: finish it here */
+        for (uint32_t j = 0; j < np; j++) (void)md5_batch_wait(p->b[e->part[j].dev], e->part[j].t);
+        free(e);
     }
     return rc;
 }
 
-static void jobs_init(md5hip_pool *p, struct job *jobs, enum job_kind kind, const uint64_t *first,
-                      unsigned char *digests)
+/* wait (block = 1) or poll (block = 0) on a pool ticket: 1 done / 0 running
+ * and *err its error, or -EINVAL */
+static int pool_ticket(md5hip_pool *p, uint64_t ticket, int block, int *err)
 {
-    for (uint32_t g = 0; g < p->ndev; g++) {
-        memset(&jobs[g], 0, sizeof jobs[g]);
-        jobs[g].kind = kind;
-        jobs[g].b = p->b[g];
-        jobs[g].lo = first[g];
-        jobs[g].hi = first[g + 1];
-        jobs[g].digests = digests + (size_t)p->dsz * first[g];
+    *err = 0;
+    if (ticket == 0) return 1;
+    if (!(ticket & MT_BIT)) {
+        const uint32_t g = (uint32_t)(ticket & 63u);
+        if (g >= p->ndev) return -EINVAL;
+        const int r = block ? md5_batch_wait(p->b[g], ticket >> 6) : md5_batch_poll(p->b[g], ticket >> 6);
+        if (r == -EINVAL) return -EINVAL;
+        if (block) { *err = r; return 1; }
+        if (r < 0) { *err = r; return 1; }
+        return r;                                     /* 1 done, 0 running */
     }
+    const uint64_t id = ticket & ~MT_BIT;
+    pthread_mutex_lock(&p->mu);
+    if (id == 0 || id >= p->mt_next) {
+        pthread_mutex_unlock(&p->mu);
+        return -EINVAL;
+    }
+    struct mt_entry *e = mt_find(p, id);
+    if (!e) {                                         /* completed and dropped */
+        *err = failed_find(p, id);
+        pthread_mutex_unlock(&p->mu);
+        return 1;
+    }
+    struct mt_part parts[POOL_MAX_DEV];
+    const uint32_t np = e->nparts;
+    memcpy(parts, e->part, np * sizeof *parts);
+    pthread_mutex_unlock(&p->mu);
+    /* the batcher calls below may block: p->mu is not held */
+    int done = 1;
+    for (uint32_t j = 0; j < np; j++) {
+        const int r = block ? md5_batch_wait(p->b[parts[j].dev], parts[j].t)
+                            : md5_batch_poll(p->b[parts[j].dev], parts[j].t);
+        if (block) {
+            if (r && !*err) *err = r;
+        } else if (r < 0) {
+            if (!*err) *err = r;
+        } else if (r == 0) {
+            done = 0;                                 /* keep polling: every part is hastened */
+        }
+    }
+    if (done) {
+        pthread_mutex_lock(&p->mu);
+        mt_reap(p);
+        pthread_mutex_unlock(&p->mu);
+    }
+    return done;
+}
+
+int md5hip_pool_wait(md5hip_pool *p, uint64_t ticket)
+{
+    if (!p) return -EINVAL;
+    int err;
+    const int r = pool_ticket(p, ticket, 1, &err);
+    return r < 0 ? r : err;
+}
+
+int md5hip_pool_poll(md5hip_pool *p, uint64_t ticket)
+{
+    if (!p) return -EINVAL;
+    int err;
+    const int r = pool_ticket(p, ticket, 0, &err);
+    if (r < 0) return r;
+    return r == 1 && err ? err : r;
+}
+
+/* ------------------------------------------------------------------------
+ * Entries
+ * ------------------------------------------------------------------------ */
+static int check_ptrs(const void *const *ptrs, const uint32_t *lens, uint64_t n)
+{
+    if (!ptrs || !lens) return -EINVAL;
+    for (uint64_t i = 0; i < n; i++)
+        if (!ptrs[i] && lens[i]) return -EINVAL;
+    return 0;
+}
+
+static int check_iov(const struct md5hip_iov *segs, const uint64_t *seg_first, uint64_t n)
+{
+    if (!segs || !seg_first || seg_first[0] != 0) return -EINVAL;
+    for (uint64_t i = 0; i < n; i++) {
+        if (seg_first[i + 1] < seg_first[i]) return -EINVAL;
+        for (uint64_t j = seg_first[i]; j < seg_first[i + 1]; j++)
+            if (!segs[j].base && segs[j].len) return -EINVAL;
+    }
+    return 0;
+}
+
+int md5hip_pool_submit_async(md5hip_pool *p, const void *const *ptrs, const uint32_t *lens,
+                             uint64_t n, unsigned char *digests, uint64_t *ticket)
+{
+    if (!p || !ticket) return -EINVAL;
+    *ticket = 0;
+    if (n == 0) return 0;
+    if (!digests) return -EINVAL;
+    int rc = check_ptrs(ptrs, lens, n);
+    if (rc) return rc;
+    const struct pool_src s = {SRC_PTRS, ptrs, lens, NULL, NULL, NULL, 0, 0};
+    return pool_submit(p, &s, n, digests, ticket, -1, 0);
+}
+
+int md5hip_pool_submit_iov_async(md5hip_pool *p, const struct md5hip_iov *segs,
+                                 const uint64_t *seg_first, uint64_t n, unsigned char *digests,
+                                 uint64_t *ticket)
+{
+    if (!p || !ticket) return -EINVAL;
+    *ticket = 0;
+    if (n == 0) return 0;
+    if (!digests) return -EINVAL;
+    int rc = check_iov(segs, seg_first, n);
+    if (rc) return rc;
+    const struct pool_src s = {SRC_IOV, NULL, NULL, segs, seg_first, NULL, 0, 0};
+    return pool_submit(p, &s, n, digests, ticket, -1, 0);
 }
 
 int md5hip_pool_submit(md5hip_pool *p, const void *const *ptrs, const uint32_t *lens, uint64_t n,
@@ -184,56 +591,11 @@ int md5hip_pool_submit(md5hip_pool *p, const void *const *ptrs, const uint32_t *
 {
     if (!p) return -EINVAL;
     if (n == 0) return 0;
-    if (!ptrs || !lens || !digests) return -EINVAL;
-    for (uint64_t i = 0; i < n; i++)
-        if (!ptrs[i] && lens[i]) return -EINVAL;
-    uint64_t first[POOL_MAX_DEV + 1];
-    struct job jobs[POOL_MAX_DEV];
-    pthread_mutex_lock(&p->lock);
-    md5hip_pool_plan(lens, n, p->ndev, first);
-    jobs_init(p, jobs, JOB_PTRS, first, digests);
-    for (uint32_t g = 0; g < p->ndev; g++) { jobs[g].ptrs = ptrs; jobs[g].lens = lens; }
-    int rc = run_jobs(jobs, p->ndev);
-    pthread_mutex_unlock(&p->lock);
-    return rc;
-}
-
-/* (p->lock held) */
-static int pool_submit_iov_locked(md5hip_pool *p, const struct md5hip_iov *segs,
-                                  const uint64_t *seg_first, uint64_t n, unsigned char *digests)
-{
-    uint32_t *lens = malloc(4 * n);
-    uint64_t *rebased = malloc(8 * (n + p->ndev));
-    if (!lens || !rebased) { free(lens); free(rebased); return -ENOMEM; }
-    int rc = 0;
-    for (uint64_t i = 0; i < n && rc == 0; i++) {
-        if (seg_first[i + 1] < seg_first[i]) { rc = -EINVAL; break; }
-        uint64_t L = 0;
-        for (uint64_t s = seg_first[i]; s < seg_first[i + 1]; s++) {
-            if (!segs[s].base && segs[s].len) { rc = -EINVAL; break; }
-            L += segs[s].len;
-        }
-        lens[i] = L > 0xffffffffull ? 0xffffffffu : (uint32_t)L;   /* batcher rejects it */
-    }
-    if (rc == 0) {
-        uint64_t first[POOL_MAX_DEV + 1];
-        struct job jobs[POOL_MAX_DEV];
-        md5hip_pool_plan(lens, n, p->ndev, first);
-        jobs_init(p, jobs, JOB_IOV, first, digests);
-        /* each device sees its own seg_first[] re-based to 0 (n+G entries total) */
-        uint64_t at = 0;
-        for (uint32_t g = 0; g < p->ndev; g++) {
-            jobs[g].segs = segs;
-            jobs[g].seg_first = seg_first;
-            jobs[g].rebased = rebased + at;
-            for (uint64_t i = first[g]; i <= first[g + 1]; i++)
-                rebased[at++] = seg_first[i] - seg_first[first[g]];
-        }
-        rc = run_jobs(jobs, p->ndev);
-    }
-    free(lens);
-    free(rebased);
-    return rc;
+    if (!digests) return -EINVAL;
+    int rc = check_ptrs(ptrs, lens, n);
+    if (rc) return rc;
+    const struct pool_src s = {SRC_PTRS, ptrs, lens, NULL, NULL, NULL, 0, 0};
+    return pool_submit(p, &s, n, digests, NULL, -1, 0);
 }
 
 int md5hip_pool_submit_iov(md5hip_pool *p, const struct md5hip_iov *segs, const uint64_t *seg_first,
@@ -241,11 +603,11 @@ int md5hip_pool_submit_iov(md5hip_pool *p, const struct md5hip_iov *segs, const 
 {
     if (!p) return -EINVAL;
     if (n == 0) return 0;
-    if (!segs || !seg_first || !digests || seg_first[0] != 0) return -EINVAL;
-    pthread_mutex_lock(&p->lock);
-    const int rc = pool_submit_iov_locked(p, segs, seg_first, n, digests);
-    pthread_mutex_unlock(&p->lock);
-    return rc;
+    if (!digests) return -EINVAL;
+    int rc = check_iov(segs, seg_first, n);
+    if (rc) return rc;
+    const struct pool_src s = {SRC_IOV, NULL, NULL, segs, seg_first, NULL, 0, 0};
+    return pool_submit(p, &s, n, digests, NULL, -1, 0);
 }
 
 int md5hip_pool_host_fixed(md5hip_pool *p, const void *h_base, uint64_t n, uint32_t len,
@@ -254,19 +616,8 @@ int md5hip_pool_host_fixed(md5hip_pool *p, const void *h_base, uint64_t n, uint3
     if (!p) return -EINVAL;
     if (n == 0) return 0;
     if (!h_base || !digests || len > stride) return -EINVAL;
-    uint64_t first[POOL_MAX_DEV + 1];
-    struct job jobs[POOL_MAX_DEV];
-    pthread_mutex_lock(&p->lock);
-    md5hip_pool_plan(NULL, n, p->ndev, first);
-    jobs_init(p, jobs, JOB_FIXED, first, digests);
-    for (uint32_t g = 0; g < p->ndev; g++) {
-        jobs[g].h_base = h_base;
-        jobs[g].len = len;
-        jobs[g].stride = stride;
-    }
-    int rc = run_jobs(jobs, p->ndev);
-    pthread_mutex_unlock(&p->lock);
-    return rc;
+    const struct pool_src s = {SRC_FIXED, NULL, NULL, NULL, NULL, h_base, len, stride};
+    return pool_submit(p, &s, n, digests, NULL, -1, 0);
 }
 
 int md5hip_pool_verify_iov(md5hip_pool *p, const struct md5hip_iov *segs, const uint64_t *seg_first,
@@ -274,14 +625,19 @@ int md5hip_pool_verify_iov(md5hip_pool *p, const struct md5hip_iov *segs, const 
 {
     if (!p) return -EINVAL;
     if (n == 0) return 0;
-    if (!expected || !ok || !segs || !seg_first || seg_first[0] != 0) return -EINVAL;
-    /* the digest size is read and used under one hold of the pool lock, so a
-     * concurrent md5hip_pool_set_digest cannot change it in between */
-    pthread_mutex_lock(&p->lock);
-    const uint32_t dsz = p->dsz;
+    if (!expected || !ok) return -EINVAL;
+    int rc = check_iov(segs, seg_first, n);
+    if (rc) return rc;
+    /* one snapshot of the kind for the digest size and the submission */
+    pthread_mutex_lock(&p->mu);
+    const int kind = p->kind;
+    const uint32_t fastcrc = p->fastcrc;
+    pthread_mutex_unlock(&p->mu);
+    const uint32_t dsz = kind == MD5HIP_DIGEST_CRC32 ? 4 : 16;
     unsigned char *got = malloc((size_t)dsz * n);
-    int rc = got ? pool_submit_iov_locked(p, segs, seg_first, n, got) : -ENOMEM;
-    pthread_mutex_unlock(&p->lock);
+    if (!got) return -ENOMEM;
+    const struct pool_src s = {SRC_IOV, NULL, NULL, segs, seg_first, NULL, 0, 0};
+    rc = pool_submit(p, &s, n, got, NULL, kind, fastcrc);
     if (rc == 0) {
         const unsigned char *e = expected;
         for (uint64_t i = 0; i < n; i++) {

@@ -207,6 +207,7 @@ struct slot {
     uint32_t *hh, hkmax, *h_bkt, *d_bkt;
     int hovf;
     uint64_t opened_us, launched_us;  /* first chunk reserved / went in flight */
+    uint64_t load;                    /* this slot's share of b->load_bytes */
 };
 
 struct md5hip_batcher {
@@ -226,6 +227,8 @@ struct md5hip_batcher {
     int open;          /* index of the OPEN slot new chunks go to, -1 = none */
     uint32_t inflight;
     struct tk_ring tk; /* tickets: live ids, their references and errors (md5_tickets.h) */
+    uint64_t load_bytes;      /* weight (len + 64 per chunk) reserved and not yet retired:
+                                 read without the lock by md5hip_batcher_load (the pool's router) */
     struct md5hip_batcher_stats st;
     pthread_mutex_t mu;
     pthread_cond_t done_cv;   /* a slot retired / a ticket completed */
@@ -233,6 +236,7 @@ struct md5hip_batcher {
     pthread_t progress;
     int progress_started, stop;
     int waiters;              /* threads blocked on a ticket: poll the launches fast */
+    hipEvent_t after_ev;      /* recorded on a producer's stream (md5_batch_submit_device_on) */
 };
 
 #define CK(x) do { if ((x) != hipSuccess) { rc = -ENODEV; goto fail; } } while (0)
@@ -422,6 +426,7 @@ static void slot_reset(struct slot *sl)
     sl->nsegs = 0;
     sl->tickets_in = 0;
     sl->copied_n = sl->planned_n = sl->seen_n = 0;
+    sl->load = 0;
     if (sl->hh) memset(sl->hh, 0, sizeof(uint32_t) * ((size_t)sl->hkmax + 1));
     sl->hkmax = 0;
     sl->hovf = 0;
@@ -436,6 +441,8 @@ static void slot_retire(md5hip_batcher *b, struct slot *sl, int err)
             memcpy(g->user, sl->h_dig + (size_t)sl->dsz * g->first, (size_t)sl->dsz * g->count);
         tk_put(b, g->ticket, err);
     }
+    __atomic_store_n(&b->load_bytes, b->load_bytes - sl->load, __ATOMIC_RELAXED);
+    sl->load = 0;
     if (sl->state == SLOT_INFLIGHT) {
         b->inflight--;
         const double d = (double)(now_us() - sl->launched_us);
@@ -609,6 +616,7 @@ static void batcher_free(md5hip_batcher *b)
         hipHostFree(sl->h_bkt); hipFree(sl->d_bkt);
     }
     free(b->s);
+    if (b->after_ev) hipEventDestroy(b->after_ev);
     tk_ring_free(&b->tk);
     pthread_mutex_destroy(&b->mu);
     pthread_cond_destroy(&b->done_cv);
@@ -670,6 +678,7 @@ static int batcher_new(int device, uint64_t slice_bytes, uint32_t nslots, uint64
     b->s = calloc(nslots, sizeof *b->s);
     /* ticket 0 = "nothing": complete at once */
     if (!b->s || tk_ring_init(&b->tk, 1)) { rc = -ENOMEM; goto fail; }
+    CK(hipEventCreateWithFlags(&b->after_ev, hipEventDisableTiming));
     for (uint32_t k = 0; k < nslots; k++) {
         struct slot *sl = &b->s[k];
         CK(hipStreamCreateWithFlags(&sl->stream, hipStreamNonBlocking));
@@ -1011,6 +1020,8 @@ static long reserve(md5hip_batcher *b, struct slot *sl, const struct chunk_src *
             sl->used += sz;
         }
         sl->h_len[sl->n] = (uint32_t)L;
+        sl->load += L + 64;
+        __atomic_store_n(&b->load_bytes, b->load_bytes + L + 64, __ATOMIC_RELAXED);
         {
             const uint64_t k = (L >> 6) + 1;
             if (k > MD5HIP_HIST_KMAX) {
@@ -1030,8 +1041,12 @@ static long reserve(md5hip_batcher *b, struct slot *sl, const struct chunk_src *
 
 /* The submission engine.  kind < 0: the batcher's current digest kind;
  * else this submission's own (it never changes the batcher's setting). */
+/* after != NULL: the producer's stream -- every slot taking chunks of this
+ * submission waits on the producer's work enqueued so far before its kernel
+ * (an event recorded on `after`, waited on by the slot's stream). */
 static int submit(md5hip_batcher *b, const struct chunk_src *src, uint64_t n, unsigned char *digests,
-                  int on_device, int async, uint64_t *ticket, int kind, uint32_t fastcrc)
+                  int on_device, int async, uint64_t *ticket, int kind, uint32_t fastcrc,
+                  hipStream_t after)
 {
     for (uint64_t i = 0; i < n; i++) {
         const uint64_t L = src_len(src, i);
@@ -1056,6 +1071,10 @@ static int submit(md5hip_batcher *b, const struct chunk_src *src, uint64_t n, un
         fastcrc = b->fastcrc;
     }
     rc = tk_new(b, &t);
+    if (rc == 0 && after && hipEventRecord(b->after_ev, after) != hipSuccess) {
+        tk_put(b, t, 0);
+        rc = -EINVAL;                              /* not a stream of this device */
+    }
     if (rc) {
         pthread_mutex_unlock(&b->mu);
         dev_leave(&g);
@@ -1078,6 +1097,13 @@ static int submit(md5hip_batcher *b, const struct chunk_src *src, uint64_t n, un
         }
         const uint64_t m = (uint64_t)got;
         const uint64_t hi = sl->used;
+        /* recorded and waited on under one hold of b->mu (slot_take may have
+         * let another producer record the event meanwhile), before this
+         * slot's kernel can be enqueued: the kernel runs after the producer's
+         * work enqueued up to here */
+        if (after && (hipEventRecord(b->after_ev, after) != hipSuccess ||
+                      hipStreamWaitEvent(sl->stream, b->after_ev, 0) != hipSuccess) && !sl->err)
+            sl->err = -EIO;
         if ((rc = seg_push(sl, (struct seg){t, at, m, digests + (size_t)dsz * i, on_device}))) {
             sl->err = rc;                    /* its reserved chunks have no segment */
             break;
@@ -1213,7 +1239,7 @@ int md5_batch_submit(md5hip_batcher *b, const void *const *ptrs, const uint32_t 
     int rc = check_ptrs(ptrs, lens, n);
     if (rc) return rc;
     const struct chunk_src src = {ptrs, lens, NULL, NULL, NULL};
-    return submit(b, &src, n, digests, 0, 0, NULL, -1, 0);
+    return submit(b, &src, n, digests, 0, 0, NULL, -1, 0, NULL);
 }
 
 int md5_batch_submit_async(md5hip_batcher *b, const void *const *ptrs, const uint32_t *lens,
@@ -1226,7 +1252,7 @@ int md5_batch_submit_async(md5hip_batcher *b, const void *const *ptrs, const uin
     int rc = check_ptrs(ptrs, lens, n);
     if (rc) return rc;
     const struct chunk_src src = {ptrs, lens, NULL, NULL, NULL};
-    return submit(b, &src, n, digests, 0, 1, ticket, -1, 0);
+    return submit(b, &src, n, digests, 0, 1, ticket, -1, 0, NULL);
 }
 
 int md5_batch_submit_iov(md5hip_batcher *b, const struct md5hip_iov *segs,
@@ -1238,7 +1264,7 @@ int md5_batch_submit_iov(md5hip_batcher *b, const struct md5hip_iov *segs,
     int rc = check_iov(segs, seg_first, n);
     if (rc) return rc;
     const struct chunk_src src = {NULL, NULL, segs, seg_first, NULL};
-    return submit(b, &src, n, digests, 0, 0, NULL, -1, 0);
+    return submit(b, &src, n, digests, 0, 0, NULL, -1, 0, NULL);
 }
 
 int md5_batch_submit_iov_async(md5hip_batcher *b, const struct md5hip_iov *segs,
@@ -1252,7 +1278,7 @@ int md5_batch_submit_iov_async(md5hip_batcher *b, const struct md5hip_iov *segs,
     int rc = check_iov(segs, seg_first, n);
     if (rc) return rc;
     const struct chunk_src src = {NULL, NULL, segs, seg_first, NULL};
-    return submit(b, &src, n, digests, 0, 1, ticket, -1, 0);
+    return submit(b, &src, n, digests, 0, 1, ticket, -1, 0, NULL);
 }
 
 int md5_batch_submit_device_async(md5hip_batcher *b, const uint64_t *d_ptrs, const uint32_t *lens,
@@ -1266,7 +1292,7 @@ int md5_batch_submit_device_async(md5hip_batcher *b, const uint64_t *d_ptrs, con
     for (uint64_t i = 0; i < n; i++)
         if (!d_ptrs[i] && lens[i]) return -EINVAL;
     const struct chunk_src src = {NULL, lens, NULL, NULL, d_ptrs};
-    return submit(b, &src, n, digests, digests_on_device != 0, 1, ticket, -1, 0);
+    return submit(b, &src, n, digests, digests_on_device != 0, 1, ticket, -1, 0, NULL);
 }
 
 int md5_batch_submit_device(md5hip_batcher *b, const uint64_t *d_ptrs, const uint32_t *lens,
@@ -1278,15 +1304,14 @@ int md5_batch_submit_device(md5hip_batcher *b, const uint64_t *d_ptrs, const uin
     for (uint64_t i = 0; i < n; i++)
         if (!d_ptrs[i] && lens[i]) return -EINVAL;
     const struct chunk_src src = {NULL, lens, NULL, NULL, d_ptrs};
-    return submit(b, &src, n, digests, digests_on_device != 0, 0, NULL, -1, 0);
+    return submit(b, &src, n, digests, digests_on_device != 0, 0, NULL, -1, 0, NULL);
 }
 
-int md5hip_batch_host_fixed(md5hip_batcher *b, const void *h_base, uint64_t n, uint32_t len,
-                            uint64_t stride, unsigned char *digests)
+/* Fixed-length chunks straight from one contiguous host range (MODE_FIXED:
+ * one H2D copy per slot, no host gather).  ticket NULL = synchronous. */
+static int host_fixed(md5hip_batcher *b, int kind, uint32_t fastcrc, const void *h_base, uint64_t n,
+                      uint32_t len, uint64_t stride, unsigned char *digests, uint64_t *ticket)
 {
-    if (!b) return -EINVAL;
-    if (n == 0) return 0;
-    if (!h_base || !digests || len > stride) return -EINVAL;
     if (stride > b->cap) return -E2BIG;
     struct dev_guard g;
     if (dev_enter(&g, b->device)) return -ENODEV;
@@ -1294,6 +1319,11 @@ int md5hip_batch_host_fixed(md5hip_batcher *b, const void *h_base, uint64_t n, u
     uint64_t per = b->cap / stride;
     if (per > b->maxn) per = b->maxn;
     pthread_mutex_lock(&b->mu);
+    if (kind < 0) {
+        kind = b->kind;
+        fastcrc = b->fastcrc;
+    }
+    const uint32_t dsz = kind == MD5HIP_DIGEST_CRC32 ? 4 : 16;
     uint64_t t = 0;
     int rc = tk_new(b, &t);
     if (rc) {
@@ -1306,14 +1336,16 @@ int md5hip_batch_host_fixed(md5hip_batcher *b, const void *h_base, uint64_t n, u
         const uint64_t m = n - i < per ? n - i : per;
         /* straight from the caller's (ideally pinned) buffer: no host gather,
          * a slot of its own (the open slot keeps coalescing other work) */
-        struct slot *sl = slot_take(b, MODE_FIXED, b->kind, b->fastcrc);
+        struct slot *sl = slot_take(b, MODE_FIXED, kind, fastcrc);
         sl->n = m;
         sl->fx_src = src + i * stride;
         sl->fx_bytes = (m - 1) * stride + len;
         sl->fx_len = len;
         sl->fx_stride = stride;
         sl->full = 1;
-        if ((rc = seg_push(sl, (struct seg){t, 0, m, digests + (size_t)b->dsz * i, 0}))) {
+        sl->load = m * ((uint64_t)len + 64);
+        __atomic_store_n(&b->load_bytes, b->load_bytes + sl->load, __ATOMIC_RELAXED);
+        if ((rc = seg_push(sl, (struct seg){t, 0, m, digests + (size_t)dsz * i, 0}))) {
             slot_retire(b, sl, rc);
             break;
         }
@@ -1321,14 +1353,87 @@ int md5hip_batch_host_fixed(md5hip_batcher *b, const void *h_base, uint64_t n, u
         slot_try_launch(b, sl);
     }
     tk_put(b, t, rc);
-    int err = 0;
-    b->waiters++;
-    pthread_cond_broadcast(&b->work_cv);
-    while (!tk_done(b, t, &err)) pthread_cond_wait(&b->done_cv, &b->mu);
-    b->waiters--;
-    if (!rc) rc = err;
+    if (ticket) *ticket = t;
+    if (!ticket || rc) {
+        int err = 0;
+        b->waiters++;
+        pthread_cond_broadcast(&b->work_cv);
+        while (!tk_done(b, t, &err)) pthread_cond_wait(&b->done_cv, &b->mu);
+        b->waiters--;
+        if (!rc) rc = err;
+    }
     pthread_mutex_unlock(&b->mu);
     dev_leave(&g);
+    return rc;
+}
+
+int md5_batch_submit_device_on(md5hip_batcher *b, const uint64_t *d_ptrs, const uint32_t *lens,
+                               uint64_t n, unsigned char *digests, int digests_on_device,
+                               void *producer_stream, uint64_t *ticket)
+{
+    if (ticket) *ticket = 0;
+    if (!b) return -EINVAL;
+    if (n == 0) return 0;
+    if (!d_ptrs || !lens || !digests) return -EINVAL;
+    for (uint64_t i = 0; i < n; i++)
+        if (!d_ptrs[i] && lens[i]) return -EINVAL;
+    const struct chunk_src src = {NULL, lens, NULL, NULL, d_ptrs};
+    return submit(b, &src, n, digests, digests_on_device != 0, ticket != NULL, ticket, -1, 0,
+                  (hipStream_t)producer_stream);
+}
+
+int md5hip_batch_host_fixed(md5hip_batcher *b, const void *h_base, uint64_t n, uint32_t len,
+                            uint64_t stride, unsigned char *digests)
+{
+    if (!b) return -EINVAL;
+    if (n == 0) return 0;
+    if (!h_base || !digests || len > stride) return -EINVAL;
+    return host_fixed(b, -1, 0, h_base, n, len, stride, digests, NULL);
+}
+
+/* ------------------------------------------------------------------------
+ * Entries for the multi-GPU pool (md5_internal.h)
+ * ------------------------------------------------------------------------ */
+uint64_t md5hip_batcher_load(const md5hip_batcher *b)
+{
+    return __atomic_load_n(&b->load_bytes, __ATOMIC_RELAXED);
+}
+
+uint64_t md5hip_batcher_slice(const md5hip_batcher *b) { return b->cap; }
+
+int md5hip_submit_as(md5hip_batcher *b, int kind, uint32_t fastcrc, const void *const *ptrs,
+                     const uint32_t *lens, const struct md5hip_iov *segs, const uint64_t *seg_first,
+                     uint64_t n, unsigned char *digests, uint64_t *ticket)
+{
+    if (ticket) *ticket = 0;
+    if (!b) return -EINVAL;
+    if (n == 0) return 0;
+    if (!digests) return -EINVAL;
+    int rc = ptrs ? check_ptrs(ptrs, lens, n) : check_iov(segs, seg_first, n);
+    if (rc) return rc;
+    const struct chunk_src src = {ptrs, ptrs ? lens : NULL, ptrs ? NULL : segs, ptrs ? NULL : seg_first,
+                                  NULL};
+    return submit(b, &src, n, digests, 0, ticket != NULL, ticket, kind, fastcrc, NULL);
+}
+
+int md5hip_host_fixed_as(md5hip_batcher *b, int kind, uint32_t fastcrc, const void *h_base,
+                         uint64_t n, uint32_t len, uint64_t stride, unsigned char *digests,
+                         uint64_t *ticket)
+{
+    if (ticket) *ticket = 0;
+    if (!b) return -EINVAL;
+    if (n == 0) return 0;
+    if (!h_base || !digests || len > stride) return -EINVAL;
+    return host_fixed(b, kind, fastcrc, h_base, n, len, stride, digests, ticket);
+}
+
+int md5hip_batcher_ticket_state(md5hip_batcher *b, uint64_t ticket, int *err)
+{
+    *err = 0;
+    if (ticket == 0) return 1;
+    pthread_mutex_lock(&b->mu);
+    int rc = ticket >= b->tk.hi ? -EINVAL : tk_done(b, ticket, err);
+    pthread_mutex_unlock(&b->mu);
     return rc;
 }
 
@@ -1354,7 +1459,7 @@ int md5hip_verify_iov_as(md5hip_batcher *b, int kind, uint32_t fastcrc,
     unsigned char *got = malloc((size_t)dsz * n);
     if (!got) return -ENOMEM;
     const struct chunk_src src = {NULL, NULL, segs, seg_first, NULL};
-    rc = submit(b, &src, n, got, 0, 0, NULL, kind, fastcrc);
+    rc = submit(b, &src, n, got, 0, 0, NULL, kind, fastcrc, NULL);
     if (rc == 0) {
         const unsigned char *e = (const unsigned char *)expected;
         for (uint64_t i = 0; i < n; i++) {

@@ -19,7 +19,7 @@ import ctypes
 
 import numpy as np
 
-from ._lib import MD5Context, MD5HipBatcherStats, MD5HipError, MD5HipIov, check, lib
+from ._lib import MD5Context, MD5HipBatcherStats, MD5HipError, MD5HipIov, MD5HipPoolStats, check, lib
 
 try:
     import torch
@@ -335,7 +335,8 @@ class Batcher:
                submit_async="md5_batch_submit_async", submit_iov_async="md5_batch_submit_iov_async",
                wait="md5_batch_wait", poll="md5_batch_poll", flush="md5_batch_flush",
                submit_device_async="md5_batch_submit_device_async",
-               submit_device="md5_batch_submit_device", set_inflight="md5hip_batcher_set_inflight",
+               submit_device="md5_batch_submit_device", submit_device_on="md5_batch_submit_device_on",
+               set_inflight="md5hip_batcher_set_inflight",
                set_linger="md5hip_batcher_set_linger", stats="md5hip_batcher_get_stats")
 
     def __init__(self, device: int = 0, slice_bytes: int = 0, nslots: int = 0,
@@ -345,6 +346,7 @@ class Batcher:
         check("md5hip_batcher_create", lib().md5hip_batcher_create(device, slice_bytes, nslots,
                                                                     ctypes.byref(h)))
         self._h = h
+        self.device = device
         self.set_digest(kind, fastcrc)
 
     def _call(self, op, *args):
@@ -468,36 +470,62 @@ class Batcher:
                           ctypes.byref(t)))
         return Batcher.Pending(self, t.value, out, n, (keep, arr, fa))
 
-    @staticmethod
-    def _dev_args(ptrs, lens, out):
+    def _dev_args(self, ptrs, lens, out):
+        """(ptrs, lens, digest destination, on_device) for the device-input
+        entries; `out` is a device tensor on the batcher's device (digests
+        stay there), a C-contiguous uint8 numpy array, or None (a new host
+        array).  Either must hold n digests of this batcher's kind."""
         P = np.ascontiguousarray(ptrs, dtype=np.uint64)
         L = np.ascontiguousarray(lens, dtype=np.uint32)
         if P.size != L.size:
             raise ValueError("ptrs and lens differ in length")
+        need = P.size * self.dsz
         if torch is not None and isinstance(out, torch.Tensor):
-            if not out.is_cuda or not out.is_contiguous() or out.numel() * out.element_size() < P.size * 16:
-                raise ValueError("out must be a contiguous device tensor of >= n x 16 bytes")
-            return P, L, out.data_ptr(), 1
+            if not out.is_cuda or not out.is_contiguous() or out.numel() * out.element_size() < need:
+                raise ValueError(f"out must be a contiguous device tensor of >= n x {self.dsz} bytes")
+            if out.device.index != self.device:
+                raise ValueError(f"out is on cuda:{out.device.index}, the batcher on cuda:{self.device}")
+            return P, L, out, 1
         if out is None:
-            out = np.empty((max(P.size, 1), 16), dtype=np.uint8)
+            out = self._out(P.size)
+        elif not (isinstance(out, np.ndarray) and out.dtype == np.uint8 and out.flags.c_contiguous
+                  and out.nbytes >= need):
+            raise ValueError(f"out must be a C-contiguous uint8 array of >= n x {self.dsz} bytes")
         return P, L, out, 0
 
-    def submit_device_async(self, ptrs, lens, out=None) -> "Batcher.Pending":
-        """md5_batch_submit_device_async: chunk i = (device address ptrs[i],
+    def _producer(self, after):
+        """The producer stream handle for md5_batch_submit_device_on:
+        'current' = torch's current stream on the batcher's device."""
+        if isinstance(after, str):
+            if after != "current":
+                raise ValueError("after: 'current', None or a stream")
+            if torch is None:
+                return None
+            return torch.cuda.current_stream(self.device).cuda_stream
+        if after is None:
+            return None
+        return getattr(after, "cuda_stream", after)
+
+    def submit_device_async(self, ptrs, lens, out=None, after="current") -> "Batcher.Pending":
+        """md5_batch_submit_device_on: chunk i = (device address ptrs[i],
         lens[i]); digests into `out` -- a device tensor (digests stay on the
-        device) or, by default, a host array returned by .wait()."""
+        device) or, by default, a host array returned by .wait().  The kernel
+        runs after the work already enqueued on `after` (default: torch's
+        current stream -- the stream that wrote the chunks); None = no
+        ordering (the caller has synchronized)."""
         P, L, o, on_dev = self._dev_args(ptrs, lens, out)
         t = ctypes.c_uint64()
-        dst = o if on_dev else o.ctypes.data
-        check(*self._call("submit_device_async", P.ctypes.data, L.ctypes.data, P.size, dst, on_dev,
-                          ctypes.byref(t)))
-        return Batcher.Pending(self, t.value, out if on_dev else o, P.size, (P, L, out), on_dev)
+        dst = o.data_ptr() if on_dev else o.ctypes.data
+        check(*self._call("submit_device_on", P.ctypes.data, L.ctypes.data, P.size, dst, on_dev,
+                          self._producer(after), ctypes.byref(t)))
+        return Batcher.Pending(self, t.value, o, P.size, (P, L, o), on_dev)
 
-    def submit_device(self, ptrs, lens, out=None):
+    def submit_device(self, ptrs, lens, out=None, after="current"):
         P, L, o, on_dev = self._dev_args(ptrs, lens, out)
-        dst = o if on_dev else o.ctypes.data
-        check(*self._call("submit_device", P.ctypes.data, L.ctypes.data, P.size, dst, on_dev))
-        return out if on_dev else self._ret(o, P.size)
+        dst = o.data_ptr() if on_dev else o.ctypes.data
+        check(*self._call("submit_device_on", P.ctypes.data, L.ctypes.data, P.size, dst, on_dev,
+                          self._producer(after), None))
+        return o if on_dev else self._ret(o, P.size)
 
     def flush(self):
         check(*self._call("flush"))
@@ -549,6 +577,7 @@ class Queue(Batcher):
         check("md5hip_queue_create", lib().md5hip_queue_create(device, max_chunks, nslots,
                                                                 ctypes.byref(h)))
         self._h = h
+        self.device = device
         self.kind, self.dsz = self.MD5, 16
         if inflight:
             self.set_inflight(inflight)
@@ -558,14 +587,18 @@ class Queue(Batcher):
 
 
 class Pool(Batcher):
-    """Multi-GPU host pool (include/md5hip.h md5hip_pool_*): one batcher and
-    host thread per listed device, contiguous byte-balanced chunk ranges, no
-    collective.  Same methods and results as Batcher."""
+    """Multi-GPU host pool (include/md5hip.h md5hip_pool_*): a router over one
+    coalescing batcher per listed device.  A submission goes whole to the
+    least-loaded device; only one heavier than the split threshold is cut
+    over devices.  No collective.  Same methods and results as
+    Batcher, including the asynchronous forms and their tickets."""
 
     _fn = dict(set_digest="md5hip_pool_set_digest", set_gather="md5hip_pool_set_gather",
                destroy="md5hip_pool_destroy",
                submit="md5hip_pool_submit", submit_iov="md5hip_pool_submit_iov",
-               verify_iov="md5hip_pool_verify_iov", host_fixed="md5hip_pool_host_fixed")
+               verify_iov="md5hip_pool_verify_iov", host_fixed="md5hip_pool_host_fixed",
+               submit_async="md5hip_pool_submit_async", submit_iov_async="md5hip_pool_submit_iov_async",
+               wait="md5hip_pool_wait", poll="md5hip_pool_poll", set_split="md5hip_pool_set_split")
 
     def __init__(self, devices=(0,), slice_bytes: int = 0, nslots: int = 0,
                  kind: int = 0, fastcrc: int = 0):
@@ -574,11 +607,33 @@ class Pool(Batcher):
         check("md5hip_pool_create", lib().md5hip_pool_create(devs, len(devices), slice_bytes,
                                                               nslots, ctypes.byref(h)))
         self._h = h
+        self.devices = tuple(devices)
         self.set_digest(kind, fastcrc)
 
     @property
     def ndev(self) -> int:
         return lib().md5hip_pool_ndev(self._h)
+
+    def set_split(self, nbytes: int):
+        """Submissions heavier than `nbytes` are cut over devices (0 = one slice)."""
+        check(*self._call("set_split", nbytes))
+
+    def stats(self) -> dict:
+        """Routing counters: submissions, routed_whole, split, parts."""
+        st = MD5HipPoolStats()
+        check("md5hip_pool_get_stats", lib().md5hip_pool_get_stats(self._h, ctypes.byref(st)))
+        return {n: int(getattr(st, n)) for n, _ in MD5HipPoolStats._fields_}
+
+    def device_stats(self, g: int) -> dict:
+        """Device g's batcher counters (as Batcher.stats())."""
+        st = MD5HipBatcherStats()
+        check("md5hip_pool_device_stats", lib().md5hip_pool_device_stats(self._h, g, ctypes.byref(st)))
+        return {n: int(getattr(st, n)) for n, _ in MD5HipBatcherStats._fields_}
+
+    def _unsupported(self, *a, **k):
+        raise NotImplementedError("device-resident chunks belong to one device: use a Queue")
+
+    submit_device = submit_device_async = flush = set_inflight = set_linger = _unsupported
 
 
 def register_host(arr: np.ndarray):

@@ -135,6 +135,15 @@ def test_argument_errors_before_device_work():
     assert L.md5hip_arena_free(None) == EINVAL
     assert L.md5hip_arena_free(ctypes.c_void_p(1 << 30)) == -errno.ENOENT     # not an arena
     assert L.md5hip_plan_desc(None, 5, None) == EINVAL
+    # the pool router and the producer-ordered device submit (no pool / batcher)
+    assert L.md5hip_pool_submit_async(None, None, None, 1, None, ctypes.byref(t)) == EINVAL
+    assert L.md5hip_pool_submit_iov_async(None, None, None, 1, None, ctypes.byref(t)) == EINVAL
+    assert L.md5hip_pool_wait(None, 1) == EINVAL and L.md5hip_pool_poll(None, 1) == EINVAL
+    assert L.md5hip_pool_set_split(None, 1) == EINVAL
+    assert L.md5hip_pool_get_stats(None, None) == EINVAL
+    assert L.md5hip_pool_device_stats(None, 0, None) == EINVAL
+    assert L.md5hip_pool_set_digest(None, 0, 0) == EINVAL
+    assert L.md5_batch_submit_device_on(None, None, None, 1, None, 0, None, None) == EINVAL
 
 
 def test_plan_order_longest_first():

@@ -60,3 +60,19 @@ def test_dist_always_brings_up_a_one_rank_group():
     assert r.returncode == 0, r.stderr[-3000:]
     d = _line(r.stdout)
     assert d["n_gpus"] == 1 and d["ranks_seen"]["backend"] == "gloo" and d["ranks_seen"]["world"] == 1
+
+
+def test_gpus8_dry_run():
+    """The 8-rank path end to end on the CPU: spawn, 8
+    distinct ranks, 8 per-rank rates and parity samples, rank-0 aggregation,
+    and the workload named as the C4 shard the device run would hash."""
+    r = _run(["--gpus", "8", "--dist-backend", "gloo", "--dry-run", "--steps", "1", "--warmup", "0",
+              "--chunks", "8"], timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = _line(r.stdout)
+    assert d["n_gpus"] == 8 and d["ranks_seen"]["world"] == 8
+    assert sorted(x["rank"] for x in d["ranks_seen"]["ranks"]) == list(range(8))
+    assert len(d["per_gpu"]) == 8 and all(v > 0 for v in d["per_gpu"])
+    assert d["parity"]["ok"] and d["parity"]["checked"] == 64
+    assert "C4 shard: 2,097,152 x 16 KiB chunks per GPU, 16,777,216 on 8 GPU(s)" in d["config"]["workload"]
+    assert d["config"]["parallelism"].startswith("dp8")
