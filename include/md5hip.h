@@ -183,7 +183,10 @@ int md5hip_plan_desc(const uint32_t *lens, uint64_t n, uint32_t *order);
  * md5hip_order_device then builds that order on the device: with
  * d_bucket_next holding bucket_start, d_order[d_bucket_next[kmax - k]++] = i
  * for every chunk i of key k (positions within one key in no fixed order;
- * the kernels do not care).  Asynchronous on `stream`; 0 or -errno. */
+ * the kernels do not care).  Asynchronous on `stream`; 0 or -errno.  The
+ * histogram must cover every chunk: a chunk whose key exceeds kmax is left
+ * out of the order (its position keeps what it held), never written past
+ * d_bucket_next. */
 #define MD5HIP_HIST_KMAX (1u << 17)
 int md5hip_plan_hist(const uint32_t *hist, uint32_t kmax, uint64_t n, uint32_t *bucket_start);
 int md5hip_order_device(const uint32_t *d_lens, uint64_t n, uint32_t kmax, uint32_t *d_bucket_next,

@@ -9,9 +9,9 @@ from collections import Counter, defaultdict
 import numpy as np
 import torch
 
-REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, REPO)
-sys.path.insert(0, os.path.join(REPO, "scripts"))
+sys.path.insert(0, os.path.join(REPO, "scripts", "diag"))
 from sproxy_amd import md5 as m  # noqa: E402
 from c3_ab import c3_batch  # noqa: E402
 

@@ -22,9 +22,9 @@ import sys
 import numpy as np
 import torch
 
-REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, REPO)
-sys.path.insert(0, os.path.join(REPO, "scripts"))
+sys.path.insert(0, os.path.join(REPO, "scripts", "diag"))
 sys.path.insert(0, os.path.join(REPO, "tests"))
 from c3_trace_x import DIAG, batch  # noqa: E402
 import gen  # noqa: E402

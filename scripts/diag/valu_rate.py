@@ -9,7 +9,7 @@ import sys
 
 import torch
 
-REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 D = ctypes.CDLL(os.path.join(REPO, "build", "diag", "libmd5hip_diag.so"))
 D.md5diag_run.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32,
                           ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p]

@@ -1263,8 +1263,11 @@ order_scatter(const uint32_t* __restrict__ lens, uint64_t n, uint32_t kmax,
               uint32_t* __restrict__ next, uint32_t* __restrict__ order) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t lane = threadIdx.x & 63u;
-  const bool live = i < n;
-  const uint32_t key = live ? (lens[i] >> 6) + 1u : 0u;
+  const uint32_t k0 = i < n ? (lens[i] >> 6) + 1u : 0u;
+  // a key past kmax (lengths the caller's histogram does not cover) would
+  // index before next[0]: such a chunk is left out of the order instead
+  const bool live = i < n && k0 <= kmax;
+  const uint32_t key = live ? k0 : 0u;
   uint64_t todo = __ballot(live);
   while (todo) {                                       // wave-uniform
     const uint32_t leader = (uint32_t)__builtin_ctzll(todo);

@@ -22,7 +22,9 @@ template __global__ void crc32_desc<true>(const uint8_t*, const uint64_t*, const
 #include <errno.h>
 #include <stdlib.h>
 #include <string.h>
+#include <atomic>
 #include <map>
+#include <tuple>
 #include <mutex>
 #include <thread>
 #include <vector>
@@ -61,19 +63,29 @@ int cu_count() {
 // BALANCED's self-resetting group counters: one pair per (device, stream),
 // allocated and zeroed on first use (launches on one stream are ordered, so
 // a counter reset by the last wave of launch k is zero for launch k+1).
+// hipStreamPerThread is one handle that names a different stream in every
+// thread, so it is keyed by a per-thread id as well (ids are never reused,
+// so a finished thread's launch still in flight keeps its own counter).
 std::mutex g_ctr_mu;
-std::map<std::pair<int, hipStream_t>, uint32_t*> g_ctr;
+std::map<std::tuple<int, hipStream_t, uint64_t>, uint32_t*> g_ctr;
+std::atomic<uint64_t> g_thread_ids{0};
+
+uint64_t this_thread_id() {
+  thread_local const uint64_t id = ++g_thread_ids;
+  return id;
+}
 
 uint32_t* balanced_counter(hipStream_t s) {
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  const auto key = std::make_tuple(dev, s, s == hipStreamPerThread ? this_thread_id() : 0ull);
   std::lock_guard<std::mutex> lk(g_ctr_mu);
-  auto it = g_ctr.find({dev, s});
+  auto it = g_ctr.find(key);
   if (it != g_ctr.end()) return it->second;
   uint32_t* c = nullptr;
   if (hipMalloc(&c, 4 * sizeof(uint32_t)) != hipSuccess) return nullptr;
   if (hipMemset(c, 0, 4 * sizeof(uint32_t)) != hipSuccess) { (void)hipFree(c); return nullptr; }
-  g_ctr[{dev, s}] = c;
+  g_ctr[key] = c;
   return c;
 }
 

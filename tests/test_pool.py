@@ -44,41 +44,57 @@ def _bufs(lens, seed):
 
 
 def test_pool_router_eight_threads(cuda):
-    """8 threads x 6 async vectors each through a pool over (0,0,0,0): every
-    ticket equals the oracle, every vector went whole to one device, every
-    device took work and coalesced launches happened."""
+    """8 threads x 6 async vectors each through a pool over (0,0,0,0), the
+    blocks in a registered page heap (zero-copy, as INTEGRATION.md asks of
+    netcache): every ticket equals the oracle, every vector went whole to one
+    device, every device took work, and vectors arriving while launches run
+    were coalesced."""
     vecs = _vectors(48, seed=301)
-    data = [_bufs(lens, 400 + j) for j, lens in enumerate(vecs)]
+    sizes = [sum(v) for v in vecs]
+    heap = gen.xorshift_array(sum(sizes) + 64, seed=302)
+    starts = np.concatenate([[0], np.cumsum(sizes)[:-1]]).astype(np.int64)
+    data = []
+    for j, lens in enumerate(vecs):
+        offs = starts[j] + np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.int64)
+        data.append(([heap[o:o + L] for o, L in zip(offs, lens)], gen.oracle_digests(heap, offs, lens)))
     errors, results = [], {}
-    with m.Pool((0, 0, 0, 0)) as p:
-        start = threading.Barrier(8)
+    m.register_host(heap)
+    try:
+        with m.Pool((0, 0, 0, 0)) as p:
+            start = threading.Barrier(8)
 
-        def worker(t):
-            try:
-                start.wait()
-                mine = list(range(t, 48, 8))
-                pend = [(j, p.submit_async(data[j][0])) for j in mine]
-                for j, pn in reversed(pend):                      # any order
-                    results[j] = pn.wait()
-            except Exception as e:                                # pragma: no cover
-                errors.append(repr(e))
+            def worker(t):
+                try:
+                    start.wait()
+                    mine = list(range(t, 48, 8))
+                    pend = [(j, p.submit_async(data[j][0])) for j in mine]
+                    for j, pn in reversed(pend):                  # any order
+                        results[j] = pn.wait()
+                except Exception as e:                            # pragma: no cover
+                    errors.append(repr(e))
 
-        th = [threading.Thread(target=worker, args=(t,)) for t in range(8)]
-        for x in th:
-            x.start()
-        for x in th:
-            x.join()
-        assert not errors, errors
-        for j in range(48):
-            assert np.array_equal(results[j], data[j][1]), j
-        st = p.stats()
-        assert st["submissions"] == 48 and st["routed_whole"] == 48 and st["split"] == 0
-        dev = [p.device_stats(g) for g in range(4)]
-        assert sum(d["submissions"] for d in dev) == 48
-        assert all(d["submissions"] > 0 for d in dev), dev            # load spread
-        launches = sum(d["launches"] for d in dev)
-        assert launches < 48, dev                                     # vectors coalesced
-        assert sum(d["coalesced_launches"] for d in dev) > 0, dev
+            th = [threading.Thread(target=worker, args=(t,)) for t in range(8)]
+            for x in th:
+                x.start()
+            for x in th:
+                x.join()
+            assert not errors, errors
+            for j in range(48):
+                assert np.array_equal(results[j], data[j][1]), j
+            st = p.stats()
+            assert st["submissions"] == 48 and st["routed_whole"] == 48 and st["split"] == 0
+            dev = [p.device_stats(g) for g in range(4)]
+            assert sum(d["submissions"] for d in dev) == 48
+            assert all(d["submissions"] > 0 for d in dev), dev        # load spread
+            assert sum(d["launches"] for d in dev) < 48, dev          # vectors coalesced
+            assert sum(d["coalesced_launches"] for d in dev) > 0, dev
+    finally:
+        m.unregister_host(heap)
+    # pageable vectors too (host gather): correct, and whole
+    with m.Pool((0, 0)) as p:
+        pend = [p.submit_async(d[0]) for d in data[:8]]
+        for d, pn in zip(data[:8], pend):
+            assert np.array_equal(pn.wait(), d[1])
 
 
 def test_pool_sync_submit_from_threads(cuda):
