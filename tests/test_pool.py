@@ -49,7 +49,17 @@ def test_pool_router_eight_threads(cuda):
     netcache): every ticket equals the oracle, every vector went whole to one
     device, every device took work, and vectors arriving while launches run
     were coalesced."""
-    vecs = _vectors(48, seed=301)
+    # vectors of 1 MiB blocks (chunk_size up to 10 MiB, httpd.c:7968): a launch
+    # is at least one block's ~9 ms chain, so vectors from the other threads
+    # arrive while launches run -- what coalescing needs, whatever the
+    # Python-side cost of a submission
+    rng = np.random.default_rng(301)
+    vecs = []
+    for j in range(48):
+        lens = [1 << 20] * int(rng.integers(2, 9))
+        if j % 3 == 0:
+            lens[-1] = int(rng.integers(1, 1 << 20))                  # last-block tail
+        vecs.append(lens)
     sizes = [sum(v) for v in vecs]
     heap = gen.xorshift_array(sum(sizes) + 64, seed=302)
     starts = np.concatenate([[0], np.cumsum(sizes)[:-1]]).astype(np.int64)
@@ -90,11 +100,14 @@ def test_pool_router_eight_threads(cuda):
             assert sum(d["coalesced_launches"] for d in dev) > 0, dev
     finally:
         m.unregister_host(heap)
-    # pageable vectors too (host gather): correct, and whole
+    # netcache-sized vectors of 16 KiB blocks from pageable memory (host
+    # gather): correct, and whole
+    small = [_bufs(lens, 600 + j) for j, lens in enumerate(_vectors(8, seed=303))]
     with m.Pool((0, 0)) as p:
-        pend = [p.submit_async(d[0]) for d in data[:8]]
-        for d, pn in zip(data[:8], pend):
+        pend = [p.submit_async(d[0]) for d in small]
+        for d, pn in zip(small, pend):
             assert np.array_equal(pn.wait(), d[1])
+        assert p.stats()["routed_whole"] == 8
 
 
 def test_pool_sync_submit_from_threads(cuda):
