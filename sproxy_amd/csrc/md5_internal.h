@@ -38,7 +38,9 @@ int md5hip_verify_iov_as(struct md5hip_batcher *b, int kind, uint32_t fastcrc,
  *   md5hip_batcher_slice   staging bytes per slot
  *   md5hip_submit_as       host chunks (ptrs/lens, or segs/seg_first when
  *                          ptrs is NULL) with an explicit digest kind;
- *                          ticket NULL = synchronous
+ *                          ticket NULL = synchronous; urgent = launched at
+ *                          once like a synchronous call (the caller waits
+ *                          on the ticket right away)
  *   md5hip_host_fixed_as   md5hip_batch_host_fixed with an explicit kind,
  *                          optionally asynchronous
  *   md5hip_batcher_ticket_state  1 done (*err = its error), 0 pending,
@@ -50,7 +52,7 @@ uint64_t md5hip_batcher_slice(const struct md5hip_batcher *b);
 __attribute__((visibility("hidden")))
 int md5hip_submit_as(struct md5hip_batcher *b, int kind, uint32_t fastcrc, const void *const *ptrs,
                      const uint32_t *lens, const struct md5hip_iov *segs, const uint64_t *seg_first,
-                     uint64_t n, unsigned char *digests, uint64_t *ticket);
+                     uint64_t n, unsigned char *digests, uint64_t *ticket, int urgent);
 __attribute__((visibility("hidden")))
 int md5hip_host_fixed_as(struct md5hip_batcher *b, int kind, uint32_t fastcrc, const void *h_base,
                          uint64_t n, uint32_t len, uint64_t stride, unsigned char *digests,

@@ -324,16 +324,17 @@ struct pool_src {
     uint64_t stride;
 };
 
-/* chunks [lo, hi) of `s` to device g's batcher */
+/* chunks [lo, hi) of `s` to device g's batcher, asynchronously; urgent =
+ * the caller waits right away (launch at once, as a synchronous call) */
 static int part_submit(md5hip_pool *p, uint32_t g, int kind, uint32_t fastcrc,
                        const struct pool_src *s, uint64_t lo, uint64_t hi, unsigned char *digests,
-                       uint64_t *ticket)
+                       uint64_t *ticket, int urgent)
 {
     const uint64_t m = hi - lo;
     switch (s->kind) {
     case SRC_PTRS:
         return md5hip_submit_as(p->b[g], kind, fastcrc, s->ptrs + lo, s->lens + lo, NULL, NULL, m,
-                                digests, ticket);
+                                digests, ticket, urgent);
     case SRC_IOV: {
         /* the batcher reads seg_first[0..m] re-based to 0; it has taken the
          * chunks when the call returns, so a temporary copy will do */
@@ -342,7 +343,7 @@ static int part_submit(md5hip_pool *p, uint32_t g, int kind, uint32_t fastcrc,
         if (!sf) return -ENOMEM;
         for (uint64_t i = 0; i <= m; i++) sf[i] = s->seg_first[lo + i] - s->seg_first[lo];
         const int rc = md5hip_submit_as(p->b[g], kind, fastcrc, NULL, NULL, s->segs + s->seg_first[lo],
-                                        sf, m, digests, ticket);
+                                        sf, m, digests, ticket, urgent);
         if (sf != local) free(sf);
         return rc;
     }
@@ -396,7 +397,7 @@ static int pool_submit(md5hip_pool *p, const struct pool_src *s, uint64_t n, uns
         /* asynchronous even for a synchronous caller, so the claim ends as
          * soon as the batcher holds the chunks (its own load counts them) */
         uint64_t t = 0;
-        int rc = part_submit(p, g, kind, fastcrc, s, 0, n, digests, &t);
+        int rc = part_submit(p, g, kind, fastcrc, s, 0, n, digests, &t, ticket == NULL);
         unclaim(p, g, total);
         pthread_mutex_lock(&p->mu);
         p->st.routed_whole++;
@@ -434,7 +435,7 @@ static int pool_submit(md5hip_pool *p, const struct pool_src *s, uint64_t n, uns
         if (rc == 0 && first[j + 1] > first[j]) {
             uint64_t t = 0;
             rc = part_submit(p, sel[j], kind, fastcrc, s, first[j], first[j + 1],
-                             digests + (size_t)dsz * first[j], &t);
+                             digests + (size_t)dsz * first[j], &t, ticket == NULL);
             if (rc == 0 && t) e->part[np++] = (struct mt_part){sel[j], t};
         }
         unclaim(p, sel[j], w[j]);

@@ -1048,6 +1048,9 @@ static int submit(md5hip_batcher *b, const struct chunk_src *src, uint64_t n, un
                   int on_device, int async, uint64_t *ticket, int kind, uint32_t fastcrc,
                   hipStream_t after)
 {
+    /* async == 2: asynchronous, but launched at once as a synchronous call
+     * is (the caller waits right away: the pool's synchronous entries) */
+    const int urgent = async != 1;
     for (uint64_t i = 0; i < n; i++) {
         const uint64_t L = src_len(src, i);
         if (L > 0xffffffffull) return -E2BIG;
@@ -1118,7 +1121,7 @@ static int submit(md5hip_batcher *b, const struct chunk_src *src, uint64_t n, un
             sl->writers--;
         }
         i += m;
-        if (!async && i >= n) sl->flush = 1;  /* the caller waits right away */
+        if (urgent && i >= n) sl->flush = 1;  /* the caller waits right away */
         slot_try_launch(b, sl);
     }
     tk_put(b, t, rc);                        /* the submission's own reference */
@@ -1403,7 +1406,7 @@ uint64_t md5hip_batcher_slice(const md5hip_batcher *b) { return b->cap; }
 
 int md5hip_submit_as(md5hip_batcher *b, int kind, uint32_t fastcrc, const void *const *ptrs,
                      const uint32_t *lens, const struct md5hip_iov *segs, const uint64_t *seg_first,
-                     uint64_t n, unsigned char *digests, uint64_t *ticket)
+                     uint64_t n, unsigned char *digests, uint64_t *ticket, int urgent)
 {
     if (ticket) *ticket = 0;
     if (!b) return -EINVAL;
@@ -1413,7 +1416,7 @@ int md5hip_submit_as(md5hip_batcher *b, int kind, uint32_t fastcrc, const void *
     if (rc) return rc;
     const struct chunk_src src = {ptrs, ptrs ? lens : NULL, ptrs ? NULL : segs, ptrs ? NULL : seg_first,
                                   NULL};
-    return submit(b, &src, n, digests, 0, ticket != NULL, ticket, kind, fastcrc, NULL);
+    return submit(b, &src, n, digests, 0, ticket ? (urgent ? 2 : 1) : 0, ticket, kind, fastcrc, NULL);
 }
 
 int md5hip_host_fixed_as(md5hip_batcher *b, int kind, uint32_t fastcrc, const void *h_base,
