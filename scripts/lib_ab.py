@@ -21,7 +21,7 @@ import torch
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
-sys.path.insert(0, os.path.join(REPO, "scripts"))
+sys.path.insert(0, os.path.join(REPO, "scripts", "diag"))
 from c3_trace_x import batch  # noqa: E402
 from sproxy_amd import md5 as m  # noqa: E402
 
