@@ -21,7 +21,8 @@
  *   4. md5_batch_submit_iov_async + md5_batch_poll / md5_batch_wait (§2g)
  *   5. zero-copy: md5hip_host_register of the heap, gather modes DEVICE,
  *      DMA, AUTO (§2e)
- *   6. md5hip_pool over device 0 listed twice (§2d)
+ *   6. md5hip_pool over device 0 listed twice (§2d): one call, then four
+ *      threads submitting asynchronously at once, whole and split
  *   7. MD5Init/Update/Final page by page (the per-message drop-in, §1)
  *   8. the device entry: blocks packed into a batch arena (md5hip_arena_alloc),
  *      order and kernel from md5hip_plan_desc, md5hip_digest_desc_variant
@@ -130,6 +131,36 @@ static void *asio_thread(void *arg)
     }
     for (int r = j->reps - 1; r >= 0; r--) {        /* tickets in reverse: out-of-order completion */
         const int rc = md5_batch_wait(j->b, tk[r]);
+        if (rc && !j->rc) j->rc = rc;
+        for (int b = j->lo; b < j->hi; b++) j->bad += memcmp(dig[r][b - j->lo], j->want[b], 16) != 0;
+    }
+    return NULL;
+}
+
+/* §2d: one "ASIO" thread submitting its vectors into the shared pool */
+struct pool_job {
+    md5hip_pool *p;
+    const struct md5hip_iov *segs;
+    const uint64_t *first;
+    int lo, hi, reps;
+    unsigned char (*want)[16];
+    int bad, rc;
+};
+
+static void *pool_thread(void *arg)
+{
+    struct pool_job *j = arg;
+    unsigned char dig[8][NBLK_MAX][16];
+    uint64_t tk[8];
+    uint64_t rebased[NBLK_MAX + 1];
+    for (int b = j->lo; b <= j->hi; b++) rebased[b - j->lo] = j->first[b] - j->first[j->lo];
+    for (int r = 0; r < j->reps; r++) {
+        const int rc = md5hip_pool_submit_iov_async(j->p, j->segs + j->first[j->lo], rebased,
+                                                    (uint64_t)(j->hi - j->lo), &dig[r][0][0], &tk[r]);
+        if (rc && !j->rc) j->rc = rc;
+    }
+    for (int r = j->reps - 1; r >= 0; r--) {        /* any order */
+        const int rc = md5hip_pool_wait(j->p, tk[r]);
         if (rc && !j->rc) j->rc = rc;
         for (int b = j->lo; b < j->hi; b++) j->bad += memcmp(dig[r][b - j->lo], j->want[b], 16) != 0;
     }
@@ -295,6 +326,33 @@ int main(void)
         CHECK(rc == 0, "md5hip_pool_submit_iov = %d", rc);
         for (int b = 0; b < nblk; b++)
             CHECK(memcmp(digest[b], want_md5[b], 16) == 0, "pool block %d", b);
+        /* four ASIO threads at once, no lock of their own: each vector goes
+         * whole to one batcher; then the same with a split threshold below
+         * a vector, so every vector is cut over both */
+        for (int split = 0; split < 2; split++) {
+            if (split) {
+                rc = md5hip_pool_set_split(pool, 1u << 20);
+                CHECK(rc == 0, "md5hip_pool_set_split = %d", rc);
+            }
+            struct pool_job pj[4];
+            pthread_t pth[4];
+            for (int t = 0; t < 4; t++) {
+                pj[t] = (struct pool_job){pool, segs, first, t * nblk / 4, (t + 1) * nblk / 4, 3,
+                                          want_md5, 0, 0};
+                if (pthread_create(&pth[t], NULL, pool_thread, &pj[t]) != 0) pth[t] = 0;
+            }
+            for (int t = 0; t < 4; t++) {
+                if (pth[t]) pthread_join(pth[t], NULL);
+                else pool_thread(&pj[t]);
+                CHECK(pj[t].rc == 0 && pj[t].bad == 0, "pool thread %d (split %d): rc %d, bad %d", t,
+                      split, pj[t].rc, pj[t].bad);
+            }
+        }
+        struct md5hip_pool_stats pst;
+        rc = md5hip_pool_get_stats(pool, &pst);
+        CHECK(rc == 0 && pst.routed_whole >= 13 && pst.split == 12,
+              "pool stats rc %d whole %llu split %llu", rc, (unsigned long long)pst.routed_whole,
+              (unsigned long long)pst.split);
         md5hip_pool_destroy(pool);
     }
 
