@@ -364,7 +364,7 @@ __device__ __forceinline__ bool long_outlier(const uint32_t* __restrict__ lens,
                                              const uint32_t* __restrict__ order, uint64_t n,
                                              uint64_t depth, uint32_t bmax) {
   const uint64_t p = depth < n - 1 ? depth : n - 1;
-  const uint32_t probe = lens[order[p]] >> 6;
+  const uint32_t probe = lens[order ? order[p] : p] >> 6;
   return 4u * (uint64_t)probe <= bmax;
 }
 

@@ -39,6 +39,7 @@
  */
 #include <errno.h>
 #include <pthread.h>
+#include <sys/prctl.h>
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
@@ -206,6 +207,11 @@ struct slot {
      * the device; hovf = a chunk past MD5HIP_HIST_KMAX (host sort instead) */
     uint32_t *hh, hkmax, *h_bkt, *d_bkt;
     int hovf;
+    /* keys already non-increasing in reservation order (a vector of full
+     * blocks with a short last one, a single equal-length batch): then the
+     * identity IS the longest-first order, and no order is built or used */
+    uint32_t last_key;
+    int unsorted, use_order;
     uint64_t opened_us, launched_us;  /* first chunk reserved / went in flight */
     uint64_t load;                    /* this slot's share of b->load_bytes */
 };
@@ -319,7 +325,12 @@ static int slot_prepare(md5hip_batcher *b, struct slot *sl)
         sl->copied_n = n;
     }
     int dvar;
-    if (!sl->hovf) {
+    if (!sl->unsorted) {
+        dvar = sl->hovf ? md5hip_plan_desc(sl->h_len, n, sl->h_ord)
+                        : md5hip_plan_hist(sl->hh, sl->hkmax, n, NULL);
+        if (dvar < 0) return dvar;
+        sl->use_order = 0;
+    } else if (!sl->hovf) {
         /* from the histogram: O(keys) on the host, the order on the device */
         dvar = md5hip_plan_hist(sl->hh, sl->hkmax, n, sl->h_bkt);
         if (dvar < 0) return dvar;
@@ -333,6 +344,7 @@ static int slot_prepare(md5hip_batcher *b, struct slot *sl)
         if (dvar < 0) return dvar;
         if (hipMemcpyAsync(sl->d_ord, sl->h_ord, 4 * n, hipMemcpyHostToDevice, sl->stream)) return -EIO;
     }
+    if (sl->unsorted) sl->use_order = 1;
     sl->plan_var = dvar;
     sl->planned_n = n;
     return 0;
@@ -386,10 +398,11 @@ static int slot_enqueue(md5hip_batcher *b, struct slot *sl)
             dst = g0->user;
             sl->direct = 1;
         }
+        const uint32_t *ord = sl->use_order ? sl->d_ord : NULL;
         rc = sl->kind == MD5HIP_DIGEST_CRC32
-                 ? crc32hip_desc(sl->d_data, sl->d_off, sl->d_len, sl->d_ord, n, sl->fastcrc,
+                 ? crc32hip_desc(sl->d_data, sl->d_off, sl->d_len, ord, n, sl->fastcrc,
                                  (uint32_t *)dst, sl->stream)
-                 : md5hip_digest_desc_variant(sl->d_data, sl->d_off, sl->d_len, sl->d_ord, n,
+                 : md5hip_digest_desc_variant(sl->d_data, sl->d_off, sl->d_len, ord, n,
                                               dst, sl->stream, dvar);
         if (rc) return rc;
     }
@@ -427,6 +440,8 @@ static void slot_reset(struct slot *sl)
     sl->tickets_in = 0;
     sl->copied_n = sl->planned_n = sl->seen_n = 0;
     sl->load = 0;
+    sl->last_key = UINT32_MAX;
+    sl->unsorted = sl->use_order = 0;
     if (sl->hh) memset(sl->hh, 0, sizeof(uint32_t) * ((size_t)sl->hkmax + 1));
     sl->hkmax = 0;
     sl->hovf = 0;
@@ -537,6 +552,10 @@ static void *progress_main(void *arg)
 {
     md5hip_batcher *b = arg;
     (void)hipSetDevice(b->device);
+    /* this thread's timed waits are the event polls (10 us while a caller
+     * waits): the default 50 us timer slack would stretch each to ~60 us and
+     * deliver a finished launch that much late */
+    (void)prctl(PR_SET_TIMERSLACK, 1000UL, 0, 0, 0);
     pthread_mutex_lock(&b->mu);
     unsigned idle_us = 20;
     while (!b->stop) {
@@ -1024,6 +1043,8 @@ static long reserve(md5hip_batcher *b, struct slot *sl, const struct chunk_src *
         __atomic_store_n(&b->load_bytes, b->load_bytes + L + 64, __ATOMIC_RELAXED);
         {
             const uint64_t k = (L >> 6) + 1;
+            if (k > sl->last_key) sl->unsorted = 1;
+            sl->last_key = k > UINT32_MAX ? UINT32_MAX : (uint32_t)k;
             if (k > MD5HIP_HIST_KMAX) {
                 sl->hovf = 1;
             } else {
