@@ -194,6 +194,31 @@ def test_pool_ticket_errors(cuda):
             p.submit_device_async(np.zeros(1, np.uint64), np.zeros(1, np.uint32))
 
 
+def test_pool_failed_submission_then_good_ones(cuda):
+    """A submission the batchers refuse (a chunk larger than a slice: -E2BIG)
+    fails alone -- whole or split, nothing left in flight -- and later
+    tickets report their own results (the batcher keeps per-ticket errors,
+    md5_tickets.h)."""
+    import errno
+    lens = [200000] * 40
+    bufs, want, blob, offs = _bufs(lens, 361)
+    big = bufs[:10] + [np.zeros(3 << 20, np.uint8)] + bufs[10:20]          # 3 MiB > 2 MiB slice
+    with m.Pool((0, 0), slice_bytes=2 << 20, nslots=2) as p:
+        for split in (0, 1 << 20):
+            p.set_split(split)
+            with pytest.raises(m.MD5HipError) as ei:
+                p.submit(big)
+            assert ei.value.rc == -errno.E2BIG
+            with pytest.raises(m.MD5HipError):
+                p.submit_async(big)
+            with pytest.raises(m.MD5HipError):
+                p.submit_async([big[10]])                                       # whole
+            pend = [p.submit_async(bufs[k:k + 10]) for k in range(0, 40, 10)]
+            for k, pn in zip(range(0, 40, 10), pend):
+                assert np.array_equal(pn.wait(), want[k:k + 10])
+            assert np.array_equal(p.submit(bufs), want)
+
+
 def test_device_submit_ordered_after_producer_stream(cuda):
     """md5_batch_submit_device_on: chunks written by a kernel still running on
     the producer's stream are hashed after it, with no host sync in between."""
