@@ -402,6 +402,82 @@ diag_xdma1nt_clk(const uint8_t* __restrict__ base, uint64_t n, uint32_t len, uin
   }
 }
 
+// DRAM-locality probes of the product C2 body (md5_fixed_xdma1nt's loader and
+// hash, same occupancy): which chunks a wave takes.  S = lane stride inside a
+// block of 64*S consecutive chunks (S waves share it, wave k taking chunks
+// k, k+S, ...), so one DMA instruction's 8 rows lie S*16 KiB apart instead of
+// 16 KiB; kPerm: the wave -> group assignment permuted (odd multiplier mod the
+// wave count, a power of two), so concurrently running waves read far-apart
+// regions instead of neighbouring ones.  Digests land at their chunk's index
+// (bit-exact with the product); per-wave clock stamps after the digests.
+template <int S, bool kPerm>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5)))
+diag_xdma_map(const uint8_t* __restrict__ base, uint64_t n, uint32_t len, uint64_t stride,
+              uint4* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) uint8_t img_all[4 * 8192];
+  const uint64_t t0 = __builtin_amdgcn_s_memtime();
+  const uint64_t r0 = __builtin_amdgcn_s_memrealtime();
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint64_t nwaves = n / 64;                       // n: a multiple of 64 * S (host checks)
+  uint64_t w = (uint64_t)blockIdx.x * 4u + wave;
+  if (w < nwaves) {
+    if (kPerm) w = (w * 0x9E3779B1ull) & (nwaves - 1);  // nwaves: a power of two
+    const uint64_t blk = w / S, k = w % S;
+    const uint64_t wave_first = blk * 64u * S + k;      // lane l: chunk wave_first + l*S
+    uint8_t* img = img_all + wave * 8192u;
+    const uint32_t lane = threadIdx.x & 63u;
+    const __amdgpu_buffer_rsrc_t rsrc = uniform_rsrc(base + wave_first * stride);
+    uint32_t voff[8];
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      const uint32_t row = (uint32_t)r * 8u + (lane >> 3);
+      const uint32_t part = (lane & 7u) ^ ((row >> 1) & 7u);
+      voff[r] = row * (uint32_t)S * (uint32_t)stride + part * 16u;
+    }
+    const uint32_t g = (lane >> 1) & 7u;
+    const uint32_t nfull = len >> 6, nstage = nfull >> 1;
+    Md5Hasher<false> h;
+    auto st = h.init();
+    auto issue = [&](uint32_t stg) __attribute__((always_inline)) {
+#pragma unroll
+      for (int r = 0; r < 8; ++r)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, img + r * 1024, 16, voff[r], stg * 128u, 0, 2);
+    };
+    issue(0);
+    for (uint32_t stg = 0; stg < nstage; ++stg) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      uint4 wv[2][4];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const u32x4 v = *reinterpret_cast<const u32x4*>(img + lane * 128 + ((q ^ g) * 16));
+        wv[q >> 2][q & 3] = make_uint4(v.x, v.y, v.z, v.w);
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if (stg + 1 < nstage) issue(stg + 1);
+      __builtin_amdgcn_sched_barrier(0);
+      h.block(st, wv[0]);
+      h.block(st, wv[1]);
+    }
+    const uint64_t ci = wave_first + (uint64_t)lane * S;
+    const uint8_t* chunk = base + ci * stride;
+    if (nfull & 1u) {
+      uint4 wb[4];
+      load_block(wb, reinterpret_cast<const uint4*>(chunk + ((uint64_t)(nfull - 1) << 6)));
+      h.block(st, wb);
+    }
+    h.finish(st, chunk + ((uint64_t)nfull << 6), len & 63u, len);
+    h.store(out, ci, st);
+  }
+  const uint64_t t1 = __builtin_amdgcn_s_memtime();
+  const uint64_t r1 = __builtin_amdgcn_s_memrealtime();
+  if ((threadIdx.x & 63u) == 0) {
+    uint64_t* clk = reinterpret_cast<uint64_t*>(out + n);
+    const uint64_t wi = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    clk[2 * wi] = t1 - t0;
+    clk[2 * wi + 1] = r1 - r0;
+  }
+}
+
 // CRC-32 product body (crc32_fixed_xpose) with clock stamps after n*16 bytes.
 __global__ void __launch_bounds__(256)
 diag_crc_clk(const uint8_t* __restrict__ base, uint64_t n, uint32_t len, uint64_t stride,
@@ -769,6 +845,18 @@ extern "C" int md5diag_run(int kind, const void* base, uint64_t n, uint32_t len,
     case 60: hipLaunchKernelGGL(diag_xdma2<1>, dim3((uint32_t)((n + 63) / 64)), dim3(64), 0, s, b, n, len, stride, o); break;
     case 58: hipLaunchKernelGGL(diag_xdma<0>, dim3(grid), dim3(256), 0, s, b, n, len, stride, o); break;
     case 54: hipLaunchKernelGGL(diag_xpose1nt_nopeel, dim3(grid), dim3(256), 0, s, b, n, len, stride, o); break;
+    case 91: case 92: case 93: case 94: case 95: {
+      // DRAM-locality probes (diag_xdma_map): 91 = groups permuted, 92/93/94 =
+      // lane stride 4/16/64, 95 = stride 16 + permuted.  n: a power of two,
+      // a multiple of 64 * 64; 64 * S * stride < 2^32
+      if ((n & (n - 1)) || n % (64u * 64u) || 64ull * 64u * stride >= (1ull << 32)) return -EINVAL;
+      if (kind == 91) hipLaunchKernelGGL((diag_xdma_map<1, true>), dim3(grid), dim3(256), 0, s, b, n, len, stride, o);
+      if (kind == 92) hipLaunchKernelGGL((diag_xdma_map<4, false>), dim3(grid), dim3(256), 0, s, b, n, len, stride, o);
+      if (kind == 93) hipLaunchKernelGGL((diag_xdma_map<16, false>), dim3(grid), dim3(256), 0, s, b, n, len, stride, o);
+      if (kind == 94) hipLaunchKernelGGL((diag_xdma_map<64, false>), dim3(grid), dim3(256), 0, s, b, n, len, stride, o);
+      if (kind == 95) hipLaunchKernelGGL((diag_xdma_map<16, true>), dim3(grid), dim3(256), 0, s, b, n, len, stride, o);
+      break;
+    }
     case 90: hipLaunchKernelGGL(diag_xdma1nt_clk, dim3(grid), dim3(256), 0, s, b, n, len, stride, o); break;
     case 51: hipLaunchKernelGGL(diag_crc_clk, dim3(grid), dim3(256), 0, s, b, n, len, stride, o); break;
     case 50: hipLaunchKernelGGL(diag_xpose1nt_clk<FoldHasher>, dim3(grid), dim3(256), 0, s, b, n, len, stride, o); break;
