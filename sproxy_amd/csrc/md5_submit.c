@@ -1060,17 +1060,22 @@ static long reserve(md5hip_batcher *b, struct slot *sl, const struct chunk_src *
     return (long)(j - i);
 }
 
-/* The submission engine.  kind < 0: the batcher's current digest kind;
- * else this submission's own (it never changes the batcher's setting). */
-/* after != NULL: the producer's stream -- every slot taking chunks of this
- * submission waits on the producer's work enqueued so far before its kernel
- * (an event recorded on `after`, waited on by the slot's stream). */
+/* The submission engine.
+ *   async   0 = synchronous (returns when the digests are delivered);
+ *           1 = asynchronous (*ticket; the slot may linger and coalesce);
+ *           2 = asynchronous but launched at once like a synchronous call
+ *               (the caller waits on *ticket right away: the pool's
+ *               synchronous entries)
+ *   kind    < 0: the batcher's current digest kind; else this submission's
+ *           own (it never changes the batcher's setting)
+ *   after   != NULL: the producer's stream -- every slot taking chunks of
+ *           this submission waits on the producer's work enqueued so far
+ *           before its kernel (an event recorded on `after`, waited on by
+ *           the slot's stream) */
 static int submit(md5hip_batcher *b, const struct chunk_src *src, uint64_t n, unsigned char *digests,
                   int on_device, int async, uint64_t *ticket, int kind, uint32_t fastcrc,
                   hipStream_t after)
 {
-    /* async == 2: asynchronous, but launched at once as a synchronous call
-     * is (the caller waits right away: the pool's synchronous entries) */
     const int urgent = async != 1;
     for (uint64_t i = 0; i < n; i++) {
         const uint64_t L = src_len(src, i);
