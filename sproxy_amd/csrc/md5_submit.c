@@ -809,7 +809,7 @@ int md5hip_batcher_set_gather(md5hip_batcher *b, int mode)
 {
     if (!b || mode < MD5HIP_GATHER_HOST || mode > MD5HIP_GATHER_AUTO) return -EINVAL;
     pthread_mutex_lock(&b->mu);
-    b->gather = mode;
+    __atomic_store_n(&b->gather, mode, __ATOMIC_RELAXED);
     pthread_mutex_unlock(&b->mu);
     return 0;
 }
@@ -1085,7 +1085,10 @@ static int submit(md5hip_batcher *b, const struct chunk_src *src, uint64_t n, un
     struct dev_guard g;
     if (dev_enter(&g, b->device)) return -ENODEV;
     int zc = 0;
-    if (!src->dptrs && b->gather != MD5HIP_GATHER_HOST && b->device < REG_MAXDEV &&
+    /* gather is read here without mu (set_gather may change it meanwhile):
+     * it only decides whether this submission may go zero-copy */
+    if (!src->dptrs && __atomic_load_n(&b->gather, __ATOMIC_RELAXED) != MD5HIP_GATHER_HOST &&
+        b->device < REG_MAXDEV &&
         src_registered(src, n)) {
         zc = 1;
         for (uint64_t i = 0; i < n; i++)

@@ -1,0 +1,344 @@
+/*
+ * batcher_check.c -- the batcher, the device queue and the pool
+ * (md5_submit.c, md5_pool.c) run whole on the host against the fake HIP
+ * runtime of fake_hip.c, from 10 threads at once for a few seconds, under
+ * ASan+UBSan or TSan (tests/test_batcher_host.py).  Every thread picks
+ * random operations -- synchronous / asynchronous submits of pointer lists
+ * and page lists, verify with a flipped digest, host_fixed, device-resident
+ * submits with host or device digests (also ordered after a producer
+ * stream), pool submits whole and split, CRC-32 on its own batcher -- from
+ * pageable or registered memory, and checks every digest against the
+ * library's host MD5 computed up front; one more thread keeps changing the
+ * batchers' knobs (inflight target, linger, gather mode).  Exits 0 when
+ * every check holds.
+ */
+#include <errno.h>
+#include <pthread.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+
+#include "md5.h"
+#include "md5hip.h"
+#include "nc_digest.h"
+
+#define NCH 3000
+#define MAXV 200
+
+static unsigned char *g_heap, *g_pageable;
+static uint32_t g_lens[NCH];
+static uint64_t g_offs[NCH];
+static unsigned char g_md5[NCH][16];
+static uint32_t g_crc[NCH];
+static md5hip_batcher *g_b, *g_q, *g_crcb;
+static md5hip_pool *g_pool;
+extern uint32_t fake_hip_fail_len;
+static int g_stop;
+#define STOPPED() __atomic_load_n(&g_stop, __ATOMIC_RELAXED)
+#define STOP() __atomic_store_n(&g_stop, 1, __ATOMIC_RELAXED)
+static int g_fail;
+static pthread_mutex_t g_fail_mu = PTHREAD_MUTEX_INITIALIZER;
+
+static void fail(const char *what, int t, int rc)
+{
+    pthread_mutex_lock(&g_fail_mu);
+    if (!g_fail) printf("FAIL thread %d: %s (rc %d)\n", t, what, rc);
+    g_fail = 1;
+    STOP();
+    pthread_mutex_unlock(&g_fail_mu);
+}
+
+static uint64_t rnd(uint64_t *s)
+{
+    *s ^= *s << 13; *s ^= *s >> 7; *s ^= *s << 17;
+    return *s;
+}
+
+static double now(void)
+{
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return ts.tv_sec + ts.tv_nsec * 1e-9;
+}
+
+struct held {
+    uint64_t t;
+    int kind;                      /* 0 batcher, 1 queue, 2 pool */
+    int n, idx[MAXV];
+    unsigned char dig[MAXV][16];
+};
+
+static int check_md5(unsigned char (*dig)[16], const int *idx, int n)
+{
+    for (int i = 0; i < n; i++)
+        if (memcmp(dig[i], g_md5[idx[i]], 16)) return 0;
+    return 1;
+}
+
+static void *worker(void *arg)
+{
+    const int t = (int)(intptr_t)arg;
+    uint64_t s = 0x9E3779B97F4A7C15ull ^ (uint64_t)(t + 1) * 7919u;
+    struct held *held[4];
+    int nheld = 0;
+    const void *ptrs[MAXV];
+    uint32_t lens[MAXV];
+    uint64_t dptrs[MAXV];
+    struct md5hip_iov segs[2 * MAXV];
+    uint64_t first[MAXV + 1];
+    unsigned char dig[MAXV][16];
+    int idx[MAXV];
+    while (!STOPPED()) {
+        const int n = 1 + (int)(rnd(&s) % MAXV);
+        const unsigned char *src = rnd(&s) % 3 ? g_heap : g_pageable;
+        for (int i = 0; i < n; i++) {
+            idx[i] = (int)(rnd(&s) % NCH);
+            ptrs[i] = src + g_offs[idx[i]];
+            lens[i] = g_lens[idx[i]];
+            dptrs[i] = (uint64_t)(uintptr_t)(g_heap + g_offs[idx[i]]);
+        }
+        const int op = (int)(rnd(&s) % 10);
+        int rc = 0;
+        memset(dig, 0, sizeof dig);
+        switch (op) {
+        case 0:
+            rc = md5_batch_submit(g_b, ptrs, lens, (uint64_t)n, &dig[0][0]);
+            if (rc || !check_md5(dig, idx, n)) fail("submit", t, rc);
+            break;
+        case 1: case 2: {
+            if (nheld == 4) break;
+            struct held *h = held[nheld] = malloc(sizeof *h);
+            h->n = n;
+            memcpy(h->idx, idx, sizeof(int) * n);
+            h->kind = op == 1 ? 0 : 2;
+            rc = op == 1 ? md5_batch_submit_async(g_b, ptrs, lens, (uint64_t)n, &h->dig[0][0], &h->t)
+                         : md5hip_pool_submit_async(g_pool, ptrs, lens, (uint64_t)n, &h->dig[0][0], &h->t);
+            if (rc) fail("submit_async", t, rc);
+            else nheld++;
+            if (rc) free(h);
+            break;
+        }
+        case 3: {
+            uint64_t ns = 0;
+            for (int i = 0; i < n; i++) {
+                first[i] = ns;
+                const uint32_t a = lens[i] / 3;
+                segs[ns++] = (struct md5hip_iov){ptrs[i], a};
+                segs[ns++] = (struct md5hip_iov){(const unsigned char *)ptrs[i] + a, lens[i] - a};
+            }
+            first[n] = ns;
+            rc = rnd(&s) & 1 ? md5_batch_submit_iov(g_b, segs, first, (uint64_t)n, &dig[0][0])
+                             : md5hip_pool_submit_iov(g_pool, segs, first, (uint64_t)n, &dig[0][0]);
+            if (rc || !check_md5(dig, idx, n)) fail("submit_iov", t, rc);
+            break;
+        }
+        case 4: {
+            uint64_t ns = 0;
+            for (int i = 0; i < n; i++) {
+                first[i] = ns;
+                segs[ns++] = (struct md5hip_iov){ptrs[i], lens[i]};
+                memcpy(dig[i], g_md5[idx[i]], 16);
+            }
+            first[n] = ns;
+            const int j = (int)(rnd(&s) % (uint64_t)n);
+            dig[j][5] ^= 0x10;
+            unsigned char ok[MAXV];
+            rc = md5hip_batch_verify_iov(g_b, segs, first, (uint64_t)n, &dig[0][0], ok);
+            if (rc != 1 || ok[j]) fail("verify", t, rc);
+            break;
+        }
+        case 5: {
+            rc = md5_batch_submit_device(g_q, dptrs, lens, (uint64_t)n, &dig[0][0], 0);
+            if (rc || !check_md5(dig, idx, n)) fail("submit_device", t, rc);
+            break;
+        }
+        case 6: {
+            /* device digests (16-B aligned in place, or odd: scattered) */
+            unsigned char *raw = malloc(16 * (size_t)n + 20);
+            unsigned char *d = raw + (rnd(&s) & 1 ? 0 : 4);
+            rc = md5_batch_submit_device_on(g_q, dptrs, lens, (uint64_t)n, d, 1, rnd(&s) & 1 ? (void *)g_q : NULL,
+                                            NULL);
+            if (rc || !check_md5((unsigned char (*)[16])d, idx, n)) fail("submit_device_on", t, rc);
+            free(raw);
+            break;
+        }
+        case 7: {
+            if (nheld == 4) break;
+            struct held *h = held[nheld] = malloc(sizeof *h);
+            h->n = n;
+            memcpy(h->idx, idx, sizeof(int) * n);
+            h->kind = 1;
+            rc = md5_batch_submit_device_async(g_q, dptrs, lens, (uint64_t)n, &h->dig[0][0], 0, &h->t);
+            if (rc) fail("submit_device_async", t, rc), free(h);
+            else nheld++;
+            break;
+        }
+        case 8: {
+            uint32_t crc[MAXV];
+            rc = md5_batch_submit(g_crcb, ptrs, lens, (uint64_t)n, (unsigned char *)crc);
+            for (int i = 0; i < n && !rc; i++)
+                if (crc[i] != g_crc[idx[i]]) rc = -1000 - i;
+            if (rc) fail("crc", t, rc);
+            break;
+        }
+        default: {
+            const uint32_t L = 4096;
+            const uint64_t k = rnd(&s) % 300;
+            const int m = 1 + (int)(rnd(&s) % 60);
+            const unsigned char *base = g_heap + k * L;
+            rc = rnd(&s) & 1 ? md5hip_batch_host_fixed(g_b, base, (uint64_t)m, L, L, &dig[0][0])
+                             : md5hip_pool_host_fixed(g_pool, base, (uint64_t)m, L, L, &dig[0][0]);
+            for (int i = 0; i < m && !rc; i++) {
+                unsigned char w[16];
+                struct MD5Context c;
+                MD5Init(&c);
+                MD5Update(&c, base + (uint64_t)i * L, L);
+                MD5Final(w, &c);
+                if (memcmp(w, dig[i], 16)) rc = -2000 - i;
+            }
+            if (rc) fail("host_fixed", t, rc);
+        }
+        }
+        /* collect a held ticket now and then, in any order */
+        if (nheld && (nheld == 4 || rnd(&s) % 3 == 0)) {
+            const int j = (int)(rnd(&s) % (uint64_t)nheld);
+            struct held *h = held[j];
+            if (rnd(&s) & 1) {                       /* poll a few times first */
+                for (int k = 0; k < 3; k++) {
+                    const int p = h->kind == 2 ? md5hip_pool_poll(g_pool, h->t)
+                                               : md5_batch_poll(h->kind ? g_q : g_b, h->t);
+                    if (p < 0) fail("poll", t, p);
+                    if (p) break;
+                }
+            }
+            rc = h->kind == 2 ? md5hip_pool_wait(g_pool, h->t) : md5_batch_wait(h->kind ? g_q : g_b, h->t);
+            if (rc || !check_md5(h->dig, h->idx, h->n)) fail("wait", t, rc);
+            free(h);
+            held[j] = held[--nheld];
+        }
+    }
+    for (int j = 0; j < nheld; j++) {
+        struct held *h = held[j];
+        const int rc = h->kind == 2 ? md5hip_pool_wait(g_pool, h->t) : md5_batch_wait(h->kind ? g_q : g_b, h->t);
+        if (rc || !check_md5(h->dig, h->idx, h->n)) fail("final wait", t, rc);
+        free(h);
+    }
+    return NULL;
+}
+
+static void *knobs(void *arg)
+{
+    (void)arg;
+    uint64_t s = 42;
+    while (!STOPPED()) {
+        md5hip_batcher_set_inflight(g_b, 1 + (uint32_t)(rnd(&s) % 3));
+        md5hip_batcher_set_linger(g_q, (uint32_t)(rnd(&s) % 400));
+        md5hip_batcher_set_gather(g_b, (int)(rnd(&s) % 4));
+        md5hip_pool_set_gather(g_pool, (int)(rnd(&s) % 4));
+        md5hip_pool_set_split(g_pool, (rnd(&s) % 2) ? 0 : 256u << 10);
+        struct timespec ts = {0, 2000000};
+        nanosleep(&ts, NULL);
+    }
+    return NULL;
+}
+
+int main(int argc, char **argv)
+{
+    const double secs = argc > 1 ? atof(argv[1]) : 4.0;
+    uint64_t s = 0x1234567ull, total = 0;
+    for (int i = 0; i < NCH; i++) {
+        const uint64_t r = rnd(&s);
+        g_lens[i] = r % 7 == 0 ? 0 : r % 5 == 0 ? (uint32_t)(r % 64)
+                  : r % 11 == 0 ? (uint32_t)(r % 40000) : (uint32_t)(r % 3000);
+        g_offs[i] = total;
+        total += (g_lens[i] + 15) & ~15u;
+    }
+    g_heap = malloc(total + 64);
+    g_pageable = malloc(total + 64);
+    for (uint64_t k = 0; k < total + 64; k++) g_heap[k] = (unsigned char)(rnd(&s) >> 11);
+    memcpy(g_pageable, g_heap, total + 64);
+    for (int i = 0; i < NCH; i++) {
+        struct MD5Context c;
+        MD5Init(&c);
+        MD5Update(&c, g_heap + g_offs[i], g_lens[i]);
+        MD5Final(g_md5[i], &c);
+        g_crc[i] = nc_crc32(g_heap + g_offs[i], g_lens[i]);
+    }
+    int rc = md5hip_host_register(g_heap, total + 64);
+    if (rc) { printf("FAIL register %d\n", rc); return 1; }
+    if ((rc = md5hip_batcher_create(0, 1u << 20, 3, &g_b)) ||
+        (rc = md5hip_queue_create(0, 4096, 4, &g_q)) ||
+        (rc = md5hip_batcher_create(0, 1u << 20, 2, &g_crcb))) {
+        printf("FAIL create %d\n", rc);
+        return 1;
+    }
+    md5hip_batcher_set_digest(g_crcb, MD5HIP_DIGEST_CRC32, 0);
+    /* error paths, one thread: a chunk over the slice, a never-issued
+     * ticket, a launch that fails (sync and async; the failure is kept for
+     * a second wait and does not touch later submissions) */
+    {
+        static unsigned char big[(1u << 20) + 1], odd[77777];
+        const void *p1[2] = {big, g_pageable};
+        uint32_t l1[2] = {sizeof big, 10};
+        unsigned char d1[2][16];
+        uint64_t tk;
+        if ((rc = md5_batch_submit(g_b, p1, l1, 2, &d1[0][0])) != -E2BIG) { printf("FAIL e2big %d\n", rc); return 1; }
+        if ((rc = md5_batch_wait(g_b, 1ull << 40)) >= 0) { printf("FAIL bogus ticket %d\n", rc); return 1; }
+        fake_hip_fail_len = sizeof odd;
+        p1[0] = odd;
+        l1[0] = sizeof odd;
+        if ((rc = md5_batch_submit(g_b, p1, l1, 2, &d1[0][0])) >= 0) { printf("FAIL launch error %d\n", rc); return 1; }
+        if ((rc = md5_batch_submit_async(g_b, p1, l1, 2, &d1[0][0], &tk)) ||
+            (rc = md5_batch_wait(g_b, tk)) >= 0 || (rc = md5_batch_wait(g_b, tk)) >= 0) {
+            printf("FAIL async launch error %d\n", rc);
+            return 1;
+        }
+        fake_hip_fail_len = 0xffffffffu;
+        struct MD5Context c;
+        unsigned char w[16];
+        MD5Init(&c);
+        MD5Update(&c, g_pageable, 10);
+        MD5Final(w, &c);
+        if ((rc = md5_batch_submit(g_b, p1 + 1, l1 + 1, 1, &d1[0][0])) || memcmp(d1[0], w, 16)) {
+            printf("FAIL after error %d\n", rc);
+            return 1;
+        }
+    }
+    const int devs[3] = {0, 1, 2};
+    if ((rc = md5hip_pool_create(devs, 3, 1u << 20, 2, &g_pool))) { printf("FAIL pool %d\n", rc); return 1; }
+    enum { T = 10 };
+    pthread_t th[T], kt;
+    for (int t = 0; t < T; t++) pthread_create(&th[t], NULL, worker, (void *)(intptr_t)t);
+    pthread_create(&kt, NULL, knobs, NULL);
+    const double t0 = now();
+    while (!STOPPED() && now() - t0 < secs) {
+        struct timespec ts = {0, 20000000};
+        nanosleep(&ts, NULL);
+    }
+    STOP();
+    for (int t = 0; t < T; t++) pthread_join(th[t], NULL);
+    pthread_join(kt, NULL);
+    struct md5hip_batcher_stats bs, qs;
+    md5hip_batcher_get_stats(g_b, &bs);
+    md5hip_batcher_get_stats(g_q, &qs);
+    struct md5hip_pool_stats ps;
+    md5hip_pool_get_stats(g_pool, &ps);
+    md5hip_pool_destroy(g_pool);
+    md5hip_batcher_destroy(g_b);
+    md5hip_batcher_destroy(g_q);
+    md5hip_batcher_destroy(g_crcb);
+    md5hip_host_unregister(g_heap);
+    free(g_heap);
+    free(g_pageable);
+    if (g_fail) return 1;
+    printf("batcher %llu submissions %llu launches %llu coalesced; queue %llu / %llu / %llu; "
+           "pool %llu whole %llu split\n",
+           (unsigned long long)bs.submissions, (unsigned long long)bs.launches,
+           (unsigned long long)bs.coalesced_launches, (unsigned long long)qs.submissions,
+           (unsigned long long)qs.launches, (unsigned long long)qs.coalesced_launches,
+           (unsigned long long)ps.routed_whole, (unsigned long long)ps.split);
+    printf("batcher ok\n");
+    return 0;
+}

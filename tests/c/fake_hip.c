@@ -1,0 +1,213 @@
+/*
+ * fake_hip.c -- TEST INFRASTRUCTURE: just enough of the HIP runtime, and of
+ * the library's device entries, for the batcher (sproxy_amd/csrc/md5_submit.c)
+ * and the pool to run on a machine with no GPU, under ASan or TSan
+ * (tests/test_batcher_host.py, tests/c/batcher_check.c).
+ *
+ *   - "device" memory is host memory; device pointers are host pointers;
+ *   - a stream executes each operation when it is enqueued (copies and
+ *     "kernels" run at once, on the calling thread);
+ *   - an event recorded on a stream reports hipErrorNotReady for 0-3 queries
+ *     (a per-event pseudo-random count) before hipSuccess, so slots stay in
+ *     flight for a while and the batcher's progress thread, coalescing and
+ *     out-of-order completion all run;
+ *   - the "kernels" compute the digests on the CPU with the library's own
+ *     host MD5 (md5_stream.c) and CRC-32 (nc_digest.c).
+ * Nothing here is part of the product.
+ */
+#include <errno.h>
+#include <pthread.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <hip/hip_runtime_api.h>
+
+#include "md5.h"
+#include "md5hip.h"
+#include "nc_digest.h"
+#include "../../sproxy_amd/csrc/md5_internal.h"
+
+struct ihipEvent_t {
+    int left;                     /* queries still answered NotReady */
+    unsigned seed;
+};
+struct ihipStream_t {
+    int dummy;
+};
+
+static __thread int t_device;
+/* a launch holding a chunk of this length fails with -EIO (error paths) */
+uint32_t fake_hip_fail_len = 0xffffffffu;
+static pthread_mutex_t g_ev_mu = PTHREAD_MUTEX_INITIALIZER;
+
+hipError_t hipGetDevice(int *deviceId) { *deviceId = t_device; return hipSuccess; }
+hipError_t hipSetDevice(int deviceId) { if (deviceId < 0 || deviceId > 7) return hipErrorInvalidDevice; t_device = deviceId; return hipSuccess; }
+hipError_t hipGetDeviceCount(int *count) { *count = 8; return hipSuccess; }
+
+hipError_t hipMalloc(void **ptr, size_t size) { *ptr = malloc(size ? size : 1); return *ptr ? hipSuccess : hipErrorOutOfMemory; }
+hipError_t hipHostMalloc(void **ptr, size_t size, unsigned int flags) { (void)flags; return hipMalloc(ptr, size); }
+hipError_t hipFree(void *ptr) { free(ptr); return hipSuccess; }
+hipError_t hipHostFree(void *ptr) { free(ptr); return hipSuccess; }
+hipError_t hipHostRegister(void *hostPtr, size_t sizeBytes, unsigned int flags) { (void)hostPtr; (void)sizeBytes; (void)flags; return hipSuccess; }
+hipError_t hipHostUnregister(void *hostPtr) { (void)hostPtr; return hipSuccess; }
+hipError_t hipHostGetDevicePointer(void **devPtr, void *hstPtr, unsigned int flags) { (void)flags; *devPtr = hstPtr; return hipSuccess; }
+
+hipError_t hipStreamCreateWithFlags(hipStream_t *stream, unsigned int flags)
+{
+    (void)flags;
+    *stream = calloc(1, sizeof(struct ihipStream_t));
+    return *stream ? hipSuccess : hipErrorOutOfMemory;
+}
+hipError_t hipStreamDestroy(hipStream_t stream) { free(stream); return hipSuccess; }
+hipError_t hipStreamWaitEvent(hipStream_t stream, hipEvent_t event, unsigned int flags) { (void)stream; (void)event; (void)flags; return hipSuccess; }
+
+hipError_t hipEventCreateWithFlags(hipEvent_t *event, unsigned flags)
+{
+    (void)flags;
+    *event = calloc(1, sizeof(struct ihipEvent_t));
+    if (!*event) return hipErrorOutOfMemory;
+    (*event)->seed = (unsigned)(uintptr_t)*event;
+    return hipSuccess;
+}
+hipError_t hipEventDestroy(hipEvent_t event) { free(event); return hipSuccess; }
+hipError_t hipEventRecord(hipEvent_t event, hipStream_t stream)
+{
+    (void)stream;
+    pthread_mutex_lock(&g_ev_mu);
+    event->seed = event->seed * 1103515245u + 12345u;
+    event->left = (int)((event->seed >> 16) % 4u);
+    pthread_mutex_unlock(&g_ev_mu);
+    return hipSuccess;
+}
+hipError_t hipEventQuery(hipEvent_t event)
+{
+    pthread_mutex_lock(&g_ev_mu);
+    const int ready = event->left == 0;
+    if (!ready) event->left--;
+    pthread_mutex_unlock(&g_ev_mu);
+    return ready ? hipSuccess : hipErrorNotReady;
+}
+hipError_t hipEventSynchronize(hipEvent_t event)
+{
+    pthread_mutex_lock(&g_ev_mu);
+    event->left = 0;
+    pthread_mutex_unlock(&g_ev_mu);
+    return hipSuccess;
+}
+
+hipError_t hipMemcpyAsync(void *dst, const void *src, size_t sizeBytes, hipMemcpyKind kind, hipStream_t stream)
+{
+    (void)kind;
+    (void)stream;
+    if (sizeBytes) memmove(dst, src, sizeBytes);
+    return hipSuccess;
+}
+
+/* ------------------------------------------------------------------ "kernels" */
+static void md5_of(const unsigned char *p, uint32_t len, unsigned char *out)
+{
+    struct MD5Context c;
+    MD5Init(&c);
+    MD5Update(&c, p, len);
+    MD5Final(out, &c);
+}
+
+static uint32_t blk_crc(const unsigned char *p, uint32_t len, uint32_t F)
+{
+    if (F == 0 || len <= F) return nc_crc32(p, len);                   /* blk_io.c:408-424 */
+    return nc_crc32(p, F) ^ nc_crc32(p + (len - F), F);
+}
+
+int md5hip_digest_fixed(const void *d_base, uint64_t n, uint32_t len, uint64_t stride,
+                        unsigned char *d_digests, void *stream)
+{
+    (void)stream;
+    for (uint64_t i = 0; i < n; i++) md5_of((const unsigned char *)d_base + i * stride, len, d_digests + 16 * i);
+    return 0;
+}
+
+int crc32hip_fixed(const void *d_base, uint64_t n, uint32_t len, uint64_t stride, uint32_t fastcrc,
+                   uint32_t *d_crcs, void *stream)
+{
+    (void)stream;
+    for (uint64_t i = 0; i < n; i++) d_crcs[i] = blk_crc((const unsigned char *)d_base + i * stride, len, fastcrc);
+    return 0;
+}
+
+int md5hip_digest_desc_variant(const void *d_base, const uint64_t *d_offsets, const uint32_t *d_lens,
+                               const uint32_t *d_order, uint64_t n, unsigned char *d_digests,
+                               void *stream, int variant)
+{
+    (void)stream;
+    (void)variant;
+    if (((uintptr_t)d_digests & 15u) != 0) return -EINVAL;
+    for (uint64_t k = 0; k < n; k++)
+        if (d_lens[k] == fake_hip_fail_len) return -EIO;
+    for (uint64_t k = 0; k < n; k++) {               /* lanes in `order`, digests by chunk */
+        const uint64_t c = d_order ? d_order[k] : k;
+        if (c >= n) return -EINVAL;
+        md5_of((const unsigned char *)((uintptr_t)d_base + d_offsets[c]), d_lens[c], d_digests + 16 * c);
+    }
+    return 0;
+}
+
+int crc32hip_desc(const void *d_base, const uint64_t *d_offsets, const uint32_t *d_lens,
+                  const uint32_t *d_order, uint64_t n, uint32_t fastcrc, uint32_t *d_crcs, void *stream)
+{
+    (void)stream;
+    for (uint64_t k = 0; k < n; k++) {
+        const uint64_t c = d_order ? d_order[k] : k;
+        if (c >= n) return -EINVAL;
+        d_crcs[c] = blk_crc((const unsigned char *)((uintptr_t)d_base + d_offsets[c]), d_lens[c], fastcrc);
+    }
+    return 0;
+}
+
+int md5hip_gather_launch(const struct md5hip_seg *d_segs, uint64_t nseg, unsigned char *d_dst, void *stream)
+{
+    (void)stream;
+    for (uint64_t k = 0; k < nseg; k++)
+        memmove((void *)((uintptr_t)d_dst + d_segs[k].dst), (const void *)(uintptr_t)d_segs[k].src, d_segs[k].len);
+    return 0;
+}
+
+/* longest-first by key (len >> 6) + 1, stable (md5hip_plan_order) */
+int md5hip_plan_desc(const uint32_t *lens, uint64_t n, uint32_t *order)
+{
+    if (!lens || !order) return n ? -EINVAL : 0;
+    uint32_t kmax = 0;
+    for (uint64_t i = 0; i < n; i++) if ((lens[i] >> 6) + 1 > kmax) kmax = (lens[i] >> 6) + 1;
+    uint64_t at = 0;
+    for (int64_t k = kmax; k >= 1; k--)               /* O(n * keys): test sizes only */
+        for (uint64_t i = 0; i < n; i++)
+            if ((lens[i] >> 6) + 1 == (uint32_t)k) order[at++] = (uint32_t)i;
+    return MD5HIP_DESC_XDMA;
+}
+
+int md5hip_plan_hist(const uint32_t *hist, uint32_t kmax, uint64_t n, uint32_t *bucket_start)
+{
+    if (!hist) return -EINVAL;
+    if (bucket_start) {
+        uint64_t at = 0;
+        for (int64_t k = kmax; k >= 1; k--) {
+            bucket_start[kmax - k] = (uint32_t)at;
+            at += hist[k];
+        }
+        bucket_start[kmax] = (uint32_t)n;
+    }
+    return MD5HIP_DESC_XDMA;
+}
+
+int md5hip_order_device(const uint32_t *d_lens, uint64_t n, uint32_t kmax, uint32_t *d_bucket_next,
+                        uint32_t *d_order, void *stream)
+{
+    (void)stream;
+    for (uint64_t i = 0; i < n; i++) {
+        const uint32_t k = (d_lens[i] >> 6) + 1;
+        if (k > kmax) continue;
+        const uint32_t pos = d_bucket_next[kmax - k]++;
+        if (pos < n) d_order[pos] = (uint32_t)i;
+    }
+    return 0;
+}

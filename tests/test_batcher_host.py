@@ -1,0 +1,47 @@
+"""The whole batcher with no device: tests/c/batcher_check.c links
+md5_submit.c (batcher, device queue), md5_pool.c (router) and the host
+MD5/CRC-32 against tests/c/fake_hip.c, a fake HIP runtime whose streams run
+copies and "kernels" (the library's host MD5/CRC-32) at enqueue and whose
+events stay NotReady for a few queries, so slots are in flight, coalesce and
+complete out of order.  10 threads submit at random (sync/async pointer and
+page lists, verify, host_fixed, device-resident with host or device digests
+and a producer stream, pool whole and split, CRC-32) while another changes
+the knobs; a failing launch is injected once.  Runs under ASan+UBSan and
+under ThreadSanitizer (which found the unlocked gather-mode read in submit(),
+now atomic)."""
+import os
+import shutil
+import subprocess
+
+import pytest
+
+import gen
+
+CSRC = os.path.join(gen.REPO, "sproxy_amd", "csrc")
+INC = os.path.join(gen.REPO, "include")
+SRCS = [os.path.join(gen.REPO, "tests", "c", s) for s in ("batcher_check.c", "fake_hip.c")] + \
+       [os.path.join(CSRC, s) for s in ("md5_submit.c", "md5_pool.c", "md5_stream.c", "nc_digest.c")]
+
+
+def _build_and_run(name, san, env_extra, secs):
+    if not shutil.which("gcc") or not os.path.exists("/opt/rocm/include/hip/hip_runtime_api.h"):
+        pytest.skip("gcc or the HIP headers absent")
+    exe = os.path.join(gen.REPO, "build", name)
+    os.makedirs(os.path.dirname(exe), exist_ok=True)
+    cmd = ["gcc", "-O1", "-g", "-std=gnu11", "-Wall", "-Werror", f"-fsanitize={san}",
+           "-fno-sanitize-recover=all", "-D__HIP_PLATFORM_AMD__", "-I/opt/rocm/include", "-I", INC,
+           *SRCS, "-lpthread", "-o", exe]
+    subprocess.run(cmd, check=True, capture_output=True, text=True)
+    env = dict(os.environ, **env_extra)
+    out = subprocess.run([exe, str(secs)], capture_output=True, text=True, env=env, timeout=300)
+    assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-3000:]
+    assert out.stdout.strip().endswith("batcher ok")
+
+
+def test_batcher_under_asan():
+    _build_and_run("batcher_check_asan", "address,undefined",
+                   {"ASAN_OPTIONS": "detect_leaks=1:abort_on_error=1:verify_asan_link_order=0"}, 3)
+
+
+def test_batcher_under_tsan():
+    _build_and_run("batcher_check_tsan", "thread", {"TSAN_OPTIONS": "halt_on_error=1"}, 3)
