@@ -6,10 +6,12 @@
  * random operations -- synchronous / asynchronous submits of pointer lists
  * and page lists, verify with a flipped digest, host_fixed, device-resident
  * submits with host or device digests (also ordered after a producer
- * stream), pool submits whole and split, CRC-32 on its own batcher -- from
- * pageable or registered memory, and checks every digest against the
- * library's host MD5 computed up front; one more thread keeps changing the
- * batchers' knobs (inflight target, linger, gather mode).  Exits 0 when
+ * stream), pool submits whole and split, CRC-32 on its own batcher, netcache
+ * header verification, flush -- from pageable or registered memory, and
+ * checks every digest against the library's host MD5 computed up front; one
+ * more thread keeps changing the batchers' knobs (inflight target, linger,
+ * gather mode, pool split) and another registers, uses and unregisters a
+ * private page range.  Exits 0 when
  * every check holds.
  */
 #include <errno.h>
@@ -99,7 +101,7 @@ static void *worker(void *arg)
             lens[i] = g_lens[idx[i]];
             dptrs[i] = (uint64_t)(uintptr_t)(g_heap + g_offs[idx[i]]);
         }
-        const int op = (int)(rnd(&s) % 10);
+        const int op = (int)(rnd(&s) % 12);
         int rc = 0;
         memset(dig, 0, sizeof dig);
         switch (op) {
@@ -183,6 +185,43 @@ static void *worker(void *arg)
             if (rc) fail("crc", t, rc);
             break;
         }
+        case 9: {
+            /* netcache headers on the MD5 batcher (a CRC-32 call that must
+             * leave the shared batcher's kind alone); every 3rd one broken */
+            enum { NH = 24 };
+            unsigned char hb[NH][256];
+            const void *hp[NH];
+            unsigned char ok[NH];
+            int bad = 0;
+            for (int i = 0; i < NH; i++) {
+                const uint32_t hs = 20 + (uint32_t)(rnd(&s) % 236), magic = NC_MAGIC_V30;
+                for (int k = 0; k < 256; k++) hb[i][k] = (unsigned char)rnd(&s);
+                memcpy(hb[i] + NC_HDR_OFF_MAGIC, &magic, 4);
+                memcpy(hb[i] + NC_HDR_OFF_HEADER_SIZE, &hs, 4);
+                if (nc_header_seal(hb[i])) { rc = -1; break; }
+                if (i % 3 == 2) hb[i][hs - 1] ^= 0x40, bad++;
+                hp[i] = hb[i];
+            }
+            if (!rc) rc = md5hip_batch_verify_headers(g_b, hp, NH, ok);
+            for (int i = 0; i < NH && rc == bad; i++)
+                if (ok[i] != (i % 3 != 2)) rc = -3000 - i;
+            if (rc != bad) fail("verify_headers", t, rc);
+            rc = 0;
+            break;
+        }
+        case 10: {
+            /* asynchronous submit, then an explicit flush, then wait */
+            uint64_t tk;
+            rc = md5_batch_submit_async(g_b, ptrs, lens, (uint64_t)n, &dig[0][0], &tk);
+            if (!rc) rc = md5_batch_flush(g_b);
+            if (!rc) rc = md5_batch_wait(g_b, tk);
+            if (rc || !check_md5(dig, idx, n)) fail("flush", t, rc);
+            int kind;
+            uint32_t fc;
+            if ((rc = md5hip_batcher_get_digest(g_crcb, &kind, &fc)) || kind != MD5HIP_DIGEST_CRC32 || fc)
+                fail("get_digest", t, rc);
+            break;
+        }
         default: {
             const uint32_t L = 4096;
             const uint64_t k = rnd(&s) % 300;
@@ -241,6 +280,32 @@ static void *knobs(void *arg)
         struct timespec ts = {0, 2000000};
         nanosleep(&ts, NULL);
     }
+    return NULL;
+}
+
+/* registrations come and go beside the workers' lookups: each round
+ * registers a private copy of a heap slice, hashes chunks from it through the
+ * batcher and the pool (zero-copy while registered), unregisters it */
+static void *registrar(void *arg)
+{
+    (void)arg;
+    uint64_t s = 7;
+    const uint64_t span = g_offs[200];
+    unsigned char *copy = malloc(span + 64);
+    memcpy(copy, g_heap, span + 64);
+    const void *ptrs[200];
+    unsigned char dig[200][16];
+    int idx[200];
+    for (int i = 0; i < 200; i++) ptrs[i] = copy + g_offs[i], idx[i] = i;
+    while (!STOPPED()) {
+        int rc = md5hip_host_register(copy, span + 64);
+        const int n = 1 + (int)(rnd(&s) % 200);
+        if (!rc) rc = rnd(&s) & 1 ? md5_batch_submit(g_b, ptrs, g_lens, (uint64_t)n, &dig[0][0])
+                                  : md5hip_pool_submit(g_pool, ptrs, g_lens, (uint64_t)n, &dig[0][0]);
+        if (rc || !check_md5(dig, idx, n)) fail("registered copy", 99, rc);
+        if ((rc = md5hip_host_unregister(copy))) fail("unregister", 99, rc);
+    }
+    free(copy);
     return NULL;
 }
 
@@ -309,9 +374,10 @@ int main(int argc, char **argv)
     const int devs[3] = {0, 1, 2};
     if ((rc = md5hip_pool_create(devs, 3, 1u << 20, 2, &g_pool))) { printf("FAIL pool %d\n", rc); return 1; }
     enum { T = 10 };
-    pthread_t th[T], kt;
+    pthread_t th[T], kt, rt;
     for (int t = 0; t < T; t++) pthread_create(&th[t], NULL, worker, (void *)(intptr_t)t);
     pthread_create(&kt, NULL, knobs, NULL);
+    pthread_create(&rt, NULL, registrar, NULL);
     const double t0 = now();
     while (!STOPPED() && now() - t0 < secs) {
         struct timespec ts = {0, 20000000};
@@ -320,6 +386,7 @@ int main(int argc, char **argv)
     STOP();
     for (int t = 0; t < T; t++) pthread_join(th[t], NULL);
     pthread_join(kt, NULL);
+    pthread_join(rt, NULL);
     struct md5hip_batcher_stats bs, qs;
     md5hip_batcher_get_stats(g_b, &bs);
     md5hip_batcher_get_stats(g_q, &qs);

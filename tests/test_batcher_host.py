@@ -5,8 +5,10 @@ copies and "kernels" (the library's host MD5/CRC-32) at enqueue and whose
 events stay NotReady for a few queries, so slots are in flight, coalesce and
 complete out of order.  10 threads submit at random (sync/async pointer and
 page lists, verify, host_fixed, device-resident with host or device digests
-and a producer stream, pool whole and split, CRC-32) while another changes
-the knobs; a failing launch is injected once.  Runs under ASan+UBSan and
+and a producer stream, pool whole and split, CRC-32, netcache header
+verification on the shared MD5 batcher, explicit flush) while one thread
+changes the knobs and another registers, uses and unregisters a private
+page range; a failing launch is injected once.  Runs under ASan+UBSan and
 under ThreadSanitizer (which found the unlocked gather-mode read in submit(),
 now atomic)."""
 import os
