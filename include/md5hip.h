@@ -75,7 +75,8 @@ int md5hip_digest_desc(const void *d_base, const uint64_t *d_offsets, const uint
 /* Descriptor-batch kernels for md5hip_digest_desc_variant. */
 enum md5hip_desc_variant {
     MD5HIP_DESC_AUTO = 0,   /* the default: XDMA */
-    MD5HIP_DESC_LANE = 1,   /* each lane streams its own chunk (8-block register ring) */
+    MD5HIP_DESC_LANE = 1,   /* each lane streams its own chunk (8-block register ring):
+                               the planner's choice for small batches */
     /* 2: the register-staged XPOSE loader, moved to the diagnostic library */
     MD5HIP_DESC_HYBRID = 3, /* XDMA, but the first waves (one per CU) go lane-direct when
                                they hold a chunk >= 256 KiB (md5hip_plan_desc's choice for
@@ -165,7 +166,9 @@ int md5hip_arena_free(void *d_ptr);
 /*
  * Host planner for a descriptor batch: fills order[] as md5hip_plan_order and
  * returns the enum md5hip_desc_variant to launch it with (>= 0), or -errno.
- * With the longest chunk >= 256 KiB and the median 64-chunk group at most an
+ * LANE for a small batch (at most two 64-chunk groups per CU of the current
+ * device: the launch is one chunk's serial chain, which lane-direct loads
+ * keep free of load waits).  Otherwise, with the longest chunk >= 256 KiB and the median 64-chunk group at most an
  * eighth of the longest (a mixed batch): BALANCED when the batch holds at
  * least 0.4 x (SIMDs x the longest chain) of work, so the placement of waves
  * on SIMDs decides the time; else HYBRID when the longest chunks stand out

@@ -535,7 +535,18 @@ int md5hip_arena_free(void* ptr) {
   return rc;
 }
 
+// Small batches (at most two 64-chunk groups per CU: the netcache call
+// site's vectors of 16-1,024 blocks) run lane-direct.  There each wave is
+// nearly alone on its SIMD and the launch lasts one chunk's serial chain; the
+// 8-block register ring keeps HBM latency off that chain, where XDMA's
+// per-stage DMA wait and LDS round trip stay on it: 147 vs 163 us for
+// 64-4,096 x 16 KiB, 162 vs 171 us at 32,768; past two groups per CU the
+// lane-direct loads crowd the address units (65,536 x 16 KiB: 228 vs
+// 206 us; profiles/r03/small_batch_kernels_*.json).
+constexpr uint64_t kLaneGroupsPerCu = 2;
+
 // Planner for descriptor batches (md5hip.h): the longest-first order, and
+//  - LANE for small batches (above);
 //  - BALANCED for a mixed batch (longest chunk >= 256 KiB, median 64-chunk
 //    group <= 1/8 of it) holding >= 0.4 x (SIMDs x longest chain) of work:
 //    several waves per SIMD, where LPT placement beats the hardware's
@@ -547,9 +558,10 @@ int md5hip_arena_free(void* ptr) {
 int md5hip_plan_desc(const uint32_t* lens, uint64_t n, uint32_t* order) {
   if (int e = md5hip_plan_order(lens, n, order)) return e;
   if (n == 0) return MD5HIP_DESC_XDMA;
+  const uint64_t ngroups = (n + 63) / 64;
+  if (ngroups <= kLaneGroupsPerCu * (uint64_t)cu_count()) return MD5HIP_DESC_LANE;
   const uint32_t bmax = lens[order[0]] >> 6;
   if (bmax < kHybridLongBlocks) return MD5HIP_DESC_XDMA;
-  const uint64_t ngroups = (n + 63) / 64;
   const uint64_t median = (uint64_t)(lens[order[(ngroups / 2) * 64]] >> 6) + 1;
   uint64_t total = 0;           // work in block-steps: a group runs as long as its first lane
   for (uint64_t g = 0; g < ngroups; ++g) total += (uint64_t)(lens[order[g * 64]] >> 6) + 1;
@@ -582,6 +594,7 @@ int md5hip_plan_hist(const uint32_t* hist, uint32_t kmax, uint64_t n, uint32_t* 
   }
   if (bucket_start) bucket_start[kmax] = (uint32_t)r;   // key 0 (never used): the end
   if (n == 0 || !top) return MD5HIP_DESC_XDMA;
+  if (ngroups <= kLaneGroupsPerCu * (uint64_t)cu_count()) return MD5HIP_DESC_LANE;
   const uint32_t bmax = top - 1;
   if (bmax < kHybridLongBlocks) return MD5HIP_DESC_XDMA;
   return plan_choice(bmax, median, total, (uint32_t)(probe - 1));

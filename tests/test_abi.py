@@ -163,9 +163,10 @@ def test_plan_order_longest_first():
 
 
 def test_plan_desc_picks_hybrid_only_for_standout_long_chunks():
-    """md5hip_plan_desc: the same order as md5hip_plan_order, and HYBRID only
-    when the longest chunks (>= 256 KiB) stand out (the chunk two waves per CU
-    deep -- 256 CUs when no device is visible -- is <= 1/4 as long)."""
+    """md5hip_plan_desc: the same order as md5hip_plan_order; LANE for small
+    batches (<= 2 groups per CU -- 256 CUs when no device is visible); HYBRID
+    only when the longest chunks (>= 256 KiB) stand out (the chunk two waves
+    per CU deep is <= 1/4 as long)."""
     rng = np.random.default_rng(5)
     mixed = np.array([4096 << int(k) for k in rng.integers(0, 9, 80000)], dtype=np.uint32)
     order, v = m.plan_desc(mixed)
@@ -174,10 +175,19 @@ def test_plan_desc_picks_hybrid_only_for_standout_long_chunks():
     ragged = np.full(65536, 262144, np.uint32)
     ragged[::8] = rng.integers(1, 262144, 8192)
     assert m.plan_desc(ragged)[1] == "xdma"                # probe 32,768 deep is still full size
-    few = np.full(1000, 1 << 20, np.uint32)
+    few = np.full(40000, 1 << 20, np.uint32)
     few[-1] = 100
-    assert m.plan_desc(few)[1] == "hybrid"                 # fewer chunks than two waves per CU
-    assert m.plan_desc(np.full(5000, 65536, np.uint32))[1] == "xdma"              # < 256 KiB
+    assert m.plan_desc(few)[1] == "xdma"                   # long, but all of equal length
+    few[5000:] = 4096
+    assert m.plan_desc(few)[1] == "hybrid"                 # long chunks stand out
+    assert m.plan_desc(np.full(50000, 65536, np.uint32))[1] == "xdma"             # < 256 KiB
+    # small batches (<= 2 groups per CU, 256 CUs without a device): LANE
+    for n in (1, 64, 1000, 32768):
+        assert m.plan_desc(np.full(n, 16384, np.uint32))[1] == "lane", n
+    small_mixed = np.full(1000, 1 << 20, np.uint32)
+    small_mixed[-1] = 100
+    assert m.plan_desc(small_mixed)[1] == "lane"
+    assert m.plan_desc(np.full(32769, 16384, np.uint32))[1] == "xdma"
     assert m.plan_desc(np.array([], np.uint32))[0].size == 0
 
 
