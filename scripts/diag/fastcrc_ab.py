@@ -1,9 +1,10 @@
 #!/usr/bin/env python3
 """fastcrc (F = 128 / 64) on 1,048,576 x 16 KiB blocks: the product kernel
 (crc32_fast_pipe) against diagnostic depths -- window groups in flight per
-wave (md5diag_crc_fast_pipe: 2 @ 16 waves/CU, 3 @ 12, 4 @ 8, 2 @ 12) --
+wave (md5diag_crc_fast_pipe: 2 @ 16 waves/CU, 3 @ 12, 4 @ 8, 2 @ 12; and
+2 @ 16 with each window's halves loaded as two runs, the pre-round-3 order) --
 hipEvent ms per launch over interleaved rounds, results compared.
-usage: fastcrc_ab.py [--rounds R]"""
+usage: fastcrc_ab.py [--rounds R] [--F 128 64]"""
 import argparse
 import ctypes
 import json
@@ -17,12 +18,13 @@ sys.path.insert(0, REPO)
 from sproxy_amd import md5 as m  # noqa: E402
 
 DIAG = os.path.join(REPO, "build", "diag", "libmd5hip_diag.so")
-DEPTHS = {2: "d2_16w", 3: "d3_12w", 4: "d4_8w", 13: "d2_12w"}
+DEPTHS = {2: "d2_16w", 3: "d3_12w", 4: "d4_8w", 13: "d2_12w", 20: "d2_16w_runs"}
 
 
 def main():
     p = argparse.ArgumentParser()
     p.add_argument("--rounds", type=int, default=5)
+    p.add_argument("--F", type=int, nargs="*", default=[128, 64])
     a = p.parse_args()
     D = ctypes.CDLL(DIAG)
     vp = ctypes.c_void_p
@@ -33,7 +35,7 @@ def main():
     m.fill_synthetic(data, seed=0xFA)
     st = torch.cuda.current_stream().cuda_stream
     res = {}
-    for F in (128, 64):
+    for F in a.F:
         ref = m.crc32_fixed(data, n, L, fastcrc=F)
         outs = {k: torch.empty(n, dtype=torch.int32, device="cuda") for k in DEPTHS}
         run = lambda k: D.md5diag_crc_fast_pipe(k, data.data_ptr(), n, L, L, F, outs[k].data_ptr(), st)  # noqa

@@ -11,6 +11,10 @@
    (seed 1000), its 1 MiB chunks alone (the chain floor), and K coalesced
    batches.
 
+   Round 3 adds the exclusive split (md5diag_fed_split_excl): the longest
+   groups' pairs (or, as the control, HYBRID's lone chain waves) padded to a
+   whole CU's LDS so no XDMA wave of the rest shares their CU.
+
 Prints one JSON object.  usage: fed_ab.py [--rounds R] [--batches K ...]
 """
 import argparse
@@ -54,6 +58,7 @@ def main():
     D.md5diag_run.argtypes = [ci, vp, u64, u32, u64, vp, vp]
     D.md5diag_variant_desc.argtypes = [ci, vp, vp, vp, vp, u64, vp, vp]
     D.md5diag_fed_split.argtypes = [ci, vp, vp, vp, vp, u64, vp, vp]
+    D.md5diag_fed_split_excl.argtypes = [ci, u64, vp, vp, vp, vp, u64, vp, vp]
     st = torch.cuda.current_stream().cuda_stream
     res = {}
 
@@ -71,7 +76,10 @@ def main():
     res["chain_probe"] = probe
     print(json.dumps({"chain_probe": probe}), flush=True)
 
-    def fed(base, dO, dL, dR, n, dig, v=4):
+    def fed(base, dO, dL, dR, n, dig, v=4, L=0):
+        if v >= 200:   # exclusive chain CUs: 200 = fed pairs + XDMA, 201 = HYBRID part + XDMA
+            return D.md5diag_fed_split_excl(v - 200, L, base.data_ptr(), dO.data_ptr(), dL.data_ptr(),
+                                            dR.data_ptr(), n, dig.data_ptr(), st)
         if v >= 100:   # split launches: 100 = fed pairs + XDMA, 101 = HYBRID part + XDMA
             return D.md5diag_fed_split(v - 100, base.data_ptr(), dO.data_ptr(), dL.data_ptr(),
                                        dR.data_ptr(), n, dig.data_ptr(), st)
@@ -110,12 +118,17 @@ def main():
         dR = torch.from_numpy(order.astype(np.int32)).cuda()
         dig = torch.empty((n, 16), dtype=torch.uint8, device="cuda")
         ref = m.digest_desc(big, dO, dL, dR, variant="hybrid")
+        # the longest groups (first chunk of the group, in order, at the batch's maximum)
+        firsts = Lk[order[::64]]
+        Lmax = int((firsts == firsts.max()).sum())
         eq = []
-        for v in (4, 100, 101):
-            assert fed(big, dO, dL, dR, n, dig, v) == 0
+        for v in (4, 100, 101, 200, 201):
+            assert fed(big, dO, dL, dR, n, dig, v, Lmax) == 0
             torch.cuda.synchronize()
             eq.append(bool(torch.equal(dig, ref)))
         legs = {"hybrid": lambda: m.digest_desc(big, dO, dL, dR, out=dig, variant="hybrid"),
+                "fed_split_excl": lambda: fed(big, dO, dL, dR, n, dig, 200, Lmax),
+                "hybrid_split_excl": lambda: fed(big, dO, dL, dR, n, dig, 201, Lmax),
                 "fed_one_launch": lambda: fed(big, dO, dL, dR, n, dig, 4),
                 "fed_split": lambda: fed(big, dO, dL, dR, n, dig, 100),
                 "hybrid_split": lambda: fed(big, dO, dL, dR, n, dig, 101)}
@@ -126,6 +139,7 @@ def main():
             for k, f in legs.items():
                 ms[k] += timed(f, 1)
         entry = {"chunks": int(n), "payload_gib": round(float(Lk.sum()) / 2**30, 3), "planner": var,
+                 "excl_groups": Lmax,
                  "fed_equal_hybrid": eq, "ms": {k: [round(x, 3) for x in v] for k, v in ms.items()}}
         if K == 1:   # the 1 MiB chunks alone: the chain floor
             sel = np.nonzero(Lk == (1 << 20))[0]
@@ -135,7 +149,8 @@ def main():
             sd = torch.empty((sel.size, 16), dtype=torch.uint8, device="cuda")
             fl = {"hybrid": lambda: m.digest_desc(big, sO, sL, sR, out=sd, variant="hybrid"),
                   "fed_one_launch": lambda: fed(big, sO, sL, sR, sel.size, sd, 4),
-                  "fed_split": lambda: fed(big, sO, sL, sR, sel.size, sd, 100)}
+                  "fed_split": lambda: fed(big, sO, sL, sR, sel.size, sd, 100),
+                  "fed_excl": lambda: fed(big, sO, sL, sR, sel.size, sd, 202)}
             fms = {k: [] for k in fl}
             for _ in range(a.rounds):
                 for k, f in fl.items():

@@ -9,7 +9,11 @@ rounds; digests must equal XDMA's.  Prints one JSON object.
 With --crc: the product's CRC-32 launches on the same batches instead
 (crc32hip_desc through the descriptors, crc32hip_fixed on the contiguous
 layout), digests checked equal to each other.
-usage: small_batch_ab.py [--sizes 16,64,256,1024,4096] [--len 16384] [--iters 100] [--crc]"""
+With --fed: also the diagnostic library's fed pairs for every group
+(md5diag_variant_desc 9: a feeder wave forms M + K for the chain wave, 4 VALU
+per step on the chain instead of 5), and the same with each pair
+padded to a whole CU's LDS (md5diag_fed_split_excl 2).
+usage: small_batch_ab.py [--sizes 16,64,256,1024,4096] [--len 16384] [--iters 100] [--crc] [--fed]"""
 import argparse
 import ctypes
 import json
@@ -29,10 +33,18 @@ def main():
     ap.add_argument("--iters", type=int, default=100)
     ap.add_argument("--rounds", type=int, default=2)
     ap.add_argument("--crc", action="store_true")
+    ap.add_argument("--fed", action="store_true")
     a = ap.parse_args()
     import torch
     from sproxy_amd._lib import lib
     L = lib()
+    D = None
+    if a.fed:
+        D = ctypes.CDLL(os.path.join(REPO, "build", "diag", "libmd5hip_diag.so"), mode=ctypes.RTLD_LOCAL)
+        vp = ctypes.c_void_p
+        D.md5diag_variant_desc.argtypes = [ctypes.c_int, vp, vp, vp, vp, ctypes.c_uint64, vp, vp]
+        D.md5diag_fed_split_excl.argtypes = [ctypes.c_int, ctypes.c_uint64, vp, vp, vp, vp,
+                                             ctypes.c_uint64, vp, vp]
     stream = torch.cuda.Stream()
     sp = ctypes.c_void_p(stream.cuda_stream)
     out = {"len": a.len, "iters": a.iters, "sizes": {}}
@@ -43,7 +55,10 @@ def main():
     for n in (int(x) for x in a.sizes.split(",")):
         offs = torch.arange(n, dtype=torch.int64, device="cuda") * a.len
         lens = torch.full((n,), a.len, dtype=torch.int32, device="cuda")
-        variants = {"crc_desc": 0, "crc_fixed": 1} if a.crc else VARIANTS
+        variants = {"crc_desc": 0, "crc_fixed": 1} if a.crc else dict(VARIANTS)
+        if D is not None and not a.crc:
+            variants["fed"] = -9
+            variants["fed_excl"] = -1002
         dsz = 4 if a.crc else 16
         dig = {v: torch.zeros((n, dsz), dtype=torch.uint8, device="cuda") for v in variants}
         res = {v: [] for v in variants}
@@ -56,6 +71,10 @@ def main():
                         return L.crc32hip_desc(d, o, ln, None, n, 0, out_p, sp)
                     if a.crc:
                         return L.crc32hip_fixed(d, n, a.len, a.len, 0, out_p, sp)
+                    if code <= -1000:
+                        return D.md5diag_fed_split_excl(-code - 1000, 0, d, o, ln, None, n, out_p, sp)
+                    if code < 0:
+                        return D.md5diag_variant_desc(-code, d, o, ln, None, n, out_p, sp)
                     return L.md5hip_digest_desc_variant(d, o, ln, None, n, out_p, sp, code)
                 with torch.cuda.stream(stream):
                     for _ in range(20):

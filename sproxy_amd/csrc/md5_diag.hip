@@ -313,6 +313,62 @@ diag_chain_fed(uint32_t nblocks, uint4* __restrict__ out) {
   out[i] = make_uint4(st.a, st.b, st.c, st.d);
 }
 
+// Lone-chain step mixes (round 3, kinds 84-87).  The product step is
+// v_add / v_bitop3 / v_add3 / v_alignbit / v_add; v_add3 and v_alignbit cost
+// ~4.4 cycles per wave-instruction at full occupancy, v_add / v_bitop3 ~3.
+// Here every addition is a separate v_add_u32_e32 (pinned, so hipcc cannot form
+// v_add3; an asm volatile add would make hipcc pad with s_nop): kind 84 = 6 VALU per step (w+M, +K, f, +f, rotate, +x), kind 85
+// the fed step as 5 (w+W, f, +f, rotate, +x), against kinds 32 / 80.
+__device__ __forceinline__ uint32_t vadd(uint32_t a, uint32_t b) {
+  uint32_t r = a + b;
+  asm("" : "+v"(r));      // an empty pin (as md5_core.h kLat): no v_add3, no s_nop
+  return r;
+}
+__device__ __forceinline__ uint32_t vaddk(uint32_t a, uint32_t k) { return vadd(a, k); }
+template <bool kFed>
+__device__ __forceinline__ void compress_adds(State& st, const uint32_t (&m)[16]) {
+  uint32_t a = st.a, b = st.b, c = st.c, d = st.d;
+  // kFed: W[j] stands in for M[g(j)] + K[j]; otherwise M and K are added apart
+  auto W = [&](int j) __attribute__((always_inline)) -> uint32_t { return m[md5_msg_idx(j)]; };
+  auto step = [&](uint32_t& w, uint32_t x, uint32_t y, uint32_t z, int j, int s, int fn)
+      __attribute__((always_inline)) {
+    uint32_t t = vadd(w, W(j));
+    if constexpr (!kFed) t = vaddk(t, kMd5K[j]);
+    const uint32_t f = fn == 1 ? f1(x, y, z) : fn == 2 ? f2(x, y, z) : fn == 3 ? f3(x, y, z) : f4(x, y, z);
+    t = vadd(t, f);
+    w = x + rotl(t, s);     // not pinned: a pin before v_bitop3 costs an s_nop
+  };
+  constexpr int S[4][4] = {{7, 12, 17, 22}, {5, 9, 14, 20}, {4, 11, 16, 23}, {6, 10, 15, 21}};
+#pragma unroll
+  for (int j = 0; j < 64; j += 4) {
+    const int r = j >> 4;
+    step(a, b, c, d, j, S[r][0], r + 1);
+    step(d, a, b, c, j + 1, S[r][1], r + 1);
+    step(c, d, a, b, j + 2, S[r][2], r + 1);
+    step(b, c, d, a, j + 3, S[r][3], r + 1);
+  }
+  st.a += a;
+  st.b += b;
+  st.c += c;
+  st.d += d;
+}
+template <bool kFed>
+__global__ void __launch_bounds__(64)
+diag_chain_adds(uint32_t nblocks, uint4* __restrict__ out) {
+  const uint32_t i = blockIdx.x * 64u + threadIdx.x;
+  uint32_t m0[16];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) m0[k] = i * 2654435761u + 40503u * k;
+  State st = initial_state();
+  for (uint32_t b = 0; b < nblocks; ++b) {
+    uint32_t m[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) m[k] = m0[k] ^ b;     // off the chain, as diag_chain
+    compress_adds<kFed>(st, m);
+  }
+  out[i] = make_uint4(st.a, st.b, st.c, st.d);
+}
+
 // Two independent chains per lane in one instruction stream (kind 81): does
 // a lone wave issue faster when it has a second chain to interleave?  Same
 // message words as diag_chain (xor with the block index), kLat step.
@@ -887,6 +943,12 @@ extern "C" int md5diag_run(int kind, const void* base, uint64_t n, uint32_t len,
     case 80:   // n = workgroups, len = bytes per chain: the fed chain
       hipLaunchKernelGGL(diag_chain_fed, dim3((uint32_t)n), dim3(64), 0, s, len >> 6, o);
       break;
+    case 84:   // n = workgroups, len = bytes per chain: 6 single adds per step
+      hipLaunchKernelGGL(diag_chain_adds<false>, dim3((uint32_t)n), dim3(64), 0, s, len >> 6, o);
+      break;
+    case 85:   // the fed step with single adds (5 per step)
+      hipLaunchKernelGGL(diag_chain_adds<true>, dim3((uint32_t)n), dim3(64), 0, s, len >> 6, o);
+      break;
     case 13: case 14: {
       // single-chain latency: n lanes (one wave per CU at n = 16384), each
       // hashing `len` bytes; 64-thread workgroups so every CU gets one wave
@@ -1088,14 +1150,16 @@ extern "C" int md5diag_crc_fast_lane(const void* d_base, uint64_t n, uint32_t le
   return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }
 
-// fastcrc F = 64 / 128 with D window groups in flight per wave
+// fastcrc F = 64 / 128 with D window groups in flight per wave; P = false
+// loads a 128-B window as two runs of four 16-B loads (the order before
+// round 3's paired halves, depth code 20)
 namespace md5hip {
-template <int D, int T>
+template <int D, int T, bool P = true>
 __global__ void __launch_bounds__(T)
 diag_crc_fast_pipe(const uint8_t* __restrict__ base, uint64_t n, uint64_t stride, uint32_t flen,
                    uint32_t F, uint32_t* __restrict__ out) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[Crc32PermHasher::kLdsBytes];
-  fast_pipe_body<D>(base, nullptr, nullptr, n, stride, flen, F, out, lds);
+  fast_pipe_body<D, P>(base, nullptr, nullptr, n, stride, flen, F, out, lds);
 }
 }  // namespace md5hip
 
@@ -1111,6 +1175,7 @@ extern "C" int md5diag_crc_fast_pipe(int depth, const void* d_base, uint64_t n, 
   else if (depth == 3) hipLaunchKernelGGL((diag_crc_fast_pipe<3, 768>), g, dim3(768), 0, s, p, n, stride, len, fastcrc, d_out);
   else if (depth == 4) hipLaunchKernelGGL((diag_crc_fast_pipe<4, 512>), g, dim3(512), 0, s, p, n, stride, len, fastcrc, d_out);
   else if (depth == 13) hipLaunchKernelGGL((diag_crc_fast_pipe<2, 768>), g, dim3(768), 0, s, p, n, stride, len, fastcrc, d_out);
+  else if (depth == 20) hipLaunchKernelGGL((diag_crc_fast_pipe<2, 1024, false>), g, dim3(1024), 0, s, p, n, stride, len, fastcrc, d_out);
   else return -EINVAL;
   return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }
@@ -1242,6 +1307,11 @@ extern "C" int md5diag_variant_desc(int v, const void* d_base, const uint64_t* o
                        (uint4*)d_out, nlong);
     return hipGetLastError() == hipSuccess ? 0 : -EIO;
   }
+  if (v == 9) {   // every group of >= 2 blocks as a fed pair (small batches)
+    hipLaunchKernelGGL((md5_desc_fed_pairs<4, 2, 2>), dim3((uint32_t)((n + 63) / 64)), dim3(128), 0,
+                       (hipStream_t)stream, (const uint8_t*)d_base, offs, lens, order, n, (uint4*)d_out);
+    return hipGetLastError() == hipSuccess ? 0 : -EIO;
+  }
   if (v != 2) return -EINVAL;
   hipLaunchKernelGGL(md5_desc_xpose, dim3((uint32_t)((n + 63) / 64)), dim3(64), 0, (hipStream_t)stream,
                      (const uint8_t*)d_base, offs, lens, order, n, (uint4*)d_out);
@@ -1279,6 +1349,72 @@ extern "C" int md5diag_fed_split(int kind, const void* d_base, const uint64_t* o
                        order, nfirst, (uint4*)d_out);
   else
     hipLaunchKernelGGL(md5_desc_hybrid, dim3((uint32_t)L), dim3(64), 0, hs, b, offs, lens, order, nfirst,
+                       (uint4*)d_out, (uint32_t)L);
+  if (hipGetLastError() != hipSuccess) return -EIO;
+  if (n > nfirst)
+    hipLaunchKernelGGL(md5_desc_xdma, dim3((uint32_t)(groups - L)), dim3(64), 0, s, b, offs, lens,
+                       order + nfirst, n - nfirst, (uint4*)d_out);
+  if (hipGetLastError() != hipSuccess) return -EIO;
+  if (hipEventRecord(e1, hs) != hipSuccess || hipStreamWaitEvent(s, e1, 0) != hipSuccess) return -EIO;
+  return 0;
+}
+
+// Exclusive chain CUs.  As md5diag_fed_split, but the first L groups' pair
+// (kind 0: fed chain + feeder) or lone chain wave (kind 1: HYBRID's
+// lane-direct long wave, the control) is launched with its LDS padded to the
+// CU's whole 160 KiB, so no other workgroup -- in particular no XDMA wave of
+// the rest, launched beside it on `stream` -- shares its CU.  L is the
+// caller's (the longest groups, in order).  kind 2: every group a padded fed
+// pair, no rest (small batches; L ignored).
+namespace {
+int excl_pad(const void* k, uint32_t* pad) {
+  hipFuncAttributes at;
+  if (hipFuncGetAttributes(&at, k) != hipSuccess) return -EIO;
+  const uint32_t total = 160u * 1024u;
+  *pad = total > (uint32_t)at.sharedSizeBytes ? total - (uint32_t)at.sharedSizeBytes : 0u;
+  return hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)*pad) == hipSuccess
+             ? 0 : -EIO;
+}
+}  // namespace
+
+extern "C" int md5diag_fed_split_excl(int kind, uint64_t L, const void* d_base, const uint64_t* offs,
+                                      const uint32_t* lens, const uint32_t* order, uint64_t n,
+                                      void* d_out, void* stream) {
+  if (n == 0) return 0;
+  const uint8_t* b = (const uint8_t*)d_base;
+  const uint64_t groups = (n + 63) / 64;
+  if (kind == 2) {
+    const void* k = reinterpret_cast<const void*>(md5_desc_fed_pairs<4, 2, 2>);
+    uint32_t pad = 0;
+    if (int e = excl_pad(k, &pad)) return e;
+    hipLaunchKernelGGL((md5_desc_fed_pairs<4, 2, 2>), dim3((uint32_t)groups), dim3(128), pad,
+                       (hipStream_t)stream, b, offs, lens, order, n, (uint4*)d_out);
+    return hipGetLastError() == hipSuccess ? 0 : -EIO;
+  }
+  if (!order || L == 0) return -EINVAL;
+  static hipStream_t hs = nullptr;
+  static hipEvent_t e0 = nullptr, e1 = nullptr;
+  if (!hs) {
+    int lo = 0, hi = 0;
+    if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess ||
+        hipStreamCreateWithPriority(&hs, hipStreamNonBlocking, hi) != hipSuccess ||
+        hipEventCreateWithFlags(&e0, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&e1, hipEventDisableTiming) != hipSuccess)
+      return -ENODEV;
+  }
+  hipStream_t s = (hipStream_t)stream;
+  if (L > groups) L = groups;
+  const uint64_t nfirst = L * 64 < n ? L * 64 : n;
+  const void* k = kind == 0 ? reinterpret_cast<const void*>(md5_desc_fed_pairs<4, 2>)
+                            : reinterpret_cast<const void*>(md5_desc_hybrid);
+  uint32_t pad = 0;
+  if (int e = excl_pad(k, &pad)) return e;
+  if (hipEventRecord(e0, s) != hipSuccess || hipStreamWaitEvent(hs, e0, 0) != hipSuccess) return -EIO;
+  if (kind == 0)
+    hipLaunchKernelGGL((md5_desc_fed_pairs<4, 2>), dim3((uint32_t)L), dim3(128), pad, hs, b, offs, lens,
+                       order, nfirst, (uint4*)d_out);
+  else
+    hipLaunchKernelGGL(md5_desc_hybrid, dim3((uint32_t)L), dim3(64), pad, hs, b, offs, lens, order, nfirst,
                        (uint4*)d_out, (uint32_t)L);
   if (hipGetLastError() != hipSuccess) return -EIO;
   if (n > nfirst)

@@ -969,7 +969,12 @@ crc32_fast_xdma16(const uint8_t* __restrict__ base, const uint64_t* __restrict__
 // flight beside it.  Persistent: one 1024-thread workgroup per CU, groups
 // wave-major, grid-stride.
 // D: window groups in flight per wave (D-1 loaded ahead of the one hashed).
-template <int D>
+// kPairHalves: a 128-B window's two 64-B halves are requested in alternating
+// instructions (bytes 0, 64, 16, 80, ...), so the second half of a line
+// reaches L2 while the first half's fill is still pending there; loaded as
+// two runs of four (0..48, then 64..112), 15 % of second halves found their
+// line already evicted and fetched it again.
+template <int D, bool kPairHalves = true>
 __device__ __forceinline__ void fast_pipe_body(const uint8_t* __restrict__ base,
                                                const uint64_t* __restrict__ offs,
                                                const uint32_t* __restrict__ lens, uint64_t n,
@@ -1001,8 +1006,19 @@ __device__ __forceinline__ void fast_pipe_body(const uint8_t* __restrict__ base,
     return w;
   };
   auto fetch = [&](const Win& w, uint4 (&W)[2][4]) __attribute__((always_inline)) {
-    load_block(W[0], reinterpret_cast<const uint4*>(w.p));
-    if (nb == 2) load_block(W[1], reinterpret_cast<const uint4*>(w.p + 64));
+    const uint4* q = reinterpret_cast<const uint4*>(w.p);
+    if (kPairHalves && nb == 2) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {      // the barriers keep hipcc from sorting by offset
+        W[0][k] = ld16(q + k);
+        __builtin_amdgcn_sched_barrier(0);
+        W[1][k] = ld16(q + 4 + k);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    } else {
+      load_block(W[0], q);
+      if (nb == 2) load_block(W[1], q + 4);
+    }
   };
   auto hash = [&](const Win& w, uint64_t gi, uint4 (&W)[2][4]) __attribute__((always_inline)) {
     typename Crc32PermHasher::State st = h.init();

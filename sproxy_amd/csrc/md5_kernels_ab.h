@@ -770,8 +770,10 @@ md5_desc_hybrid_fed(const uint8_t* __restrict__ base, const uint64_t* __restrict
 // workgroups), for a split launch: the rest goes to md5_desc_xdma on the
 // caller's stream while this kernel runs on a high-priority stream, so the
 // XDMA waves get the ordinary one-wave workgroups and 8 KiB images and the
-// pairs their 32 KiB (md5diag_fed_split).
-template <int D = 4, int NT = 2>
+// pairs their 32 KiB (md5diag_fed_split).  kMinBlocks = 2: every aligned
+// group of at least two blocks runs as a pair (small batches, where each
+// wave is nearly alone on its SIMD; md5diag_variant_desc 9).
+template <int D = 4, int NT = 2, uint32_t kMinBlocks = kHybridLongBlocks>
 __global__ void __launch_bounds__(128)
 md5_desc_fed_pairs(const uint8_t* __restrict__ base, const uint64_t* __restrict__ offs,
                    const uint32_t* __restrict__ lens, const uint32_t* __restrict__ order, uint64_t n,
@@ -790,7 +792,7 @@ md5_desc_fed_pairs(const uint8_t* __restrict__ base, const uint64_t* __restrict_
   const uint32_t nfull = len >> 6;
   const uint32_t bmax = wave_max(nfull);
   const bool unaligned = __ballot(live && ((((uintptr_t)base + off) & 15u) != 0)) != 0;
-  if (bmax >= kHybridLongBlocks && !unaligned) {
+  if (bmax >= kMinBlocks && !unaligned) {
     fed_long_group<D, NT>(base, out, lds, wave == 1, nfull, bmax, off, len, c, live);
     return;
   }
