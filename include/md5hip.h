@@ -87,7 +87,12 @@ enum md5hip_desc_variant {
                                taking 64-chunk groups longest-first (LPT list scheduling):
                                the planner's choice for mixed batches holding several
                                waves of work per SIMD (coalesced submissions) */
-    MD5HIP_DESC_NUM_VARIANTS = 6
+    MD5HIP_DESC_FED = 6,    /* one 2-wave workgroup per 64-chunk group: a feeder wave forms
+                               each step's message word + constant, so the chain wave runs
+                               4 VALU per step instead of 5; groups holding an unaligned
+                               chunk start (or no chunk of >= 128 B) go LANE.  The
+                               planner's choice for small batches (round 3) */
+    MD5HIP_DESC_NUM_VARIANTS = 7
 };
 int md5hip_digest_desc_variant(const void *d_base, const uint64_t *d_offsets,
                                const uint32_t *d_lens, const uint32_t *d_order, uint64_t n,
@@ -166,9 +171,11 @@ int md5hip_arena_free(void *d_ptr);
 /*
  * Host planner for a descriptor batch: fills order[] as md5hip_plan_order and
  * returns the enum md5hip_desc_variant to launch it with (>= 0), or -errno.
- * LANE for a small batch (at most two 64-chunk groups per CU of the current
- * device: the launch is one chunk's serial chain, which lane-direct loads
- * keep free of load waits).  Otherwise, with the longest chunk >= 256 KiB and the median 64-chunk group at most an
+ * FED for a small batch of at most one 64-chunk group per CU of the current
+ * device whose longest chunk has >= 2 whole blocks, LANE for one of at most
+ * two groups per CU (the launch is one chunk's serial chain: FED takes an
+ * instruction per step off it, lane-direct loads keep it free of load
+ * waits).  Otherwise, with the longest chunk >= 256 KiB and the median 64-chunk group at most an
  * eighth of the longest (a mixed batch): BALANCED when the batch holds at
  * least 0.4 x (SIMDs x the longest chain) of work, so the placement of waves
  * on SIMDs decides the time; else HYBRID when the longest chunks stand out

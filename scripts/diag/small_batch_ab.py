@@ -23,7 +23,7 @@ import sys
 REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, REPO)
 
-VARIANTS = {"xdma": 4, "lane": 1, "hybrid": 3, "balanced": 5}
+VARIANTS = {"xdma": 4, "lane": 1, "hybrid": 3, "balanced": 5, "fed": 6}
 
 
 def main():
@@ -57,7 +57,7 @@ def main():
         lens = torch.full((n,), a.len, dtype=torch.int32, device="cuda")
         variants = {"crc_desc": 0, "crc_fixed": 1} if a.crc else dict(VARIANTS)
         if D is not None and not a.crc:
-            variants["fed"] = -9
+            variants["fed_diag"] = -9
             variants["fed_excl"] = -1002
         dsz = 4 if a.crc else 16
         dig = {v: torch.zeros((n, dsz), dtype=torch.uint8, device="cuda") for v in variants}

@@ -773,6 +773,266 @@ md5_desc_hybrid(const uint8_t* __restrict__ base, const uint64_t* __restrict__ o
 }
 
 // ---------------------------------------------------------------------------
+// Pre-summed schedule ("fed" chains).  The same 64 steps with the per-step
+// addend W[j] = M[kMsgIdx[j]] + K[j] supplied by someone else (md5_w below,
+// in another wave), so a step is 4 VALU -- v_bitop3, v_add3 (w + W + f),
+// v_alignbit, v_add -- instead of 5: the lone wave that runs a long chunk's
+// serial chain is issue-bound, and the fifth op moves to the feeding wave.
+// ---------------------------------------------------------------------------
+// message word of step j (md5.c:74-139: rounds 1-4 index schedules)
+__host__ __device__ constexpr int md5_msg_idx(int j) {
+  return j < 16 ? j : j < 32 ? (1 + 5 * j) & 15 : j < 48 ? (5 + 3 * j) & 15 : (7 * j) & 15;
+}
+// step j's T constant (the RFC 1321 table, as in compress above)
+__device__ constexpr uint32_t kMd5K[64] = {
+    0xd76aa478u, 0xe8c7b756u, 0x242070dbu, 0xc1bdceeeu, 0xf57c0fafu, 0x4787c62au, 0xa8304613u,
+    0xfd469501u, 0x698098d8u, 0x8b44f7afu, 0xffff5bb1u, 0x895cd7beu, 0x6b901122u, 0xfd987193u,
+    0xa679438eu, 0x49b40821u, 0xf61e2562u, 0xc040b340u, 0x265e5a51u, 0xe9b6c7aau, 0xd62f105du,
+    0x02441453u, 0xd8a1e681u, 0xe7d3fbc8u, 0x21e1cde6u, 0xc33707d6u, 0xf4d50d87u, 0x455a14edu,
+    0xa9e3e905u, 0xfcefa3f8u, 0x676f02d9u, 0x8d2a4c8au, 0xfffa3942u, 0x8771f681u, 0x6d9d6122u,
+    0xfde5380cu, 0xa4beea44u, 0x4bdecfa9u, 0xf6bb4b60u, 0xbebfbc70u, 0x289b7ec6u, 0xeaa127fau,
+    0xd4ef3085u, 0x04881d05u, 0xd9d4d039u, 0xe6db99e5u, 0x1fa27cf8u, 0xc4ac5665u, 0xf4292244u,
+    0x432aff97u, 0xab9423a7u, 0xfc93a039u, 0x655b59c3u, 0x8f0ccc92u, 0xffeff47du, 0x85845dd1u,
+    0x6fa87e4fu, 0xfe2ce6e0u, 0xa3014314u, 0x4e0811a1u, 0xf7537e82u, 0xbd3af235u, 0x2ad7d2bbu,
+    0xeb86d391u};
+
+// The 64 addends of one block, 4 per uint4 in step order: q[j >> 2] lane j & 3.
+__device__ __forceinline__ void md5_w(const uint4 (&m)[4], uint4 (&q)[16]) {
+  auto M = [&](int i) __attribute__((always_inline)) -> uint32_t {
+    const uint4& v = m[i >> 2];
+    return (i & 3) == 0 ? v.x : (i & 3) == 1 ? v.y : (i & 3) == 2 ? v.z : v.w;
+  };
+#pragma unroll
+  for (int t = 0; t < 16; ++t)
+    q[t] = make_uint4(M(md5_msg_idx(4 * t)) + kMd5K[4 * t], M(md5_msg_idx(4 * t + 1)) + kMd5K[4 * t + 1],
+                      M(md5_msg_idx(4 * t + 2)) + kMd5K[4 * t + 2],
+                      M(md5_msg_idx(4 * t + 3)) + kMd5K[4 * t + 3]);
+}
+
+#define MD5HIP_FSTEP(F, w, x, y, z, W, s) w = x + rotl(w + (W) + F(x, y, z), s)
+
+// Steps 4*T0 .. 4*T1-1 of one block from its pre-summed addends (md5_w).  A
+// quad of steps leaves the roles (a, b, c, d) where it found them, so a block
+// can be split at any quad (the fed chain wave passes a barrier mid-block).
+template <int T0, int T1>
+__device__ __forceinline__ void fed_steps(uint32_t& a, uint32_t& b, uint32_t& c, uint32_t& d,
+                                          const uint4 (&q)[16]) {
+#pragma unroll
+  for (int t = T0; t < T1; ++t) {
+    const uint4 v = q[t];
+    if (t < 4) {
+      MD5HIP_FSTEP(f1, a, b, c, d, v.x, 7);
+      MD5HIP_FSTEP(f1, d, a, b, c, v.y, 12);
+      MD5HIP_FSTEP(f1, c, d, a, b, v.z, 17);
+      MD5HIP_FSTEP(f1, b, c, d, a, v.w, 22);
+    } else if (t < 8) {
+      MD5HIP_FSTEP(f2, a, b, c, d, v.x, 5);
+      MD5HIP_FSTEP(f2, d, a, b, c, v.y, 9);
+      MD5HIP_FSTEP(f2, c, d, a, b, v.z, 14);
+      MD5HIP_FSTEP(f2, b, c, d, a, v.w, 20);
+    } else if (t < 12) {
+      MD5HIP_FSTEP(f3, a, b, c, d, v.x, 4);
+      MD5HIP_FSTEP(f3, d, a, b, c, v.y, 11);
+      MD5HIP_FSTEP(f3, c, d, a, b, v.z, 16);
+      MD5HIP_FSTEP(f3, b, c, d, a, v.w, 23);
+    } else {
+      MD5HIP_FSTEP(f4, a, b, c, d, v.x, 6);
+      MD5HIP_FSTEP(f4, d, a, b, c, v.y, 10);
+      MD5HIP_FSTEP(f4, c, d, a, b, v.z, 15);
+      MD5HIP_FSTEP(f4, b, c, d, a, v.w, 21);
+    }
+  }
+}
+#undef MD5HIP_FSTEP
+
+// One block from its 64 pre-summed addends: MD5Transform, md5.c:63-146.
+__device__ __forceinline__ void compress_fed(State& st, const uint4 (&q)[16]) {
+  uint32_t a = st.a, b = st.b, c = st.c, d = st.d;
+  fed_steps<0, 16>(a, b, c, d, q);
+  st.a += a;  // feed-forward, md5.c:142-145
+  st.b += b;
+  st.c += c;
+  st.d += d;
+}
+
+// ---------------------------------------------------------------------------
+// Fed chains (HYBRID's long groups, two waves each).  A lone wave running 64
+// long chunks' serial chains is bound by its own VALU issue: ~20 cycles per
+// step for 5 VALU (the off-chain a + M + K included; profiles/
+// r01_chain_probe.json).  Here a second wave of the workgroup -- the feeder,
+// on another SIMD -- streams the same 64 chunks lane-direct, forms each
+// block's 64 addends M[g(j)] + K[j] (md5_w) and hands them over through LDS
+// tables of [16 quads][64 lanes] x 16 B (both sides conflict-free); the chain
+// wave reads a block's addends with 16 ds_read_b128 and runs 4 VALU per step
+// (compress_fed).
+//
+// NT = 2 tables, one s_barrier per block (both waves execute 1 + bmax):
+//   chain : X_k | read W(k+1) from T[(k+1)&1] | block k from registers
+//   feeder: X_k | write W(k+2) into T[k&1]
+// At X_k the chain's reads of W(k) (from T[k&1], issued in iteration k-1)
+// have returned and the feeder's W(k+1) is written, so each side has a whole
+// block of slack.  NT = 1 table (16 KiB: a 2-wave workgroup then needs no more
+// LDS than two XDMA waves), two s_barriers per block (2 + 2 * bmax):
+//   chain : B_k | read W(k+1) | steps 0-15 of block k | A_k | steps 16-63
+//   feeder: B_k | A_k | write W(k+2) (under the chain's steps 16-63)  The barrier is bare (s_waitcnt lgkmcnt(0); s_barrier): a
+// workgroup fence would also drain the feeder's global-load ring.  Lanes past
+// their own last block keep computing on whatever the feeder clamped to and
+// discard the result, so no branch ever skips a barrier.
+// kFeedOff (diagnostics): the feeder only keeps the barriers (digests wrong).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void lds_handoff() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+// the same, pinning the chain state: steps cannot move across it
+__device__ __forceinline__ void lds_handoff(uint32_t& a, uint32_t& b, uint32_t& c, uint32_t& d) {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" : "+v"(a), "+v"(b), "+v"(c), "+v"(d) :: "memory");
+}
+
+constexpr uint32_t kFedTable = 16 * 64 * 16;     // one block's addends, 16 KiB
+
+template <int D, int NT, bool kFeedOff = false>
+__device__ __forceinline__ void fed_long_group(const uint8_t* __restrict__ base, uint4* __restrict__ out,
+                                               uint8_t* lds, bool feeder, uint32_t nfull,
+                                               uint32_t bmax, uint64_t off, uint32_t len,
+                                               uint64_t c, bool live) {
+  static_assert(D % 2 == 0, "paired refill");
+  const uint8_t* chunk = base + off;
+  const uint32_t lane = threadIdx.x & 63u;
+  auto tab = [&](uint32_t k) __attribute__((always_inline)) {
+    return reinterpret_cast<uint4(*)[64]>(lds + (NT == 2 ? (k & 1u) * kFedTable : 0u));
+  };
+  __builtin_amdgcn_s_setprio(3);
+  if (feeder) {
+    // lanes without a whole block stream the wave's longest chunk (in bounds)
+    // (base + offset keeps the loads global: a flat load would also count in
+    // lgkmcnt, and every hand-over would drain the ring)
+    const uint32_t mlane = __builtin_ctzll(__ballot(nfull == bmax));
+    const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)off, (int)mlane, 64);
+    const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(off >> 32), (int)mlane, 64);
+    const uint4* p = reinterpret_cast<const uint4*>(base + (nfull ? off : ((uint64_t)hi << 32) | lo));
+    const uint32_t lastb = (nfull ? nfull : bmax) - 1u;
+    uint4 R[D][4];
+    if constexpr (!kFeedOff) {
+#pragma unroll
+      for (int j = 0; j < D; ++j) load_block(R[j], p + 4 * min((uint32_t)j, lastb));
+    }
+    // W(k) into T[k&1] from ring slot k % D; odd slots refill their pair
+    // (blocks k-1+D, k+D: one whole 128-B line when the chunk is line-aligned)
+    auto put = [&](uint32_t k, int slot) __attribute__((always_inline)) {
+      if constexpr (!kFeedOff) {
+        uint4 q[16];
+        md5_w(R[slot], q);
+        uint4 (*t)[64] = tab(k);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) t[i][lane] = q[i];
+        if (slot & 1) {
+          load_block(R[slot - 1], p + 4 * min(k - 1 + D, lastb));
+          load_block(R[slot], p + 4 * min(k + D, lastb));
+        }
+      }
+    };
+    put(0, 0);
+    if constexpr (NT == 1) {
+      lds_handoff();                             // B_init: W(0) in
+      lds_handoff();                             // A_init: W(0) read
+    }
+    put(1, 1);
+    lds_handoff();                               // X_init / B_0: W(1) in
+    for (uint32_t k0 = 0; k0 < bmax; k0 += D) {
+#pragma unroll
+      for (int j = 0; j < D; ++j) {
+        const uint32_t k = k0 + j;
+        if (k < bmax) {                          // wave-uniform
+          if constexpr (NT == 1) lds_handoff();  // A_k
+          else lds_handoff();                    // X_k
+          if (k + 2 < bmax) put(k + 2, (j + 2) % D);
+          if constexpr (NT == 1) {
+            if (k + 1 < bmax) lds_handoff();     // B_{k+1}
+          }
+        }
+      }
+    }
+    return;
+  }
+  State st = initial_state();
+  uint4 q[2][16];                                // W(k) and W(k+1), alternating
+  lds_handoff();                                 // X_init / B_init
+#pragma unroll
+  for (int i = 0; i < 16; ++i) q[0][i] = tab(0)[i][lane];
+  if constexpr (NT == 1) lds_handoff();          // A_init
+  auto blk = [&](uint32_t k, uint4 (&cur)[16], uint4 (&nxt)[16]) __attribute__((always_inline)) {
+    uint32_t a = st.a, b = st.b, cc = st.c, d = st.d;
+    lds_handoff(a, b, cc, d);                    // X_k / B_k
+    uint4 (*t)[64] = tab(k + 1);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) nxt[i] = t[i][lane];
+    __builtin_amdgcn_sched_barrier(0);           // all 16 reads out before the steps
+    if constexpr (NT == 1) {
+      fed_steps<0, 4>(a, b, cc, d, cur);
+      lds_handoff(a, b, cc, d);                  // A_k: the reads of W(k+1) are in
+      fed_steps<4, 16>(a, b, cc, d, cur);
+    } else {
+      fed_steps<0, 16>(a, b, cc, d, cur);
+    }
+    const bool act = k < nfull;
+    st.a = act ? st.a + a : st.a;
+    st.b = act ? st.b + b : st.b;
+    st.c = act ? st.c + cc : st.c;
+    st.d = act ? st.d + d : st.d;
+  };
+  for (uint32_t k = 0; k < bmax; k += 2) {
+    blk(k, q[0], q[1]);
+    if (k + 1 < bmax) blk(k + 1, q[1], q[0]);    // wave-uniform
+  }
+  if (live) {
+    Md5Hasher<true> h;
+    h.finish(st, chunk + ((uint64_t)nfull << 6), len & 63u, len);
+    h.store(out, c, st);
+  }
+}
+
+// Small batches as fed pairs ("FED", round 3): one 2-wave workgroup per
+// 64-chunk group.  A netcache vector (16-16,384 blocks) is at most one group
+// per CU, each wave nearly alone on its SIMD, and the launch lasts one
+// chunk's serial chain -- bound by the chain wave's own VALU issue, ~4.3
+// cycles per instruction whatever the opcode (profiles/r03r/chain_mix.json).
+// The feeder wave (another SIMD, idle otherwise) forms every step's
+// M[g(j)] + K[j], so the chain runs 4 VALU per step instead of 5: 147 ->
+// 138 us for 64-4,096 x 16 KiB, 41 -> 38.6 us at 4 KiB
+// (profiles/r03q/small_fed_*.json).  A group holding a chunk start that is
+// not 16-B aligned, or no chunk of two whole blocks, runs LANE's lane-direct
+// body on wave 0 instead.
+constexpr uint32_t kFedMinBlocks = 2;
+
+__global__ void __launch_bounds__(128)
+md5_desc_fed(const uint8_t* __restrict__ base, const uint64_t* __restrict__ offs,
+             const uint32_t* __restrict__ lens, const uint32_t* __restrict__ order, uint64_t n,
+             uint4* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds[2 * kFedTable];
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const DescArrays src{offs, lens, order};
+  const uint64_t first = (uint64_t)blockIdx.x * 64u;
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint64_t i = first + lane;
+  const bool live = i < n;
+  const uint64_t c = src.index(live ? i : first);
+  const uint64_t off = src.off(c);
+  const uint32_t len = live ? src.len(c) : 0u;
+  const uint32_t nfull = len >> 6;
+  const uint32_t bmax = wave_max(nfull);
+  const bool unaligned = __ballot(live && ((((uintptr_t)base + off) & 15u) != 0)) != 0;
+  if (bmax >= kFedMinBlocks && !unaligned) {     // wave-uniform, the same in both waves
+    fed_long_group<4, 2>(base, out, lds, wave == 1, nfull, bmax, off, len, c, live);
+    return;
+  }
+  if (wave != 0 || !live) return;
+  Md5Hasher<true> h;
+  typename Md5Hasher<true>::State st = h.init();
+  lane_range<Md5Hasher<true>, 8>(h, st, base + off, len);
+  h.store(out, c, st);
+}
+
+// ---------------------------------------------------------------------------
 // Descriptor batch, LPT-scheduled ("BALANCED"): a persistent grid of ONE wave
 // per SIMD (4-wave workgroups holding more than half a CU's LDS, so each CU
 // runs exactly one) pulls 64-chunk groups in longest-first order from a

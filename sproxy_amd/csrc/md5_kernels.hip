@@ -158,7 +158,7 @@ int md5hip_digest_desc_variant(const void* d_base, const uint64_t* d_offsets,
   if (!d_base || !d_offsets || !d_lens || !d_digests) return -EINVAL;
   if (((uintptr_t)d_digests & 15u) != 0) return -EINVAL;
   if (variant != MD5HIP_DESC_AUTO && variant != MD5HIP_DESC_LANE && variant != MD5HIP_DESC_HYBRID &&
-      variant != MD5HIP_DESC_XDMA && variant != MD5HIP_DESC_BALANCED)
+      variant != MD5HIP_DESC_XDMA && variant != MD5HIP_DESC_BALANCED && variant != MD5HIP_DESC_FED)
     return -EINVAL;
   if (int e = device_ok()) return e;
   const uint64_t g = (n + 63) / 64;
@@ -184,6 +184,12 @@ int md5hip_digest_desc_variant(const void* d_base, const uint64_t* d_offsets,
     if (hipMemsetAsync(ctr, 0, 4 * sizeof(uint32_t), s) != hipSuccess) return -EIO;
     hipLaunchKernelGGL(kern, dim3((uint32_t)cu_count()), dim3(64 * WPB), lds, s,
                        base, d_offsets, d_lens, d_order, n, (uint4*)d_digests, ctr);
+    return launched();
+  }
+  if (variant == MD5HIP_DESC_FED) {
+    // chain + feeder wave per 64-chunk group (md5_kernels.h md5_desc_fed)
+    hipLaunchKernelGGL(md5_desc_fed, dim3((uint32_t)g), dim3(128), 0, s, base, d_offsets, d_lens,
+                       d_order, n, (uint4*)d_digests);
     return launched();
   }
   if (variant == MD5HIP_DESC_AUTO || variant == MD5HIP_DESC_XDMA) {
@@ -545,8 +551,19 @@ int md5hip_arena_free(void* ptr) {
 // 206 us; profiles/r03/small_batch_kernels_*.json).
 constexpr uint64_t kLaneGroupsPerCu = 2;
 
+// Of those, batches of at most one group per CU run as fed pairs (FED: the
+// chain wave's 5th VALU per step moves to a feeder wave on another SIMD; 147
+// -> 138 us at 64-4,096 x 16 KiB, 150.6 -> 141 at 16,384;
+// profiles/r03q/small_fed_16k.json) when some chunk has two whole blocks.
+constexpr uint64_t kFedGroupsPerCu = 1;
+static int small_choice(uint64_t ngroups, uint32_t bmax) {
+  if (ngroups <= kFedGroupsPerCu * (uint64_t)cu_count() && bmax >= kFedMinBlocks)
+    return MD5HIP_DESC_FED;
+  return MD5HIP_DESC_LANE;
+}
+
 // Planner for descriptor batches (md5hip.h): the longest-first order, and
-//  - LANE for small batches (above);
+//  - FED / LANE for small batches (above);
 //  - BALANCED for a mixed batch (longest chunk >= 256 KiB, median 64-chunk
 //    group <= 1/8 of it) holding >= 0.4 x (SIMDs x longest chain) of work:
 //    several waves per SIMD, where LPT placement beats the hardware's
@@ -559,8 +576,8 @@ int md5hip_plan_desc(const uint32_t* lens, uint64_t n, uint32_t* order) {
   if (int e = md5hip_plan_order(lens, n, order)) return e;
   if (n == 0) return MD5HIP_DESC_XDMA;
   const uint64_t ngroups = (n + 63) / 64;
-  if (ngroups <= kLaneGroupsPerCu * (uint64_t)cu_count()) return MD5HIP_DESC_LANE;
   const uint32_t bmax = lens[order[0]] >> 6;
+  if (ngroups <= kLaneGroupsPerCu * (uint64_t)cu_count()) return small_choice(ngroups, bmax);
   if (bmax < kHybridLongBlocks) return MD5HIP_DESC_XDMA;
   const uint64_t median = (uint64_t)(lens[order[(ngroups / 2) * 64]] >> 6) + 1;
   uint64_t total = 0;           // work in block-steps: a group runs as long as its first lane
@@ -594,8 +611,8 @@ int md5hip_plan_hist(const uint32_t* hist, uint32_t kmax, uint64_t n, uint32_t* 
   }
   if (bucket_start) bucket_start[kmax] = (uint32_t)r;   // key 0 (never used): the end
   if (n == 0 || !top) return MD5HIP_DESC_XDMA;
-  if (ngroups <= kLaneGroupsPerCu * (uint64_t)cu_count()) return MD5HIP_DESC_LANE;
   const uint32_t bmax = top - 1;
+  if (ngroups <= kLaneGroupsPerCu * (uint64_t)cu_count()) return small_choice(ngroups, bmax);
   if (bmax < kHybridLongBlocks) return MD5HIP_DESC_XDMA;
   return plan_choice(bmax, median, total, (uint32_t)(probe - 1));
 }

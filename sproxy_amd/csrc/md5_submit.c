@@ -213,6 +213,7 @@ struct slot {
     uint32_t last_key;
     int unsorted, use_order;
     uint64_t opened_us, launched_us;  /* first chunk reserved / went in flight */
+    uint64_t gen;                     /* launches of this slot so far (a waiter's check) */
     uint64_t load;                    /* this slot's share of b->load_bytes */
 };
 
@@ -265,16 +266,17 @@ static uint64_t linger_us(const md5hip_batcher *b)
     return l < (double)b->linger_max_us ? (uint64_t)l : (uint64_t)b->linger_max_us;
 }
 
-/* pthread_cond_timedwait on work_cv until `us` microseconds from now (mu held) */
-static void wait_work_us(md5hip_batcher *b, uint64_t us)
+/* pthread_cond_timedwait on cv until `us` microseconds from now (mu held) */
+static void wait_cv_us(md5hip_batcher *b, pthread_cond_t *cv, uint64_t us)
 {
     struct timespec ts;
     clock_gettime(CLOCK_REALTIME, &ts);
     ts.tv_sec += (time_t)(us / 1000000u);
     ts.tv_nsec += (long)(us % 1000000u) * 1000;
     if (ts.tv_nsec >= 1000000000L) { ts.tv_sec++; ts.tv_nsec -= 1000000000L; }
-    pthread_cond_timedwait(&b->work_cv, &b->mu, &ts);
+    pthread_cond_timedwait(cv, &b->mu, &ts);
 }
+static void wait_work_us(md5hip_batcher *b, uint64_t us) { wait_cv_us(b, &b->work_cv, us); }
 
 /* ticket table (md5_tickets.h), all under b->mu */
 static int tk_new(md5hip_batcher *b, uint64_t *t) { return tk_ring_new(&b->tk, t); }
@@ -489,6 +491,7 @@ static void slot_try_launch(md5hip_batcher *b, struct slot *sl)
     }
     sl->state = SLOT_INFLIGHT;
     sl->launched_us = now_us();
+    sl->gen++;
     b->inflight++;
     b->st.launches++;
     b->st.chunks += sl->n;
@@ -611,6 +614,57 @@ static void *progress_main(void *arg)
     }
     pthread_mutex_unlock(&b->mu);
     return NULL;
+}
+
+/* ------------------------------------------------------------------------
+ * A blocked caller watches its own launch.  Waiting on done_cv alone, a
+ * synchronous call returns up to one progress-thread poll (10 us) plus a
+ * condition-variable wake-up after its kernel ends; for a netcache vector
+ * (a ~140 us kernel) that was 20-30 us of each call.  So a thread blocked on
+ * ticket t whose launch is in flight and expected to end soon (recent
+ * launches' wall time) polls that launch's event itself and retires the slot
+ * when it completes; a launch expected to run much longer is slept through
+ * first.  The spin is bounded; past it the thread blocks on done_cv as before.
+ * ------------------------------------------------------------------------ */
+enum { WATCH_SPIN_US = 300, WATCH_LEAD_US = 200 };
+
+static void cpu_relax(void)
+{
+#if defined(__x86_64__) || defined(__i386__)
+    __builtin_ia32_pause();
+#endif
+}
+
+/* mu held on entry and exit; 1 = progress may have been made (re-check the
+ * ticket), 0 = nothing to watch (block on done_cv). */
+static int watch_own_launch(md5hip_batcher *b, uint64_t t)
+{
+    struct slot *sl = NULL;
+    for (uint32_t k = 0; k < b->nslots && !sl; k++)
+        if (b->s[k].state == SLOT_INFLIGHT && seg_has(&b->s[k], t)) sl = &b->s[k];
+    if (!sl) return 0;
+    const uint64_t gen = sl->gen, now = now_us();
+    const uint64_t end = sl->launched_us + (uint64_t)b->launch_ema_us;
+    if (end > now + WATCH_SPIN_US) {            /* long launch: sleep most of it */
+        wait_cv_us(b, &b->done_cv, end - now - WATCH_LEAD_US);
+        return 1;
+    }
+    const hipEvent_t ev = sl->done;
+    pthread_mutex_unlock(&b->mu);
+    hipError_t e;
+    const uint64_t t0 = now_us();
+    while ((e = hipEventQuery(ev)) == hipErrorNotReady && now_us() - t0 < WATCH_SPIN_US + WATCH_LEAD_US)
+        cpu_relax();
+    pthread_mutex_lock(&b->mu);
+    if (e == hipErrorNotReady) return 0;
+    /* the same launch still in flight (the progress thread may have retired
+     * it, and the slot may even be in flight again with other work) */
+    if (sl->state == SLOT_INFLIGHT && sl->gen == gen) {
+        slot_retire(b, sl, e == hipSuccess ? 0 : -EIO);
+        if (b->open >= 0) slot_try_launch(b, &b->s[b->open]);
+        pthread_cond_broadcast(&b->work_cv);
+    }
+    return 1;
 }
 
 /* ------------------------------------------------------------------------
@@ -1165,7 +1219,8 @@ static int submit(md5hip_batcher *b, const struct chunk_src *src, uint64_t n, un
                     b->s[k].flush = 1;       /* a synchronous caller: at once */
                     slot_try_launch(b, &b->s[k]);
                 }
-            pthread_cond_wait(&b->done_cv, &b->mu);
+            if (!tk_done(b, t, &err) && !watch_own_launch(b, t))
+                pthread_cond_wait(&b->done_cv, &b->mu);
         }
         b->waiters--;
         if (!rc) rc = err;
@@ -1203,7 +1258,8 @@ int md5_batch_wait(md5hip_batcher *b, uint64_t ticket)
         pthread_cond_broadcast(&b->work_cv);        /* the progress thread polls fast now */
         while (!tk_done(b, ticket, &err)) {
             hasten(b, ticket);
-            pthread_cond_wait(&b->done_cv, &b->mu);
+            if (!tk_done(b, ticket, &err) && !watch_own_launch(b, ticket))
+                pthread_cond_wait(&b->done_cv, &b->mu);
         }
         b->waiters--;
         rc = err;
@@ -1390,7 +1446,8 @@ static int host_fixed(md5hip_batcher *b, int kind, uint32_t fastcrc, const void 
         int err = 0;
         b->waiters++;
         pthread_cond_broadcast(&b->work_cv);
-        while (!tk_done(b, t, &err)) pthread_cond_wait(&b->done_cv, &b->mu);
+        while (!tk_done(b, t, &err))
+            if (!watch_own_launch(b, t)) pthread_cond_wait(&b->done_cv, &b->mu);
         b->waiters--;
         if (!rc) rc = err;
     }

@@ -127,7 +127,8 @@ def digest_fixed(data, n: int = None, length: int = None, stride: int = None, ou
     return out
 
 
-DESC_VARIANTS = {"auto": 0, "lane": 1, "hybrid": 3, "xdma": 4, "balanced": 5}   # enum md5hip_desc_variant
+DESC_VARIANTS = {"auto": 0, "lane": 1, "hybrid": 3, "xdma": 4, "balanced": 5,
+                 "fed": 6}   # enum md5hip_desc_variant
 
 
 def digest_desc(base, offsets, lens, order=None, out=None, stream=None, variant=0):

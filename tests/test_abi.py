@@ -163,8 +163,10 @@ def test_plan_order_longest_first():
 
 
 def test_plan_desc_picks_hybrid_only_for_standout_long_chunks():
-    """md5hip_plan_desc: the same order as md5hip_plan_order; LANE for small
-    batches (<= 2 groups per CU -- 256 CUs when no device is visible); HYBRID
+    """md5hip_plan_desc: the same order as md5hip_plan_order; FED for small
+    batches of <= 1 group per CU with a chunk of >= 2 whole blocks, LANE for
+    other small batches (<= 2 groups per CU -- 256 CUs when no device is
+    visible); HYBRID
     only when the longest chunks (>= 256 KiB) stand out (the chunk two waves
     per CU deep is <= 1/4 as long)."""
     rng = np.random.default_rng(5)
@@ -181,12 +183,18 @@ def test_plan_desc_picks_hybrid_only_for_standout_long_chunks():
     few[5000:] = 4096
     assert m.plan_desc(few)[1] == "hybrid"                 # long chunks stand out
     assert m.plan_desc(np.full(50000, 65536, np.uint32))[1] == "xdma"             # < 256 KiB
-    # small batches (<= 2 groups per CU, 256 CUs without a device): LANE
-    for n in (1, 64, 1000, 32768):
+    # small batches (256 CUs without a device): FED up to one group per CU,
+    # LANE up to two, and LANE when no chunk has two whole blocks
+    for n in (1, 64, 1000, 16384):
+        assert m.plan_desc(np.full(n, 16384, np.uint32))[1] == "fed", n
+    for n in (16385, 32768):
         assert m.plan_desc(np.full(n, 16384, np.uint32))[1] == "lane", n
+    for L in (0, 1, 64, 127):
+        assert m.plan_desc(np.full(1000, L, np.uint32))[1] == "lane", L
+    assert m.plan_desc(np.full(1000, 128, np.uint32))[1] == "fed"
     small_mixed = np.full(1000, 1 << 20, np.uint32)
     small_mixed[-1] = 100
-    assert m.plan_desc(small_mixed)[1] == "lane"
+    assert m.plan_desc(small_mixed)[1] == "fed"
     assert m.plan_desc(np.full(32769, 16384, np.uint32))[1] == "xdma"
     assert m.plan_desc(np.array([], np.uint32))[0].size == 0
 

@@ -71,7 +71,7 @@ def test_c3_full_batch_hybrid_vs_oracle(cuda):
     idx = np.unique(np.concatenate([long_idx, sample]))
     assert _oracle_chunks(data, offs, lens, idx, got) == 0
     # the other descriptor kernels produce the identical digest array
-    for v in ("xdma", "lane", "balanced"):
+    for v in ("xdma", "lane", "balanced", "fed"):
         assert np.array_equal(m.digest_desc(data, torch.from_numpy(offs).to(cuda),
                                             torch.from_numpy(lens.astype(np.int32)).to(cuda),
                                             torch.from_numpy(order.astype(np.int32)).to(cuda),

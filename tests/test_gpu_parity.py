@@ -188,6 +188,50 @@ def test_hybrid_long_group_edges(cuda):
     assert np.array_equal(got, want)
 
 
+def test_fed_group_edges(cuda):
+    """FED (chain wave + feeder wave per group, md5_desc_fed): groups whose
+    lanes end at every residue mod 64 around the longest chunk (lanes past
+    their own last block discard the feeder's clamped addends), lanes with no
+    whole block, exactly two blocks (the smallest fed group), a ragged last
+    group, a group of chunks under 128 B (LANE fallback), one unaligned start
+    (LANE fallback for its group only), ordered and unordered, and the
+    planner's own choice for a netcache vector."""
+    rng = np.random.default_rng(606)
+    cases = {
+        "residues": [16384 + r for r in (0, 1, 55, 56, 63, 64, 65, 127, 128, 129)] +
+                    [int(x) for x in rng.integers(1, 40000, 50)] + [0, 1, 63, 64, 100, 128],
+        "two_blocks": [128] * 10 + [127, 64, 0, 5],
+        "ragged": [int(x) for x in rng.integers(0, 70000, 64 * 5 + 7)],
+        "short_group": [int(x) for x in rng.integers(0, 128, 64)] + [4096] * 64,
+        "long": [(1 << 20) + 13] * 3 + [int(x) for x in rng.integers(0, 1 << 18, 100)],
+    }
+    for name, lens in cases.items():
+        offs, total = gen.pack_offsets(lens, align=16)
+        buf = gen.xorshift_array(total + 64, seed=len(lens) + 7)
+        want = gen.oracle_digests(buf, offs, lens)
+        for order in (m.plan_order(lens).astype(np.int32), None):
+            got = m.digest_desc(_dev(buf, cuda), torch.tensor(offs, dtype=torch.int64, device=cuda),
+                                torch.tensor(lens, dtype=torch.int32, device=cuda),
+                                None if order is None else _dev(order, cuda), variant="fed").cpu().numpy()
+            assert np.array_equal(got, want), (name, order is None)
+    # one start off 16 B: its group goes LANE, the other groups stay fed
+    lens = [16384] * 200
+    offs = list(gen.pack_offsets(lens, align=16)[0])
+    offs[70] += 4
+    buf = gen.xorshift_array(offs[-1] + 16384 + 64, seed=70)
+    want = gen.oracle_digests(buf, offs, lens)
+    got = m.digest_desc(_dev(buf, cuda), torch.tensor(offs, dtype=torch.int64, device=cuda),
+                        torch.tensor(lens, dtype=torch.int32, device=cuda), variant="fed").cpu().numpy()
+    assert np.array_equal(got, want)
+    # the planner's choice for a netcache vector is FED, through the default entry
+    order, v = m.plan_desc(np.asarray(lens, np.uint32))
+    assert v == "fed"
+    got = m.digest_desc(_dev(buf, cuda), torch.tensor(offs, dtype=torch.int64, device=cuda),
+                        torch.tensor(lens, dtype=torch.int32, device=cuda),
+                        _dev(order.astype(np.int32), cuda), variant=v).cpu().numpy()
+    assert np.array_equal(got, want)
+
+
 @pytest.mark.parametrize("dv", DESC)
 def test_desc_offsets_beyond_4gib(cuda, dv):
     """Descriptor offsets past 2^32 (64-bit row pointers): chunks scattered

@@ -226,7 +226,7 @@ def test_balanced_on_coalesced_mixed_batches(cuda):
             torch.from_numpy(order.astype(np.int32)).to(cuda))
     a = m.digest_desc(*args, variant="balanced")
     b = m.digest_desc(*args, variant="balanced")
-    for v in ("xdma", "hybrid", "lane"):
+    for v in ("xdma", "hybrid", "lane", "fed"):
         assert torch.equal(m.digest_desc(*args, variant=v), a), v
     assert torch.equal(a, b)
     idx = np.unique(np.concatenate([order[:300], order[-300:],
