@@ -139,7 +139,11 @@ enum crc32hip_variant {
     CRC32HIP_AUTO = 0,      /* the default: XDMA16 */
     CRC32HIP_XDMA16 = 6,    /* slicing-by-4 over 16 v_perm-addressed LDS table copies, 8 KiB
                                images filled by LDS-DMA, 12 waves/CU */
-    CRC32HIP_NUM_VARIANTS = 7
+    CRC32HIP_SPLIT = 7,     /* one wave per chunk: 256-B segments per lane, registers combined
+                               with crc32_combine's zero-byte operators (CRC-32 is linear);
+                               AUTO's choice for full-CRC batches of at most 4 chunks per CU
+                               (small vectors: latency).  Windows (fastcrc) never split */
+    CRC32HIP_NUM_VARIANTS = 8
 };
 int crc32hip_fixed_variant(const void *d_base, uint64_t n, uint32_t len, uint64_t stride,
                            uint32_t fastcrc, uint32_t *d_crcs, void *stream, int variant);
@@ -148,6 +152,10 @@ int crc32hip_resolve_variant(int variant);
 int crc32hip_desc(const void *d_base, const uint64_t *d_offsets, const uint32_t *d_lens,
                   const uint32_t *d_order, uint64_t n, uint32_t fastcrc, uint32_t *d_crcs,
                   void *stream);
+/* The same with the kernel named (CRC32HIP_AUTO = crc32hip_desc's choice). */
+int crc32hip_desc_variant(const void *d_base, const uint64_t *d_offsets, const uint32_t *d_lens,
+                          const uint32_t *d_order, uint64_t n, uint32_t fastcrc, uint32_t *d_crcs,
+                          void *stream, int variant);
 
 /*
  * Host helper: order[] = indices of lens[] sorted by MD5 block count,

@@ -6,9 +6,10 @@ chunks (contiguous, 16-B aligned, identity order) the four descriptor kernels
 (XDMA, LANE, HYBRID, BALANCED) are launched back to back, each timed per
 launch with HIP events (after 20 untimed launches of its own), in interleaved
 rounds; digests must equal XDMA's.  Prints one JSON object.
-With --crc: the product's CRC-32 launches on the same batches instead
-(crc32hip_desc through the descriptors, crc32hip_fixed on the contiguous
-layout), digests checked equal to each other.
+With --crc: the product's CRC-32 kernels on the same batches instead
+(crc32hip_desc_variant through the descriptors, crc32hip_fixed_variant on the
+contiguous layout; XDMA16 streaming against SPLIT, one wave per chunk),
+CRCs checked equal to each other.
 With --fed: also the diagnostic library's fed pairs for every group
 (md5diag_variant_desc 9: a feeder wave forms M + K for the chain wave, 4 VALU
 per step on the chain instead of 5), and the same with each pair
@@ -55,7 +56,8 @@ def main():
     for n in (int(x) for x in a.sizes.split(",")):
         offs = torch.arange(n, dtype=torch.int64, device="cuda") * a.len
         lens = torch.full((n,), a.len, dtype=torch.int32, device="cuda")
-        variants = {"crc_desc": 0, "crc_fixed": 1} if a.crc else dict(VARIANTS)
+        variants = ({"crc_desc_xdma16": 6, "crc_desc_split": 7, "crc_fixed_xdma16": 106,
+                     "crc_fixed_split": 107} if a.crc else dict(VARIANTS))
         if D is not None and not a.crc:
             variants["fed_diag"] = -9
             variants["fed_excl"] = -1002
@@ -67,10 +69,10 @@ def main():
                 def launch():
                     d, o, ln = (ctypes.c_void_p(t.data_ptr()) for t in (data, offs, lens))
                     out_p = ctypes.c_void_p(dig[v].data_ptr())
-                    if a.crc and code == 0:
-                        return L.crc32hip_desc(d, o, ln, None, n, 0, out_p, sp)
+                    if a.crc and code < 100:
+                        return L.crc32hip_desc_variant(d, o, ln, None, n, 0, out_p, sp, code)
                     if a.crc:
-                        return L.crc32hip_fixed(d, n, a.len, a.len, 0, out_p, sp)
+                        return L.crc32hip_fixed_variant(d, n, a.len, a.len, 0, out_p, sp, code - 100)
                     if code <= -1000:
                         return D.md5diag_fed_split_excl(-code - 1000, 0, d, o, ln, None, n, out_p, sp)
                     if code < 0:
@@ -86,7 +88,7 @@ def main():
                         ev[2 * k + 1].record(stream)
                 stream.synchronize()
                 res[v] += [ev[2 * k].elapsed_time(ev[2 * k + 1]) * 1e3 for k in range(a.iters)]
-        ref = dig["crc_desc" if a.crc else "xdma"].cpu()
+        ref = dig["crc_desc_xdma16" if a.crc else "xdma"].cpu()
         row = {}
         for v in variants:
             t = sorted(res[v])

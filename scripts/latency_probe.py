@@ -5,7 +5,9 @@ netcache-vector-sized submissions, against the kernel time of the same batch
 (md5hip_digest_desc through the planner, hipEvent).  Each library given
 (name=path; default: the product library) gets its own queue; calls are
 interleaved.  Prints one JSON object: median / p90 microseconds per call.
-usage: latency_probe.py [--iters N] [--lib name=path ...]"""
+With --crc the queues hash CRC-32 (md5hip_batcher_set_digest: the netcache
+blk_make_crc checksum) and the kernel alone is crc32hip_desc.
+usage: latency_probe.py [--iters N] [--crc] [--lib name=path ...]"""
 import argparse
 import ctypes
 import json
@@ -28,6 +30,7 @@ def load(path):
     L.md5hip_queue_create.argtypes = [ci, u64, u32, ctypes.POINTER(vp)]
     L.md5_batch_submit_device.argtypes = [vp, vp, vp, u64, vp, ci]
     L.md5hip_batcher_destroy.argtypes = [vp]
+    L.md5hip_batcher_set_digest.argtypes = [vp, ci, u32]
     return L
 
 
@@ -35,13 +38,17 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=200)
     ap.add_argument("--lib", nargs="*", default=["product=sproxy_amd/lib/libmd5hip.so"])
+    ap.add_argument("--crc", action="store_true")
     a = ap.parse_args()
+    dsz = 4 if a.crc else 16
     libs = {}
     for spec in a.lib:
         k, p = spec.split("=", 1)
         L = load(os.path.join(REPO, p))
         h = vp()
         assert L.md5hip_queue_create(0, 0, 0, ctypes.byref(h)) == 0
+        if a.crc:
+            assert L.md5hip_batcher_set_digest(h, 1, 0) == 0      # MD5HIP_DIGEST_CRC32
         libs[k] = (L, h)
     data = torch.empty(64 << 20, dtype=torch.uint8, device="cuda")
     m.fill_synthetic(data, seed=0x1A7)
@@ -49,7 +56,7 @@ def main():
     for n, L_ in ((16, 65536), (64, 16384), (256, 16384), (1024, 16384)):
         P = (data.data_ptr() + np.arange(n, dtype=np.uint64) * np.uint64(L_)).astype(np.uint64)
         lens = np.full(n, L_, dtype=np.uint32)
-        dig = torch.empty((n, 16), dtype=torch.uint8, device="cuda")
+        dig = torch.empty((n, dsz), dtype=torch.uint8, device="cuda")
         ref = None
         for k, (L, h) in libs.items():
             assert L.md5_batch_submit_device(h, P.ctypes.data, lens.ctypes.data, n, dig.data_ptr(), 1) == 0
@@ -61,11 +68,16 @@ def main():
         dL = torch.from_numpy(lens.astype(np.int32)).cuda()
         order, var = m.plan_desc(lens)
         dR = torch.from_numpy(order.astype(np.int32)).cuda()
+        if a.crc:
+            var = "crc32hip_desc"
         ks = []
         for _ in range(20):
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
-            m.digest_desc(data, dO, dL, dR, out=dig, variant=var)
+            if a.crc:
+                m.crc32_desc(data, dO, dL, dR, out=dig.view(torch.int32).view(-1))
+            else:
+                m.digest_desc(data, dO, dL, dR, out=dig, variant=var)
             e1.record()
             torch.cuda.synchronize()
             ks.append(e0.elapsed_time(e1) * 1e3)

@@ -127,6 +127,50 @@ struct CrcTables {
 };
 __constant__ const CrcTables kCrcTables{};
 
+// Zero-byte operators of the CRC-32 register, as zlib's crc32_combine builds
+// them: m[l][i] = the register after 256 * 2^l zero bytes (l = 0..6: 256 B
+// .. 16 KiB), started from the register 1 << i.  One zero byte is eight
+// single-bit steps of the reflected polynomial (crc32.c:22); the larger
+// operators are its repeated squares.  The register is linear in its start
+// value and in the data, so the CRC of a message cut into segments is the
+// XOR of each segment's register (the first started at ~0, the others at 0)
+// advanced through the bytes after that segment (crc32_split).
+struct CrcShift {
+  uint32_t m[7][32];
+  static constexpr uint32_t apply(const uint32_t (&op)[32], uint32_t v) {
+    uint32_t r = 0;
+    for (int i = 0; i < 32; ++i)
+      if ((v >> i) & 1u) r ^= op[i];
+    return r;
+  }
+  constexpr CrcShift() : m() {
+    uint32_t cur[32] = {};
+    for (int i = 0; i < 32; ++i) {
+      uint32_t c = 1u << i;
+      for (int k = 0; k < 8; ++k) c = (c & 1u) ? (c >> 1) ^ 0xEDB88320u : (c >> 1);
+      cur[i] = c;
+    }
+    for (int sq = 0; sq < 14; ++sq) {          // 2^(sq+1) zero bytes after square sq
+      uint32_t nx[32] = {};
+      for (int i = 0; i < 32; ++i) nx[i] = apply(cur, cur[i]);
+      for (int i = 0; i < 32; ++i) cur[i] = nx[i];
+      if (sq >= 7)
+        for (int i = 0; i < 32; ++i) m[sq - 7][i] = cur[i];
+    }
+  }
+};
+__constant__ const CrcShift kCrcShift{};
+
+// The register v advanced through 256 * 2^L zero bytes (L compile-time: the
+// 32 columns fold into literals), 2 VALU per column.
+template <int L>
+__device__ __forceinline__ uint32_t crc_shift(uint32_t v) {
+  uint32_t r = 0;
+#pragma unroll
+  for (int i = 0; i < 32; ++i) r ^= ((v >> i) & 1u) ? kCrcShift.m[L][i] : 0u;
+  return r;
+}
+
 struct Crc32State {
   uint32_t c;
 };

@@ -1332,6 +1332,71 @@ crc32_fast_pipe(const uint8_t* __restrict__ base, const uint64_t* __restrict__ o
   fast_pipe_body<2>(base, offs, lens, n, stride, flen, F, out, lds);
 }
 
+// ---------------------------------------------------------------------------
+// CRC-32 of small batches, one wave per chunk ("split", round 3).  Unlike
+// MD5, CRC-32 is linear, so one chunk need not be one serial chain: the
+// chunk is cut into 256-B segments, segment s on lane (s mod 64) of pass
+// s / 64, each lane runs its own register over its segment (the first
+// segment from ~0, the others from 0), and the registers are combined with
+// crc32_combine's zero-byte operators (hashers.h CrcShift): a 6-level tree
+// over the wave's lanes, each level advancing the left half through the
+// right half's bytes (256 * 2^l), then pass after pass through 16 KiB.  The
+// segments are counted from the END of the chunk, so every segment but the
+// first is exactly 256 B (the first holds the L mod 256 leftover bytes, or a
+// whole 256) and every shift is one of seven constants.  A lane's chain is 64
+// dependent table steps instead of the chunk's 4,096 -- the netcache call
+// site's vector of 16-1,024 blocks (blk_make_crc, blk_io.c:354-430) is a few
+// microseconds of work instead of one 16 KiB chain.  256-thread workgroups
+// (4 chunks) share one copy of the 64 KiB perm tables.
+// ---------------------------------------------------------------------------
+template <bool kImplicit>
+__global__ void __launch_bounds__(256)
+crc32_split(const uint8_t* __restrict__ base, const uint64_t* __restrict__ offs,
+            const uint32_t* __restrict__ lens, const uint32_t* __restrict__ order, uint64_t n,
+            uint64_t stride, uint32_t flen, uint32_t* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds[Crc32PermHasher::kLdsBytes];
+  Crc32PermHasher h;
+  h.setup(lds);                                  // all threads, before any exit
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t wpb = blockDim.x >> 6;
+  for (uint64_t q = (uint64_t)blockIdx.x * wpb + wave; q < n; q += (uint64_t)gridDim.x * wpb) {
+    const uint64_t c = (!kImplicit && order) ? (uint64_t)order[q] : q;
+    const uint8_t* m = base + (kImplicit ? c * stride : offs[c]);
+    const uint32_t L = kImplicit ? flen : lens[c];
+    const uint32_t nseg = (uint32_t)(((uint64_t)L + 255u) >> 8);
+    const uint32_t r0 = nseg ? L - ((nseg - 1u) << 8) : 0u;        // first segment: 1..256 B
+    const uint32_t npass = (nseg + 63u) >> 6;
+    uint32_t acc = 0;
+    for (uint32_t p = 0; p < npass; ++p) {
+      // passes right-aligned: the first pass's low lanes hold no segment
+      const int64_t s = (int64_t)nseg - 64 * (int64_t)(npass - p) + (int64_t)lane;
+      uint32_t reg = 0;
+      if (s >= 0) {
+        const uint64_t start = s == 0 ? 0u : (uint64_t)r0 + ((uint64_t)(s - 1) << 8);
+        typename Crc32PermHasher::State st{s == 0 ? 0xFFFFFFFFu : 0u};
+        lane_range<Crc32PermHasher, 2>(h, st, m + start, s == 0 ? r0 : 256u);
+        reg = ~st.c;                             // the raw register (finish complements)
+      }
+      // lane j ends holding segments [j - 2^(l+1) + 1, j] when j = 2^(l+1) - 1 mod 2^(l+1)
+      auto level = [&](auto lv) __attribute__((always_inline)) {
+        constexpr int l = decltype(lv)::value;
+        const uint32_t left = (uint32_t)__shfl_up((int)reg, 1u << l, 64);
+        const uint32_t sh = crc_shift<l>(left);
+        if ((lane & ((2u << l) - 1u)) == (2u << l) - 1u) reg ^= sh;
+      };
+      level(std::integral_constant<int, 0>{});
+      level(std::integral_constant<int, 1>{});
+      level(std::integral_constant<int, 2>{});
+      level(std::integral_constant<int, 3>{});
+      level(std::integral_constant<int, 4>{});
+      level(std::integral_constant<int, 5>{});
+      acc = crc_shift<6>(acc) ^ reg;             // lane 63: all passes so far
+    }
+    if (lane == 63u) out[c] = L ? ~acc : 0u;     // empty: crc32.c returns ~~0 = 0
+  }
+}
+
 template <bool kImplicit>
 __global__ void __launch_bounds__(256)
 crc32_desc(const uint8_t* __restrict__ base, const uint64_t* __restrict__ offs,

@@ -123,6 +123,21 @@ uint32_t per_cu_grid(uint64_t n) {
   return (uint32_t)(need < cap ? need : cap);
 }
 
+// CRC-32 of a small full-CRC batch: one wave per chunk, segments combined
+// (crc32_split).  AUTO takes it up to kCrcSplitPerCu chunks per CU, where the
+// streaming kernels' waves would each hold one long serial chain.
+constexpr uint64_t kCrcSplitPerCu = 16;
+bool crc_split_pick(uint64_t n, int variant) {
+  if (variant == CRC32HIP_SPLIT) return true;
+  return variant == CRC32HIP_AUTO && n <= kCrcSplitPerCu * (uint64_t)cu_count();
+}
+// 4 chunks (waves) per 256-thread workgroup; grid-stride past 8 per CU
+uint32_t crc_split_grid(uint64_t n) {
+  const uint64_t need = (n + 3) / 4;
+  const uint64_t cap = 2ull * (uint64_t)cu_count();
+  return (uint32_t)(need < cap ? need : cap);
+}
+
 }  // namespace
 
 extern "C" {
@@ -248,12 +263,19 @@ int crc32hip_fixed_variant(const void* d_base, uint64_t n, uint32_t len, uint64_
   if (n == 0) return 0;
   if (!d_base || !d_crcs || len > stride || (fastcrc & 3u)) return -EINVAL;
   if (((uintptr_t)d_crcs & 3u) != 0) return -EINVAL;
-  if (variant != CRC32HIP_AUTO && variant != CRC32HIP_XDMA16) return -EINVAL;
+  if (variant != CRC32HIP_AUTO && variant != CRC32HIP_XDMA16 && variant != CRC32HIP_SPLIT)
+    return -EINVAL;
   if (int e = device_ok()) return e;
   hipStream_t s = (hipStream_t)stream;
   const uint8_t* base = (const uint8_t*)d_base;
   const uint64_t g = (n + kDescBlock - 1) / kDescBlock;
   if (g > 0x7fffffffull) return -EINVAL;
+  if (!(fastcrc && len > fastcrc) && crc_split_pick(n, variant)) {
+    hipLaunchKernelGGL(crc32_split<true>, dim3(crc_split_grid(n)), dim3(256), 0, s, base,
+                       (const uint64_t*)nullptr, (const uint32_t*)nullptr,
+                       (const uint32_t*)nullptr, n, stride, len, d_crcs);
+    return launched();
+  }
   if (fastcrc && len > fastcrc) {
     if (fastcrc == 64 || fastcrc == 128) {
       // one- or two-block windows: lane loads, next group in flight
@@ -289,13 +311,28 @@ int crc32hip_fixed(const void* d_base, uint64_t n, uint32_t len, uint64_t stride
 int crc32hip_desc(const void* d_base, const uint64_t* d_offsets, const uint32_t* d_lens,
                   const uint32_t* d_order, uint64_t n, uint32_t fastcrc, uint32_t* d_crcs,
                   void* stream) {
+  return crc32hip_desc_variant(d_base, d_offsets, d_lens, d_order, n, fastcrc, d_crcs, stream,
+                               CRC32HIP_AUTO);
+}
+
+int crc32hip_desc_variant(const void* d_base, const uint64_t* d_offsets, const uint32_t* d_lens,
+                          const uint32_t* d_order, uint64_t n, uint32_t fastcrc, uint32_t* d_crcs,
+                          void* stream, int variant) {
   if (n == 0) return 0;
   if (!d_base || !d_offsets || !d_lens || !d_crcs || (fastcrc & 3u)) return -EINVAL;
   if (((uintptr_t)d_crcs & 3u) != 0) return -EINVAL;
+  if (variant != CRC32HIP_AUTO && variant != CRC32HIP_XDMA16 && variant != CRC32HIP_SPLIT)
+    return -EINVAL;
   if (int e = device_ok()) return e;
   hipStream_t s = (hipStream_t)stream;
   const uint64_t g = (n + kDescBlock - 1) / kDescBlock;
   if (g > 0x7fffffffull) return -EINVAL;
+  if (fastcrc == 0 && crc_split_pick(n, variant)) {
+    hipLaunchKernelGGL(crc32_split<false>, dim3(crc_split_grid(n)), dim3(256), 0, s,
+                       (const uint8_t*)d_base, d_offsets, d_lens, d_order, n, (uint64_t)0, 0u,
+                       d_crcs);
+    return launched();
+  }
   if (fastcrc == 64 || fastcrc == 128) {
     hipLaunchKernelGGL(crc32_fast_pipe, dim3(per_cu_grid(2 * n)), dim3(1024), 0, s,
                        (const uint8_t*)d_base, d_offsets, d_lens, n, (uint64_t)0, 0u, fastcrc,

@@ -196,7 +196,7 @@ def final_ctx(ctxs, out=None, stream=None):
     return out
 
 
-CRC_VARIANTS = {"auto": 0, "xdma16": 6}   # enum crc32hip_variant
+CRC_VARIANTS = {"auto": 0, "xdma16": 6, "split": 7}   # enum crc32hip_variant
 
 
 def crc32_fixed(data, n: int = None, length: int = None, stride: int = None, fastcrc: int = 0,
@@ -221,16 +221,19 @@ def crc32_fixed(data, n: int = None, length: int = None, stride: int = None, fas
     return out
 
 
-def crc32_desc(base, offsets, lens, order=None, fastcrc: int = 0, out=None, stream=None):
+def crc32_desc(base, offsets, lens, order=None, fastcrc: int = 0, out=None, stream=None, variant=0):
     _need_cuda(base, "base")
     _need_cuda(offsets, "offsets")
     _need_cuda(lens, "lens")
     n = offsets.numel()
     if out is None:
         out = torch.empty(n, dtype=torch.int32, device=base.device)
-    check("crc32hip_desc", lib().crc32hip_desc(base.data_ptr(), offsets.data_ptr(), lens.data_ptr(),
-                                               order.data_ptr() if order is not None else None, n,
-                                               fastcrc, out.data_ptr(), _stream(stream)))
+    if isinstance(variant, str):
+        variant = CRC_VARIANTS[variant]
+    check("crc32hip_desc_variant",
+          lib().crc32hip_desc_variant(base.data_ptr(), offsets.data_ptr(), lens.data_ptr(),
+                                      order.data_ptr() if order is not None else None, n,
+                                      fastcrc, out.data_ptr(), _stream(stream), variant))
     return out
 
 

@@ -204,3 +204,36 @@ def test_gpu_fastcrc_xdma_windows(cuda, fast):
                        torch.tensor(lens, dtype=torch.int32, device=cuda),
                        fastcrc=fast).cpu().numpy().view(np.uint32)
     assert np.array_equal(got, want)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("align", [16, 4, 1])
+def test_gpu_crc_split_desc(cuda, align):
+    """CRCSPLIT (crc32_split: one wave per chunk, 256-B segments combined with
+    crc32_combine's zero-byte operators) against crc32.c: every length around
+    the segment (256 B) and pass (16 KiB) boundaries, chunks of several passes
+    (up to 1 MiB + 13), empty and 1-3 byte chunks, starts at any alignment,
+    ordered and unordered; and AUTO's choice for a netcache-size vector."""
+    import torch
+    rng = np.random.default_rng(4000 + align)
+    edges = [0, 1, 2, 3, 4, 5, 63, 64, 65, 255, 256, 257, 511, 512, 513, 16383, 16384, 16385,
+             16384 + 256, 32767, 32768, 32769, 65536 + 100, (1 << 20) + 13]
+    lens = edges + [int(x) for x in rng.integers(0, 70000, 200)]
+    offs, total = gen.pack_offsets(lens, align=align)
+    buf = gen.xorshift_array(total + 64, seed=align)
+    want = gen.oracle_crc32_batch(buf, offs, lens)
+    d = _dev(buf, cuda)
+    t_off = torch.tensor(offs, dtype=torch.int64, device=cuda)
+    t_len = torch.tensor(lens, dtype=torch.int32, device=cuda)
+    for order in (m.plan_order(lens).astype(np.int32), None):
+        o = None if order is None else _dev(order, cuda)
+        for v in ("split", "auto", "xdma16"):
+            got = m.crc32_desc(d, t_off, t_len, o, variant=v).cpu().numpy().view(np.uint32)
+            assert np.array_equal(got, want), (v, order is None)
+    # a netcache vector: 64 x 16 KiB pages; AUTO splits it (<= 4 chunks per CU)
+    n, L = 64, 16384
+    host = gen.xorshift_array(n * L, seed=64)
+    want = gen.oracle_crc32_batch(host, np.arange(n, dtype=np.uint64) * L, [L] * n)
+    for v in ("auto", "split"):
+        got = m.crc32_fixed(_dev(host, cuda), n, L, variant=v).cpu().numpy().view(np.uint32)
+        assert np.array_equal(got, want), v
