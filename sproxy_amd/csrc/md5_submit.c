@@ -180,6 +180,9 @@ struct slot {
     unsigned char *h_data, *d_data;   /* staging, `cap` bytes */
     uint64_t *h_off, *d_off;          /* descriptors, `maxn` entries */
     uint32_t *h_len, *d_len;
+    const uint64_t *dh_off;           /* h_off / h_len as the device sees them (fine-grained) */
+    const uint32_t *dh_len;
+    int desc_direct;                  /* the planned launch reads dh_off / dh_len in place */
     uint32_t *h_ord, *d_ord;
     unsigned char *h_dig, *d_dig;     /* 16 * maxn */
     int direct;                       /* the kernel wrote the one device segment in place */
@@ -314,12 +317,18 @@ static int seg_has(const struct slot *sl, uint64_t t)
  * launch keeps the device busy, and the launch then only enqueues the kernel.
  * Chunks appended after it are copied and the slot re-planned at launch (an
  * order copy still in flight is overwritten by the later one, same stream). */
+/* Small slots (a netcache vector) skip the two descriptor copies: the kernel
+ * reads the fine-grained pinned arrays in place, one PCIe round trip per wave
+ * instead of two copy operations ahead of the launch on the slot's stream. */
+enum { DESC_DIRECT_MAX = 4096 };
+
 static int slot_prepare(md5hip_batcher *b, struct slot *sl)
 {
     (void)b;
     const uint64_t n = sl->n;
     if (sl->planned_n == n) return 0;
-    if (n > sl->copied_n) {
+    sl->desc_direct = n <= DESC_DIRECT_MAX;
+    if (!sl->desc_direct && n > sl->copied_n) {
         const uint64_t c0 = sl->copied_n;
         if (hipMemcpyAsync(sl->d_off + c0, sl->h_off + c0, 8 * (n - c0), hipMemcpyHostToDevice, sl->stream) ||
             hipMemcpyAsync(sl->d_len + c0, sl->h_len + c0, 4 * (n - c0), hipMemcpyHostToDevice, sl->stream))
@@ -339,7 +348,8 @@ static int slot_prepare(md5hip_batcher *b, struct slot *sl)
         if (hipMemcpyAsync(sl->d_bkt, sl->h_bkt, 4 * ((size_t)sl->hkmax + 1), hipMemcpyHostToDevice,
                            sl->stream))
             return -EIO;
-        const int e = md5hip_order_device(sl->d_len, n, sl->hkmax, sl->d_bkt, sl->d_ord, sl->stream);
+        const int e = md5hip_order_device(sl->desc_direct ? sl->dh_len : sl->d_len, n, sl->hkmax,
+                                          sl->d_bkt, sl->d_ord, sl->stream);
         if (e) return e;
     } else {
         dvar = md5hip_plan_desc(sl->h_len, n, sl->h_ord);
@@ -401,10 +411,12 @@ static int slot_enqueue(md5hip_batcher *b, struct slot *sl)
             sl->direct = 1;
         }
         const uint32_t *ord = sl->use_order ? sl->d_ord : NULL;
+        const uint64_t *doff = sl->desc_direct ? sl->dh_off : sl->d_off;
+        const uint32_t *dlen = sl->desc_direct ? sl->dh_len : sl->d_len;
         rc = sl->kind == MD5HIP_DIGEST_CRC32
-                 ? crc32hip_desc(sl->d_data, sl->d_off, sl->d_len, ord, n, sl->fastcrc,
+                 ? crc32hip_desc(sl->d_data, doff, dlen, ord, n, sl->fastcrc,
                                  (uint32_t *)dst, sl->stream)
-                 : md5hip_digest_desc_variant(sl->d_data, sl->d_off, sl->d_len, ord, n,
+                 : md5hip_digest_desc_variant(sl->d_data, doff, dlen, ord, n,
                                               dst, sl->stream, dvar);
         if (rc) return rc;
     }
@@ -757,8 +769,11 @@ static int batcher_new(int device, uint64_t slice_bytes, uint32_t nslots, uint64
         CK(hipStreamCreateWithFlags(&sl->stream, hipStreamNonBlocking));
         CK(hipEventCreateWithFlags(&sl->done, hipEventDisableTiming));
         CK(hipHostMalloc((void **)&sl->h_data, b->cap, hipHostMallocDefault));
-        CK(hipHostMalloc((void **)&sl->h_off, 8 * b->maxn, hipHostMallocDefault));
-        CK(hipHostMalloc((void **)&sl->h_len, 4 * b->maxn, hipHostMallocDefault));
+        /* fine-grained: a small slot's kernel reads them in place (slot_prepare) */
+        CK(hipHostMalloc((void **)&sl->h_off, 8 * b->maxn, hipHostMallocCoherent));
+        CK(hipHostMalloc((void **)&sl->h_len, 4 * b->maxn, hipHostMallocCoherent));
+        CK(hipHostGetDevicePointer((void **)&sl->dh_off, sl->h_off, 0));
+        CK(hipHostGetDevicePointer((void **)&sl->dh_len, sl->h_len, 0));
         CK(hipHostMalloc((void **)&sl->h_ord, 4 * b->maxn, hipHostMallocDefault));
         CK(hipHostMalloc((void **)&sl->h_dig, 16 * b->maxn, hipHostMallocDefault));
         CK(hipMalloc((void **)&sl->d_data, b->cap));
