@@ -1002,12 +1002,15 @@ __device__ __forceinline__ void fed_long_group(const uint8_t* __restrict__ base,
 // (profiles/r03q/small_fed_*.json).  A group holding a chunk start that is
 // not 16-B aligned, or no chunk of two whole blocks, runs LANE's lane-direct
 // body on wave 0 instead.
+// kImplicit: chunk i at base + i * stride, `flen` bytes (the fixed-length
+// API's small batches).
 constexpr uint32_t kFedMinBlocks = 2;
 
+template <bool kImplicit>
 __global__ void __launch_bounds__(128)
 md5_desc_fed(const uint8_t* __restrict__ base, const uint64_t* __restrict__ offs,
              const uint32_t* __restrict__ lens, const uint32_t* __restrict__ order, uint64_t n,
-             uint4* __restrict__ out) {
+             uint64_t stride, uint32_t flen, uint4* __restrict__ out) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[2 * kFedTable];
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const DescArrays src{offs, lens, order};
@@ -1015,9 +1018,9 @@ md5_desc_fed(const uint8_t* __restrict__ base, const uint64_t* __restrict__ offs
   const uint32_t lane = threadIdx.x & 63u;
   const uint64_t i = first + lane;
   const bool live = i < n;
-  const uint64_t c = src.index(live ? i : first);
-  const uint64_t off = src.off(c);
-  const uint32_t len = live ? src.len(c) : 0u;
+  const uint64_t c = kImplicit ? (live ? i : first) : src.index(live ? i : first);
+  const uint64_t off = kImplicit ? c * stride : src.off(c);
+  const uint32_t len = live ? (kImplicit ? flen : src.len(c)) : 0u;
   const uint32_t nfull = len >> 6;
   const uint32_t bmax = wave_max(nfull);
   const bool unaligned = __ballot(live && ((((uintptr_t)base + off) & 15u) != 0)) != 0;

@@ -123,6 +123,10 @@ uint32_t per_cu_grid(uint64_t n) {
   return (uint32_t)(need < cap ? need : cap);
 }
 
+// MD5 batches of at most this many 64-chunk groups per CU run as fed pairs
+// (md5_desc_fed; planners below, and the fixed-length AUTO launch).
+constexpr uint64_t kFedGroupsPerCu = 1;
+
 // CRC-32 of a small full-CRC batch: one wave per chunk, segments combined
 // (crc32_split).  AUTO takes it up to kCrcSplitPerCu chunks per CU, where the
 // streaming kernels' waves would each hold one long serial chain.
@@ -203,8 +207,8 @@ int md5hip_digest_desc_variant(const void* d_base, const uint64_t* d_offsets,
   }
   if (variant == MD5HIP_DESC_FED) {
     // chain + feeder wave per 64-chunk group (md5_kernels.h md5_desc_fed)
-    hipLaunchKernelGGL(md5_desc_fed, dim3((uint32_t)g), dim3(128), 0, s, base, d_offsets, d_lens,
-                       d_order, n, (uint4*)d_digests);
+    hipLaunchKernelGGL(md5_desc_fed<false>, dim3((uint32_t)g), dim3(128), 0, s, base, d_offsets,
+                       d_lens, d_order, n, (uint64_t)0, 0u, (uint4*)d_digests);
     return launched();
   }
   if (variant == MD5HIP_DESC_AUTO || variant == MD5HIP_DESC_XDMA) {
@@ -246,6 +250,14 @@ int md5hip_digest_fixed_variant(const void* d_base, uint64_t n, uint32_t len, ui
   if (variant == MD5HIP_DIRECT2 || stride >= (1ull << 31) / 64) {
     hipLaunchKernelGGL((md5_fixed_direct<2, Md5Hasher<false>>), dim3((uint32_t)grid), dim3(kBlock),
                        0, s, base, n, len, stride, out);
+    return launched();
+  }
+  if (variant == MD5HIP_AUTO && (n + 63) / 64 <= kFedGroupsPerCu * (uint64_t)cu_count() &&
+      (len >> 6) >= kFedMinBlocks) {
+    // a small batch: its launch is one chunk's chain, which fed pairs shorten
+    hipLaunchKernelGGL(md5_desc_fed<true>, dim3((uint32_t)((n + 63) / 64)), dim3(128), 0, s, base,
+                       (const uint64_t*)nullptr, (const uint32_t*)nullptr,
+                       (const uint32_t*)nullptr, n, stride, len, out);
     return launched();
   }
   hipLaunchKernelGGL(md5_fixed_xdma1nt, dim3((uint32_t)grid), dim3(kBlock), 0, s, base, n, len,
@@ -588,11 +600,10 @@ int md5hip_arena_free(void* ptr) {
 // 206 us; profiles/r03/small_batch_kernels_*.json).
 constexpr uint64_t kLaneGroupsPerCu = 2;
 
-// Of those, batches of at most one group per CU run as fed pairs (FED: the
-// chain wave's 5th VALU per step moves to a feeder wave on another SIMD; 147
-// -> 138 us at 64-4,096 x 16 KiB, 150.6 -> 141 at 16,384;
+// Of those, batches of at most one group per CU (kFedGroupsPerCu) run as fed
+// pairs (FED: the chain wave's 5th VALU per step moves to a feeder wave on
+// another SIMD; 147 -> 138 us at 64-4,096 x 16 KiB, 150.6 -> 141 at 16,384;
 // profiles/r03q/small_fed_16k.json) when some chunk has two whole blocks.
-constexpr uint64_t kFedGroupsPerCu = 1;
 static int small_choice(uint64_t ngroups, uint32_t bmax) {
   if (ngroups <= kFedGroupsPerCu * (uint64_t)cu_count() && bmax >= kFedMinBlocks)
     return MD5HIP_DESC_FED;

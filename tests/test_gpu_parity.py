@@ -745,3 +745,26 @@ def test_order_device_is_a_longest_first_permutation(cuda):
             got = m.digest_desc(dev, torch.tensor(offs, dtype=torch.int64, device=cuda), d_len, d_ord,
                                 variant=v)
             assert np.array_equal(got.cpu().numpy(), gen.oracle_digests(host, offs, [int(x) for x in lens]))
+
+
+def test_fixed_auto_small_batches_run_fed(golden, cuda):
+    """md5hip_digest_fixed's AUTO launch sends a batch of at most one 64-chunk
+    group per CU to fed pairs (md5_desc_fed, implicit layout) when its chunks
+    have two whole blocks: every golden edge length, a ragged last group,
+    unaligned strides (the lane-direct kernel), against md5.c's digests."""
+    e = golden["edge"]
+    big = np.frombuffer(gen.mul_pattern(max(e["lengths"])), dtype=np.uint8)
+    for L, want in zip(e["lengths"], e["md5"]):
+        if L > (1 << 17):
+            continue
+        for stride in (max(16, (L + 15) // 16 * 16), L + 4):
+            n = 130
+            host = np.zeros(n * stride + 16, dtype=np.uint8)
+            for i in range(n):
+                host[i * stride:i * stride + L] = big[:L]
+            got = m.digest_fixed(_dev(host, cuda), n, L, stride).cpu().numpy()
+            assert all(bytes(x).hex() == want for x in got), (L, stride)
+    n, L = 4000, 16384                                   # 63 groups: FED
+    host = gen.xorshift_array(n * L, seed=4000)
+    got = m.digest_fixed(_dev(host, cuda), n, L).cpu().numpy()
+    assert np.array_equal(got, gen.oracle_digests_fixed(host, n, L))
