@@ -141,8 +141,9 @@ enum crc32hip_variant {
                                images filled by LDS-DMA, 12 waves/CU */
     CRC32HIP_SPLIT = 7,     /* one wave per chunk: 256-B segments per lane, registers combined
                                with crc32_combine's zero-byte operators (CRC-32 is linear);
-                               AUTO's choice for full-CRC batches of at most 4 chunks per CU
-                               (small vectors: latency).  Windows (fastcrc) never split */
+                               AUTO's choice for full-CRC batches of up to 128 chunks per CU
+                               of >= 2 KiB (12 per CU shorter; 16 per CU when the lengths
+                               are device-side only).  Windows (fastcrc) never split */
     CRC32HIP_NUM_VARIANTS = 8
 };
 int crc32hip_fixed_variant(const void *d_base, uint64_t n, uint32_t len, uint64_t stride,

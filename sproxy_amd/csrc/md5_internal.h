@@ -23,6 +23,11 @@ __attribute__((visibility("hidden")))
 int md5hip_gather_launch(const struct md5hip_seg *d_segs, uint64_t nseg, unsigned char *d_dst,
                          void *stream);
 
+/* CRC kernel variant (enum crc32hip_variant) for a full-CRC descriptor batch
+ * of n chunks whose mean length is known (md5_kernels.hip). */
+__attribute__((visibility("hidden")))
+int md5hip_crc_desc_choice(uint64_t n, uint64_t mean_len);
+
 /* Batched verify with a digest kind of its own (md5_submit.c): the
  * batcher's setting is not touched, so concurrent submitters keep theirs. */
 struct md5hip_batcher;

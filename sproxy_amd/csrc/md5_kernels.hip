@@ -127,13 +127,24 @@ uint32_t per_cu_grid(uint64_t n) {
 // (md5_desc_fed; planners below, and the fixed-length AUTO launch).
 constexpr uint64_t kFedGroupsPerCu = 1;
 
-// CRC-32 of a small full-CRC batch: one wave per chunk, segments combined
-// (crc32_split).  AUTO takes it up to kCrcSplitPerCu chunks per CU, where the
-// streaming kernels' waves would each hold one long serial chain.
+// CRC-32 of a full-CRC batch, split across a wave per chunk (crc32_split)
+// or streamed one lane per chunk.  The streaming launch lasts one chunk's
+// serial chain, ~13 ns per byte (220 us at 16 KiB, 12.9 ms at 1 MiB) with an
+// ~18 us floor; the split one moves ~2.8 TB/s with ~3 ns per chunk of fixed
+// work.  Measured crossovers (profiles/r03aa/, profiles/r03u/): ~36 K chunks
+// at 16 KiB, ~38 K at 64 KiB, none up to 4 K at 1 MiB, ~3.5 K at 1 KiB.  So
+// with the chunk length known, split up to 128 chunks per CU when chunks are
+// >= 2 KiB and up to 12 per CU below; with it unknown (device-side lengths),
+// up to kCrcSplitPerCu.
 constexpr uint64_t kCrcSplitPerCu = 16;
-bool crc_split_pick(uint64_t n, int variant) {
+bool crc_split_fits(uint64_t n, uint64_t len) {
+  const uint64_t cus = (uint64_t)cu_count();
+  if (len == 0) return n <= kCrcSplitPerCu * cus;
+  return len >= 2048 ? n <= 128 * cus : n <= 12 * cus;
+}
+bool crc_split_pick(uint64_t n, int variant, uint64_t len = 0) {
   if (variant == CRC32HIP_SPLIT) return true;
-  return variant == CRC32HIP_AUTO && n <= kCrcSplitPerCu * (uint64_t)cu_count();
+  return variant == CRC32HIP_AUTO && crc_split_fits(n, len);
 }
 // 4 chunks (waves) per 256-thread workgroup; grid-stride past 8 per CU
 uint32_t crc_split_grid(uint64_t n) {
@@ -147,6 +158,12 @@ uint32_t crc_split_grid(uint64_t n) {
 extern "C" {
 
 int md5hip_abi_version(void) { return MD5HIP_ABI_VERSION; }
+
+// md5_internal.h: the CRC variant for a descriptor batch whose mean chunk
+// length the caller knows (the batcher does).
+__attribute__((visibility("hidden"))) int md5hip_crc_desc_choice(uint64_t n, uint64_t mean_len) {
+  return crc_split_fits(n, mean_len ? mean_len : 1) ? CRC32HIP_SPLIT : CRC32HIP_AUTO;
+}
 
 // The shipped kernels are fixed: the round-1 A/B variants live in the
 // diagnostic library (md5_diag.hip, md5_kernels_ab.h), and no environment
@@ -282,7 +299,7 @@ int crc32hip_fixed_variant(const void* d_base, uint64_t n, uint32_t len, uint64_
   const uint8_t* base = (const uint8_t*)d_base;
   const uint64_t g = (n + kDescBlock - 1) / kDescBlock;
   if (g > 0x7fffffffull) return -EINVAL;
-  if (!(fastcrc && len > fastcrc) && crc_split_pick(n, variant)) {
+  if (!(fastcrc && len > fastcrc) && crc_split_pick(n, variant, len ? len : 1)) {
     hipLaunchKernelGGL(crc32_split<true>, dim3(crc_split_grid(n)), dim3(256), 0, s, base,
                        (const uint64_t*)nullptr, (const uint32_t*)nullptr,
                        (const uint32_t*)nullptr, n, stride, len, d_crcs);

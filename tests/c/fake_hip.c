@@ -164,6 +164,19 @@ int crc32hip_desc(const void *d_base, const uint64_t *d_offsets, const uint32_t 
     return 0;
 }
 
+int crc32hip_desc_variant(const void *d_base, const uint64_t *d_offsets, const uint32_t *d_lens,
+                          const uint32_t *d_order, uint64_t n, uint32_t fastcrc, uint32_t *d_crcs,
+                          void *stream, int variant)
+{
+    if (variant != 0 && variant != 6 && variant != 7) return -EINVAL;
+    return crc32hip_desc(d_base, d_offsets, d_lens, d_order, n, fastcrc, d_crcs, stream);
+}
+
+int md5hip_crc_desc_choice(uint64_t n, uint64_t mean_len)
+{
+    return (mean_len >= 2048 ? n <= 128 * 256 : n <= 12 * 256) ? 7 : 0;
+}
+
 int md5hip_gather_launch(const struct md5hip_seg *d_segs, uint64_t nseg, unsigned char *d_dst, void *stream)
 {
     (void)stream;

@@ -237,3 +237,27 @@ def test_gpu_crc_split_desc(cuda, align):
     for v in ("auto", "split"):
         got = m.crc32_fixed(_dev(host, cuda), n, L, variant=v).cpu().numpy().view(np.uint32)
         assert np.array_equal(got, want), v
+
+
+@pytest.mark.gpu
+def test_gpu_crc_queue_long_blocks_split(cuda):
+    """The queue's CRC-32 launch picks the split kernel from the slot's mean
+    chunk length (md5hip_crc_desc_choice): long blocks (netcache chunk_size
+    up to MiBs: 1 MiB + ragged, 256 KiB) split at any count it allows, short
+    ones (< 2 KiB) only in small batches, and every CRC equals crc32.c's."""
+    import torch
+    q = m.Queue(device=torch.cuda.current_device())
+    q.set_digest(m.Batcher.CRC32)
+    rng = np.random.default_rng(2024)
+    for lens in ([(1 << 20) + 13] * 5 + [1 << 20] * 40 + [5, 0],
+                 [256 << 10] * 300 + [int(x) for x in rng.integers(0, 256 << 10, 50)],
+                 [int(x) for x in rng.integers(0, 2048, 5000)]):
+        offs, total = gen.pack_offsets(lens, align=16)
+        buf = gen.xorshift_array(total + 64, seed=len(lens))
+        want = gen.oracle_crc32_batch(buf, offs, lens)
+        d = _dev(buf, cuda)
+        ptrs = np.asarray(offs, dtype=np.uint64) + np.uint64(d.data_ptr())
+        got = q.submit_device(ptrs, np.asarray(lens, dtype=np.uint32))
+        got = np.asarray(got).view(np.uint32).reshape(-1)
+        assert np.array_equal(got, want), len(lens)
+    q.close()
