@@ -6,7 +6,7 @@ Run it under `rocprofv3 --kernel-trace --memory-copy-trace` and join the
 traces with --join DIR afterwards: per call, the host call window against the
 device's copies and kernels inside it (first op start - call start, op
 durations, gaps, last op end - call end).
-usage: call_breakdown.py [--mode host|device] [--nb 64] [--calls 200] [--out stamps.json]
+usage: call_breakdown.py [--mode host|device] [--nb 64] [--calls 200] [--crc] [--out stamps.json]
        call_breakdown.py --join TRACE_DIR --stamps stamps.json"""
 import argparse
 import csv
@@ -42,6 +42,8 @@ def run(a):
         m.fill_synthetic(data, seed=3)
         torch.cuda.synchronize()
         b = m.Queue(device=0)
+        if a.crc:
+            b.set_digest(m.Batcher.CRC32)
         ptrs = (np.uint64(data.data_ptr()) + np.arange(nb, dtype=np.uint64) * np.uint64(Lc))
         lens = np.full(nb, Lc, np.uint32)
         dig = torch.empty((nb, 16), dtype=torch.uint8, device="cuda")
@@ -107,6 +109,7 @@ def main():
     ap.add_argument("--out", default="stamps.json")
     ap.add_argument("--join", default=None)
     ap.add_argument("--stamps", default=None)
+    ap.add_argument("--crc", action="store_true", help="device mode: CRC-32 digests")
     a = ap.parse_args()
     if a.join:
         join(a)

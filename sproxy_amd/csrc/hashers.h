@@ -338,9 +338,16 @@ struct Crc32PermHasher {
   uint32_t lane4;                      // (lane % 16) * 4: table 0, for the byte-wise tail
   uint32_t lb[4], sel[4];              // slot k: (t << 6) | (c << 2), and the v_perm selector
   __device__ __forceinline__ void setup(uint8_t* l) {
-    uint32_t* t = reinterpret_cast<uint32_t*>(l);
-    for (uint32_t k = threadIdx.x; k < 256u * 64u; k += blockDim.x)
-      t[k] = kCrcTables.t[(k >> 4) & 3u][k >> 6];
+    // the 16 copies of one (table, entry) value are 64 contiguous bytes: one
+    // load and four 16-B LDS writes per value, 1,024 values per workgroup
+    // (a load per dword cost a small launch ~2 us of L2 round trips)
+    uint4* t = reinterpret_cast<uint4*>(l);
+    for (uint32_t j = threadIdx.x; j < 1024u; j += blockDim.x) {
+      const uint32_t v = kCrcTables.t[j & 3u][j >> 2];
+      const uint4 q = make_uint4(v, v, v, v);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) t[4u * j + c] = q;
+    }
     __syncthreads();
     lds = l;
     lane4 = (threadIdx.x & 15u) * 4u;
