@@ -143,7 +143,8 @@ enum crc32hip_variant {
                                with crc32_combine's zero-byte operators (CRC-32 is linear);
                                AUTO's choice for full-CRC batches of up to 128 chunks per CU
                                of >= 2 KiB (12 per CU shorter; 16 per CU when the lengths
-                               are device-side only).  Windows (fastcrc) never split */
+                               are device-side only); fastcrc windows of >= 2 KiB split as
+                               two messages per chunk, shorter ones keep the window kernels */
     CRC32HIP_NUM_VARIANTS = 8
 };
 int crc32hip_fixed_variant(const void *d_base, uint64_t n, uint32_t len, uint64_t stride,

@@ -35,6 +35,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=2)
     ap.add_argument("--crc", action="store_true")
     ap.add_argument("--fed", action="store_true")
+    ap.add_argument("--fastcrc", type=int, default=0, help="with --crc: blk_make_crc's window size")
     a = ap.parse_args()
     import torch
     from sproxy_amd._lib import lib
@@ -48,7 +49,7 @@ def main():
                                              ctypes.c_uint64, vp, vp]
     stream = torch.cuda.Stream()
     sp = ctypes.c_void_p(stream.cuda_stream)
-    out = {"len": a.len, "iters": a.iters, "sizes": {}}
+    out = {"len": a.len, "iters": a.iters, "fastcrc": a.fastcrc, "sizes": {}}
     nmax = max(int(x) for x in a.sizes.split(","))
     data = torch.empty(nmax * a.len, dtype=torch.uint8, device="cuda")
     rc = L.md5hip_fill_synthetic(ctypes.c_void_p(data.data_ptr()), data.numel(), 12345, sp)
@@ -70,9 +71,9 @@ def main():
                     d, o, ln = (ctypes.c_void_p(t.data_ptr()) for t in (data, offs, lens))
                     out_p = ctypes.c_void_p(dig[v].data_ptr())
                     if a.crc and code < 100:
-                        return L.crc32hip_desc_variant(d, o, ln, None, n, 0, out_p, sp, code)
+                        return L.crc32hip_desc_variant(d, o, ln, None, n, a.fastcrc, out_p, sp, code)
                     if a.crc:
-                        return L.crc32hip_fixed_variant(d, n, a.len, a.len, 0, out_p, sp, code - 100)
+                        return L.crc32hip_fixed_variant(d, n, a.len, a.len, a.fastcrc, out_p, sp, code - 100)
                     if code <= -1000:
                         return D.md5diag_fed_split_excl(-code - 1000, 0, d, o, ln, None, n, out_p, sp)
                     if code < 0:

@@ -1352,11 +1352,49 @@ crc32_fast_pipe(const uint8_t* __restrict__ base, const uint64_t* __restrict__ o
 // microseconds of work instead of one 16 KiB chain.  256-thread workgroups
 // (4 chunks) share one copy of the 64 KiB perm tables.
 // ---------------------------------------------------------------------------
+// The CRC-32 (crc32.c: ~0 in, ~ out) of [m, m + L) by the whole wave; the
+// result is valid in lane 63.
+__device__ __forceinline__ uint32_t split_crc_msg(Crc32PermHasher& h, const uint8_t* m, uint32_t L,
+                                                  uint32_t lane) {
+  const uint32_t nseg = (uint32_t)(((uint64_t)L + 255u) >> 8);
+  const uint32_t r0 = nseg ? L - ((nseg - 1u) << 8) : 0u;          // first segment: 1..256 B
+  const uint32_t npass = (nseg + 63u) >> 6;
+  uint32_t acc = 0;
+  for (uint32_t p = 0; p < npass; ++p) {
+    // passes right-aligned: the first pass's low lanes hold no segment
+    const int64_t s = (int64_t)nseg - 64 * (int64_t)(npass - p) + (int64_t)lane;
+    uint32_t reg = 0;
+    if (s >= 0) {
+      const uint64_t start = s == 0 ? 0u : (uint64_t)r0 + ((uint64_t)(s - 1) << 8);
+      typename Crc32PermHasher::State st{s == 0 ? 0xFFFFFFFFu : 0u};
+      lane_range<Crc32PermHasher, 2>(h, st, m + start, s == 0 ? r0 : 256u);
+      reg = ~st.c;                               // the raw register (finish complements)
+    }
+    // lane j ends holding segments [j - 2^(l+1) + 1, j] when j = 2^(l+1) - 1 mod 2^(l+1)
+    auto level = [&](auto lv) __attribute__((always_inline)) {
+      constexpr int l = decltype(lv)::value;
+      const uint32_t left = (uint32_t)__shfl_up((int)reg, 1u << l, 64);
+      const uint32_t sh = crc_shift<l>(left);
+      if ((lane & ((2u << l) - 1u)) == (2u << l) - 1u) reg ^= sh;
+    };
+    level(std::integral_constant<int, 0>{});
+    level(std::integral_constant<int, 1>{});
+    level(std::integral_constant<int, 2>{});
+    level(std::integral_constant<int, 3>{});
+    level(std::integral_constant<int, 4>{});
+    level(std::integral_constant<int, 5>{});
+    acc = crc_shift<6>(acc) ^ reg;               // lane 63: all passes so far
+  }
+  return L ? ~acc : 0u;                          // empty: crc32.c returns ~~0 = 0
+}
+
+// F > 0: blk_make_crc's fastcrc mode, CRC(first F bytes) ^ CRC(last F bytes)
+// for chunks longer than F (blk_io.c:408-424), each window split as above.
 template <bool kImplicit>
 __global__ void __launch_bounds__(256)
 crc32_split(const uint8_t* __restrict__ base, const uint64_t* __restrict__ offs,
             const uint32_t* __restrict__ lens, const uint32_t* __restrict__ order, uint64_t n,
-            uint64_t stride, uint32_t flen, uint32_t* __restrict__ out) {
+            uint64_t stride, uint32_t flen, uint32_t F, uint32_t* __restrict__ out) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[Crc32PermHasher::kLdsBytes];
   Crc32PermHasher h;
   h.setup(lds);                                  // all threads, before any exit
@@ -1367,36 +1405,12 @@ crc32_split(const uint8_t* __restrict__ base, const uint64_t* __restrict__ offs,
     const uint64_t c = (!kImplicit && order) ? (uint64_t)order[q] : q;
     const uint8_t* m = base + (kImplicit ? c * stride : offs[c]);
     const uint32_t L = kImplicit ? flen : lens[c];
-    const uint32_t nseg = (uint32_t)(((uint64_t)L + 255u) >> 8);
-    const uint32_t r0 = nseg ? L - ((nseg - 1u) << 8) : 0u;        // first segment: 1..256 B
-    const uint32_t npass = (nseg + 63u) >> 6;
-    uint32_t acc = 0;
-    for (uint32_t p = 0; p < npass; ++p) {
-      // passes right-aligned: the first pass's low lanes hold no segment
-      const int64_t s = (int64_t)nseg - 64 * (int64_t)(npass - p) + (int64_t)lane;
-      uint32_t reg = 0;
-      if (s >= 0) {
-        const uint64_t start = s == 0 ? 0u : (uint64_t)r0 + ((uint64_t)(s - 1) << 8);
-        typename Crc32PermHasher::State st{s == 0 ? 0xFFFFFFFFu : 0u};
-        lane_range<Crc32PermHasher, 2>(h, st, m + start, s == 0 ? r0 : 256u);
-        reg = ~st.c;                             // the raw register (finish complements)
-      }
-      // lane j ends holding segments [j - 2^(l+1) + 1, j] when j = 2^(l+1) - 1 mod 2^(l+1)
-      auto level = [&](auto lv) __attribute__((always_inline)) {
-        constexpr int l = decltype(lv)::value;
-        const uint32_t left = (uint32_t)__shfl_up((int)reg, 1u << l, 64);
-        const uint32_t sh = crc_shift<l>(left);
-        if ((lane & ((2u << l) - 1u)) == (2u << l) - 1u) reg ^= sh;
-      };
-      level(std::integral_constant<int, 0>{});
-      level(std::integral_constant<int, 1>{});
-      level(std::integral_constant<int, 2>{});
-      level(std::integral_constant<int, 3>{});
-      level(std::integral_constant<int, 4>{});
-      level(std::integral_constant<int, 5>{});
-      acc = crc_shift<6>(acc) ^ reg;             // lane 63: all passes so far
-    }
-    if (lane == 63u) out[c] = L ? ~acc : 0u;     // empty: crc32.c returns ~~0 = 0
+    uint32_t crc;
+    if (F && L > F)
+      crc = split_crc_msg(h, m, F, lane) ^ split_crc_msg(h, m + (L - F), F, lane);
+    else
+      crc = split_crc_msg(h, m, L, lane);
+    if (lane == 63u) out[c] = crc;
   }
 }
 

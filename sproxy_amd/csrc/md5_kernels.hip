@@ -51,12 +51,16 @@ int launched() {
 
 // Compute units of the current device (grid sizing of one-workgroup-per-CU
 // kernels and HYBRID's long-wave count).
+// Cached per device: a small launch asks several times (planner, grid, the
+// CRC choice), and the attribute query is a runtime call each time.
 int cu_count() {
+  static std::atomic<int> cached[64];
   int dev = 0, cus = 0;
-  if (hipGetDevice(&dev) != hipSuccess ||
-      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-      cus <= 0)
+  if (hipGetDevice(&dev) != hipSuccess) return 256;
+  if (dev >= 0 && dev < 64 && (cus = cached[dev].load(std::memory_order_relaxed)) > 0) return cus;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
     return 256;
+  if (dev >= 0 && dev < 64) cached[dev].store(cus, std::memory_order_relaxed);
   return cus;
 }
 
@@ -137,6 +141,7 @@ constexpr uint64_t kFedGroupsPerCu = 1;
 // >= 2 KiB and up to 12 per CU below; with it unknown (device-side lengths),
 // up to kCrcSplitPerCu.
 constexpr uint64_t kCrcSplitPerCu = 16;
+constexpr uint32_t kCrcSplitMinWindow = 2048;    // fastcrc windows split from this size
 bool crc_split_fits(uint64_t n, uint64_t len) {
   const uint64_t cus = (uint64_t)cu_count();
   if (len == 0) return n <= kCrcSplitPerCu * cus;
@@ -164,6 +169,8 @@ int md5hip_abi_version(void) { return MD5HIP_ABI_VERSION; }
 __attribute__((visibility("hidden"))) int md5hip_crc_desc_choice(uint64_t n, uint64_t mean_len) {
   return crc_split_fits(n, mean_len ? mean_len : 1) ? CRC32HIP_SPLIT : CRC32HIP_AUTO;
 }
+// (with fastcrc the batcher passes 2n windows of fastcrc bytes; windows under
+// kCrcSplitMinWindow keep the window kernels whatever the variant says)
 
 // The shipped kernels are fixed: the round-1 A/B variants live in the
 // diagnostic library (md5_diag.hip, md5_kernels_ab.h), and no environment
@@ -299,10 +306,16 @@ int crc32hip_fixed_variant(const void* d_base, uint64_t n, uint32_t len, uint64_
   const uint8_t* base = (const uint8_t*)d_base;
   const uint64_t g = (n + kDescBlock - 1) / kDescBlock;
   if (g > 0x7fffffffull) return -EINVAL;
-  if (!(fastcrc && len > fastcrc) && crc_split_pick(n, variant, len ? len : 1)) {
+  // the split kernel: full-CRC batches, and windowed ones (two messages of
+  // fastcrc bytes per chunk) with windows of >= 2 KiB; shorter windows are
+  // chains short enough for the window kernels (F = 1000: split 28-48 us
+  // against 30-32 us, F = 4096: 15-31 against 57-60; profiles/r03af/)
+  const bool windows = fastcrc && len > fastcrc;
+  if ((!windows || fastcrc >= kCrcSplitMinWindow) &&
+      crc_split_pick(windows ? 2 * n : n, variant, windows ? fastcrc : (len ? len : 1))) {
     hipLaunchKernelGGL(crc32_split<true>, dim3(crc_split_grid(n)), dim3(256), 0, s, base,
                        (const uint64_t*)nullptr, (const uint32_t*)nullptr,
-                       (const uint32_t*)nullptr, n, stride, len, d_crcs);
+                       (const uint32_t*)nullptr, n, stride, len, fastcrc, d_crcs);
     return launched();
   }
   if (fastcrc && len > fastcrc) {
@@ -356,10 +369,10 @@ int crc32hip_desc_variant(const void* d_base, const uint64_t* d_offsets, const u
   hipStream_t s = (hipStream_t)stream;
   const uint64_t g = (n + kDescBlock - 1) / kDescBlock;
   if (g > 0x7fffffffull) return -EINVAL;
-  if (fastcrc == 0 && crc_split_pick(n, variant)) {
+  if ((fastcrc == 0 || fastcrc >= kCrcSplitMinWindow) && crc_split_pick(fastcrc ? 2 * n : n, variant)) {
     hipLaunchKernelGGL(crc32_split<false>, dim3(crc_split_grid(n)), dim3(256), 0, s,
                        (const uint8_t*)d_base, d_offsets, d_lens, d_order, n, (uint64_t)0, 0u,
-                       d_crcs);
+                       fastcrc, d_crcs);
     return launched();
   }
   if (fastcrc == 64 || fastcrc == 128) {

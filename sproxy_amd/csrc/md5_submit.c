@@ -416,8 +416,9 @@ static int slot_enqueue(md5hip_batcher *b, struct slot *sl)
         rc = sl->kind == MD5HIP_DIGEST_CRC32
                  ? crc32hip_desc_variant(sl->d_data, doff, dlen, ord, n, sl->fastcrc,
                                          (uint32_t *)dst, sl->stream,
-                                         sl->fastcrc ? CRC32HIP_AUTO
-                                                     : md5hip_crc_desc_choice(n, sl->load / n - 64))
+                                         md5hip_crc_desc_choice(sl->fastcrc ? 2 * n : n,
+                                                                sl->fastcrc ? sl->fastcrc
+                                                                            : sl->load / n - 64))
                  : md5hip_digest_desc_variant(sl->d_data, doff, dlen, ord, n,
                                               dst, sl->stream, dvar);
         if (rc) return rc;

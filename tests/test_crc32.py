@@ -230,6 +230,12 @@ def test_gpu_crc_split_desc(cuda, align):
         for v in ("split", "auto", "xdma16"):
             got = m.crc32_desc(d, t_off, t_len, o, variant=v).cpu().numpy().view(np.uint32)
             assert np.array_equal(got, want), (v, order is None)
+    # fastcrc windows (head ^ tail, blk_io.c:408-424) split as two messages
+    for fast in (4, 100, 1000, 4096, 16368):
+        want_f = gen.oracle_crc32_batch(buf, offs, lens, fast)
+        for v in ("split", "auto"):
+            got = m.crc32_desc(d, t_off, t_len, fastcrc=fast, variant=v).cpu().numpy().view(np.uint32)
+            assert np.array_equal(got, want_f), (fast, v)
     # a netcache vector: 64 x 16 KiB pages; AUTO splits it (<= 4 chunks per CU)
     n, L = 64, 16384
     host = gen.xorshift_array(n * L, seed=64)
