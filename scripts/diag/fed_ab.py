@@ -77,7 +77,8 @@ def main():
     print(json.dumps({"chain_probe": probe}), flush=True)
 
     def fed(base, dO, dL, dR, n, dig, v=4, L=0):
-        if v >= 200:   # exclusive chain CUs: 200 = fed pairs + XDMA, 201 = HYBRID part + XDMA
+        if v >= 200:   # exclusive chain CUs: 200 = fed pairs + XDMA, 201 = HYBRID part + XDMA,
+            # 203 = fed pairs + the rest as HYBRID
             return D.md5diag_fed_split_excl(v - 200, L, base.data_ptr(), dO.data_ptr(), dL.data_ptr(),
                                             dR.data_ptr(), n, dig.data_ptr(), st)
         if v >= 100:   # split launches: 100 = fed pairs + XDMA, 101 = HYBRID part + XDMA
@@ -122,13 +123,14 @@ def main():
         firsts = Lk[order[::64]]
         Lmax = int((firsts == firsts.max()).sum())
         eq = []
-        for v in (4, 100, 101, 200, 201):
+        for v in (4, 100, 101, 200, 201, 203):
             assert fed(big, dO, dL, dR, n, dig, v, Lmax) == 0
             torch.cuda.synchronize()
             eq.append(bool(torch.equal(dig, ref)))
         legs = {"hybrid": lambda: m.digest_desc(big, dO, dL, dR, out=dig, variant="hybrid"),
                 "fed_split_excl": lambda: fed(big, dO, dL, dR, n, dig, 200, Lmax),
                 "hybrid_split_excl": lambda: fed(big, dO, dL, dR, n, dig, 201, Lmax),
+                "fed_excl_rest_hybrid": lambda: fed(big, dO, dL, dR, n, dig, 203, Lmax),
                 "fed_one_launch": lambda: fed(big, dO, dL, dR, n, dig, 4),
                 "fed_split": lambda: fed(big, dO, dL, dR, n, dig, 100),
                 "hybrid_split": lambda: fed(big, dO, dL, dR, n, dig, 101)}

@@ -1405,19 +1405,22 @@ extern "C" int md5diag_fed_split_excl(int kind, uint64_t L, const void* d_base, 
   hipStream_t s = (hipStream_t)stream;
   if (L > groups) L = groups;
   const uint64_t nfirst = L * 64 < n ? L * 64 : n;
-  const void* k = kind == 0 ? reinterpret_cast<const void*>(md5_desc_fed_pairs<4, 2>)
+  const void* k = kind != 1 ? reinterpret_cast<const void*>(md5_desc_fed_pairs<4, 2>)
                             : reinterpret_cast<const void*>(md5_desc_hybrid);
   uint32_t pad = 0;
   if (int e = excl_pad(k, &pad)) return e;
   if (hipEventRecord(e0, s) != hipSuccess || hipStreamWaitEvent(hs, e0, 0) != hipSuccess) return -EIO;
-  if (kind == 0)
+  if (kind != 1)
     hipLaunchKernelGGL((md5_desc_fed_pairs<4, 2>), dim3((uint32_t)L), dim3(128), pad, hs, b, offs, lens,
                        order, nfirst, (uint4*)d_out);
   else
     hipLaunchKernelGGL(md5_desc_hybrid, dim3((uint32_t)L), dim3(64), pad, hs, b, offs, lens, order, nfirst,
                        (uint4*)d_out, (uint32_t)L);
   if (hipGetLastError() != hipSuccess) return -EIO;
-  if (n > nfirst)
+  if (n > nfirst && kind == 3)     // the rest as HYBRID: its own longest groups lane-direct
+    hipLaunchKernelGGL(md5_desc_hybrid, dim3((uint32_t)(groups - L)), dim3(64), 0, s, b, offs, lens,
+                       order + nfirst, n - nfirst, (uint4*)d_out, (uint32_t)(diag_cus() - (int)L));
+  else if (n > nfirst)
     hipLaunchKernelGGL(md5_desc_xdma, dim3((uint32_t)(groups - L)), dim3(64), 0, s, b, offs, lens,
                        order + nfirst, n - nfirst, (uint4*)d_out);
   if (hipGetLastError() != hipSuccess) return -EIO;
