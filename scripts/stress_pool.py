@@ -5,7 +5,8 @@ choosing at random per step among
   pool submit / submit_async (+wait later, any order) / submit_iov(_async) /
   verify_iov with one flipped digest / host_fixed,
   queue submit_device(_async) with host or device digests, ordered after
-  the thread's own torch stream,
+  the thread's own torch stream, and the same through a CRC-32 queue
+  (blk_make_crc digests; small and long-block vectors pick the split kernel),
 over random vectors (1-300 chunks, 0 B - 1 MiB, tails, zero-length) cut from
 a registered page heap or from pageable memory.  Every digest is checked
 against digests the oracle computed up front.  Prints one JSON summary; exits
@@ -27,6 +28,12 @@ sys.path.insert(0, os.path.join(REPO, "tests"))
 import gen  # noqa: E402
 
 
+def _flat(got, exp):
+    """A CRC ticket's result as uint32 values like its expectation."""
+    got = np.asarray(got.cpu() if hasattr(got, "cpu") else got)
+    return got.view(np.uint32).reshape(-1) if exp.dtype == np.uint32 else got
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--secs", type=float, default=60.0)
@@ -45,6 +52,7 @@ def main():
     offs, total = gen.pack_offsets(lens, align=16)
     heap = gen.xorshift_array(total + 64, seed=77)
     want = gen.oracle_digests(heap, offs, lens)
+    want_crc = gen.oracle_crc32_batch(heap, offs, lens)
     pageable = heap.copy()                      # the same bytes, never registered
     dev = torch.from_numpy(heap).cuda()
     torch.cuda.synchronize()
@@ -52,6 +60,8 @@ def main():
     pool = m.Pool(tuple([0] * a.devices), slice_bytes=32 << 20, nslots=3)
     pool.set_split(8 << 20)
     q = m.Queue(device=0, max_chunks=1 << 16)
+    qc = m.Queue(device=0, max_chunks=1 << 16)    # CRC-32 (blk_make_crc) through its own queue
+    qc.set_digest(m.Batcher.CRC32)
     stop = time.perf_counter() + a.secs
     counts, errors = {}, []
     lock = threading.Lock()
@@ -71,7 +81,8 @@ def main():
                 src = heap if r.random() < 0.6 else pageable
                 bufs = [src[offs[i]:offs[i] + lens[i]] for i in idx]
                 exp = want[idx]
-                op = r.choice(["sync", "async", "iov", "iov_async", "verify", "qdev", "qdev_async", "fixed"])
+                op = r.choice(["sync", "async", "iov", "iov_async", "verify", "qdev", "qdev_async", "fixed",
+                               "crc_qdev", "crc_qdev_async"])
                 if op == "sync":
                     assert np.array_equal(pool.submit(bufs), exp), op
                 elif op == "async":
@@ -101,6 +112,16 @@ def main():
                             assert np.array_equal(got, exp), op
                         else:
                             held.append((q.submit_device_async(ptrs, L), exp))
+                elif op in ("crc_qdev", "crc_qdev_async"):
+                    ptrs = np.asarray([dev.data_ptr() + offs[i] for i in idx], np.uint64)
+                    L = np.asarray([lens[i] for i in idx], np.uint32)
+                    ec = want_crc[idx]
+                    with torch.cuda.stream(stream):
+                        if op == "crc_qdev":
+                            got = np.asarray(qc.submit_device(ptrs, L)).view(np.uint32).reshape(-1)
+                            assert np.array_equal(got, ec), op
+                        else:
+                            held.append((qc.submit_device_async(ptrs, L), ec))
                 else:
                     j = r.randrange(nchunks - 40)
                     n = r.randint(1, 40)
@@ -114,9 +135,9 @@ def main():
                 note(op)
                 if len(held) > 6 or (held and r.random() < 0.3):
                     h, e = held.pop(r.randrange(len(held)))
-                    assert np.array_equal(h.wait(), e), "held"
+                    assert np.array_equal(_flat(h.wait(), e), e), "held"
             for h, e in held:
-                assert np.array_equal(h.wait(), e), "held"
+                assert np.array_equal(_flat(h.wait(), e), e), "held"
         except Exception as ex:                      # pragma: no cover
             with lock:
                 errors.append(f"thread {t}: {ex!r}")
@@ -131,13 +152,16 @@ def main():
     st = pool.stats()
     dstats = [pool.device_stats(g) for g in range(a.devices)]
     qst = q.stats()
+    qcst = qc.stats()
     pool.close()
     q.close()
+    qc.close()
     m.unregister_host(heap)
     print(json.dumps({"secs": round(wall, 1), "threads": a.threads, "ops": counts,
                       "pool": st, "pool_device_launches": [d["launches"] for d in dstats],
                       "pool_coalesced": [d["coalesced_launches"] for d in dstats],
                       "queue": {k: qst[k] for k in ("submissions", "launches", "coalesced_launches")},
+                      "crc_queue": {k: qcst[k] for k in ("submissions", "launches", "coalesced_launches")},
                       "errors": errors}))
     return 1 if errors else 0
 
