@@ -890,13 +890,23 @@ __device__ __forceinline__ void lds_handoff(uint32_t& a, uint32_t& b, uint32_t& 
 
 constexpr uint32_t kFedTable = 16 * 64 * 16;     // one block's addends, 16 KiB
 
-template <int D, int NT, bool kFeedOff = false>
-__device__ __forceinline__ void fed_long_group(const uint8_t* __restrict__ base, uint4* __restrict__ out,
-                                               uint8_t* lds, bool feeder, uint32_t nfull,
-                                               uint32_t bmax, uint64_t off, uint32_t len,
-                                               uint64_t c, bool live) {
+// kDigest = false (MD5Update on contexts): the chain starts from st0 and the
+// state after the lane's nfull blocks is returned, with no padding or store.
+// kAbs: off is an absolute address (base unused; offsetting a null base would
+// be undefined), taken as a global pointer so the feeder's loads stay global.
+template <int D, int NT, bool kFeedOff = false, bool kDigest = true, bool kAbs = false>
+__device__ __forceinline__ State fed_long_group(const uint8_t* __restrict__ base, uint4* __restrict__ out,
+                                                uint8_t* lds, bool feeder, uint32_t nfull,
+                                                uint32_t bmax, uint64_t off, uint32_t len,
+                                                uint64_t c, bool live, State st0 = initial_state()) {
   static_assert(D % 2 == 0, "paired refill");
-  const uint8_t* chunk = base + off;
+  auto at = [&](uint64_t o) __attribute__((always_inline)) -> const uint8_t* {
+    if constexpr (kAbs)
+      return (const uint8_t*)(const __attribute__((address_space(1))) uint8_t*)(uintptr_t)o;
+    else
+      return base + o;
+  };
+  const uint8_t* chunk = at(off);
   const uint32_t lane = threadIdx.x & 63u;
   auto tab = [&](uint32_t k) __attribute__((always_inline)) {
     return reinterpret_cast<uint4(*)[64]>(lds + (NT == 2 ? (k & 1u) * kFedTable : 0u));
@@ -909,7 +919,7 @@ __device__ __forceinline__ void fed_long_group(const uint8_t* __restrict__ base,
     const uint32_t mlane = __builtin_ctzll(__ballot(nfull == bmax));
     const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)off, (int)mlane, 64);
     const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(off >> 32), (int)mlane, 64);
-    const uint4* p = reinterpret_cast<const uint4*>(base + (nfull ? off : ((uint64_t)hi << 32) | lo));
+    const uint4* p = reinterpret_cast<const uint4*>(at(nfull ? off : ((uint64_t)hi << 32) | lo));
     const uint32_t lastb = (nfull ? nfull : bmax) - 1u;
     uint4 R[D][4];
     if constexpr (!kFeedOff) {
@@ -952,9 +962,9 @@ __device__ __forceinline__ void fed_long_group(const uint8_t* __restrict__ base,
         }
       }
     }
-    return;
+    return st0;
   }
-  State st = initial_state();
+  State st = st0;
   uint4 q[2][16];                                // W(k) and W(k+1), alternating
   lds_handoff();                                 // X_init / B_init
 #pragma unroll
@@ -984,11 +994,14 @@ __device__ __forceinline__ void fed_long_group(const uint8_t* __restrict__ base,
     blk(k, q[0], q[1]);
     if (k + 1 < bmax) blk(k + 1, q[1], q[0]);    // wave-uniform
   }
-  if (live) {
-    Md5Hasher<true> h;
-    h.finish(st, chunk + ((uint64_t)nfull << 6), len & 63u, len);
-    h.store(out, c, st);
+  if constexpr (kDigest) {
+    if (live) {
+      Md5Hasher<true> h;
+      h.finish(st, chunk + ((uint64_t)nfull << 6), len & 63u, len);
+      h.store(out, c, st);
+    }
   }
+  return st;
 }
 
 // Small batches as fed pairs ("FED", round 3): one 2-wave workgroup per
@@ -1474,10 +1487,14 @@ struct LaneSpan {
 
 // One wave per 64 contexts (one-wave workgroups, the loader's 8 KiB image);
 // 125 VGPRs hold it at 4 waves per SIMD, as md5_desc_xdma's clobber does.
-__global__ void __launch_bounds__(64)
-md5_update_ctx(uint32_t* __restrict__ ctxs, const uint64_t* __restrict__ ptrs,
-               const uint32_t* __restrict__ lens, uint64_t n) {
-  __shared__ __attribute__((aligned(16))) uint8_t img[8192];
+// The body, per wave.  kFed: the whole blocks run as the
+// chain wave of a fed pair (md5_update_ctx_fed, bmax = the group's most
+// blocks); otherwise through the descriptor loader into `img` (8 KiB).
+template <bool kFed>
+__device__ __forceinline__ void update_ctx_body(uint32_t* __restrict__ ctxs,
+                                                const uint64_t* __restrict__ ptrs,
+                                                const uint32_t* __restrict__ lens, uint64_t n,
+                                                uint8_t* img, uint32_t bmax) {
   const uint64_t first = (uint64_t)blockIdx.x * 64u;
   const uint64_t i = first + (threadIdx.x & 63u);
   const bool live = i < n;
@@ -1529,11 +1546,17 @@ md5_update_ctx(uint32_t* __restrict__ ctxs, const uint64_t* __restrict__ ptrs,
     any = true;
   }
   const uint32_t nblk = append_only ? 0u : (len - pos) >> 6;   // md5.c:204-210
-  CtxHasher h;
-  h.s0 = st;
-  h.res = st;
-  desc_xpose_group<2, CtxHasher, 0, 1, false, true, true, LaneSpan>(
-      h, nullptr, LaneSpan{(uint64_t)(uintptr_t)(data + pos), nblk << 6}, n, first, nullptr, img);
+  if constexpr (kFed) {
+    st = fed_long_group<4, 2, false, false, true>(nullptr, nullptr, img, false, nblk, bmax,
+                                            (uint64_t)(uintptr_t)(data + pos), nblk << 6, 0, live, st);
+  } else {
+    CtxHasher h;
+    h.s0 = st;
+    h.res = st;
+    desc_xpose_group<2, CtxHasher, 0, 1, false, true, true, LaneSpan>(
+        h, nullptr, LaneSpan{(uint64_t)(uintptr_t)(data + pos), nblk << 6}, n, first, nullptr, img);
+    st = h.res;
+  }
   if (!live) return;
   if (append_only) {
 #pragma unroll
@@ -1541,7 +1564,6 @@ md5_update_ctx(uint32_t* __restrict__ ctxs, const uint64_t* __restrict__ ptrs,
     ctx_store(cp, c);
     return;
   }
-  st = h.res;
   if (nblk) {                                          // the bytes md5.c leaves in in[] past the tail
     const uint8_t* lb = data + pos + ((uint64_t)(nblk - 1) << 6);
     uint4 w[4];
@@ -1567,6 +1589,46 @@ md5_update_ctx(uint32_t* __restrict__ ctxs, const uint64_t* __restrict__ ptrs,
   }
   c.w[0] = st.a; c.w[1] = st.b; c.w[2] = st.c; c.w[3] = st.d;
   ctx_store(cp, c);
+}
+
+__global__ void __launch_bounds__(64)
+md5_update_ctx(uint32_t* __restrict__ ctxs, const uint64_t* __restrict__ ptrs,
+               const uint32_t* __restrict__ lens, uint64_t n) {
+  __shared__ __attribute__((aligned(16))) uint8_t img[8192];
+  update_ctx_body<false>(ctxs, ptrs, lens, n, img, 0u);
+}
+
+// Few contexts (at most one 64-context group per CU): the launch is one
+// update's serial chain, so the whole blocks run as fed pairs (a feeder wave
+// forms M + K, as md5_desc_fed).  Both waves work out each lane's span of
+// whole blocks from its context and length alone; a group with a span that
+// is not 16-B aligned, or without two blocks, runs the loader body on wave 0.
+__global__ void __launch_bounds__(128)
+md5_update_ctx_fed(uint32_t* __restrict__ ctxs, const uint64_t* __restrict__ ptrs,
+                   const uint32_t* __restrict__ lens, uint64_t n) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds[2 * kFedTable];
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint64_t first = (uint64_t)blockIdx.x * 64u;
+  const uint64_t i = first + (threadIdx.x & 63u);
+  const bool live = i < n;
+  const uint32_t len = live ? lens[i] : 0u;
+  const uint8_t* data = reinterpret_cast<const uint8_t*>(live ? ptrs[i] : 0ull);
+  const uint32_t t = (ctxs[22 * (live ? i : first) + 4] >> 3) & 63u;   // pending bytes
+  const bool append_only = t && len < 64u - t;
+  const uint32_t pos = append_only ? 0u : (t ? 64u - t : 0u);
+  const uint32_t nblk = append_only ? 0u : (len - pos) >> 6;
+  const uint32_t bmax = wave_max(nblk);
+  const bool unaligned = __ballot(nblk && ((((uintptr_t)data + pos) & 15u) != 0)) != 0;
+  if (bmax < kFedMinBlocks || unaligned) {     // wave-uniform, the same in both waves
+    if (wave == 0) update_ctx_body<false>(ctxs, ptrs, lens, n, lds, 0u);
+    return;
+  }
+  if (wave == 1) {
+    fed_long_group<4, 2, false, false, true>(nullptr, nullptr, lds, true, nblk, bmax,
+                                       (uint64_t)(uintptr_t)(data + pos), nblk << 6, 0, live);
+    return;
+  }
+  update_ctx_body<true>(ctxs, ptrs, lens, n, lds, bmax);
 }
 
 __global__ void __launch_bounds__(256)

@@ -412,6 +412,13 @@ int md5hip_update_ctx(struct MD5Context* d_ctxs, const void* const* d_ptrs, cons
   if (int e = device_ok()) return e;
   const uint64_t g = (n + 63) / 64;                   // one wave per 64 contexts
   if (g > 0x7fffffffull) return -EINVAL;
+  if (g <= kFedGroupsPerCu * (uint64_t)cu_count()) {
+    // few contexts: one update's chain bounds the launch; fed pairs shorten it
+    hipLaunchKernelGGL(md5_update_ctx_fed, dim3((uint32_t)g), dim3(128), 0, (hipStream_t)stream,
+                       reinterpret_cast<uint32_t*>(d_ctxs), reinterpret_cast<const uint64_t*>(d_ptrs),
+                       d_lens, n);
+    return launched();
+  }
   hipLaunchKernelGGL(md5_update_ctx, dim3((uint32_t)g), dim3(64), 0, (hipStream_t)stream,
                      reinterpret_cast<uint32_t*>(d_ctxs), reinterpret_cast<const uint64_t*>(d_ptrs),
                      d_lens, n);

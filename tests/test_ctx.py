@@ -138,15 +138,18 @@ def test_bit_count_carry_and_high_word(cuda):
     assert np.array_equal(m.final_ctx(ctx).cpu().numpy(), ref.final(ctx_h))
 
 
-def test_lds_dma_waves_and_pending_blocks(cuda):
+@pytest.mark.parametrize("groups", [24, 300])
+def test_lds_dma_waves_and_pending_blocks(cuda, groups):
     """Waves whose update data is 16-B (and 128-B) aligned take the LDS-DMA
     loader (md5_update_ctx -> desc_xpose_group); contexts with a pending
     partial block shift the bulk by 64 - t bytes, so neighbouring waves mix
-    the DMA and lane-direct paths.  Three rounds, every context byte against
-    the reference after each."""
+    the DMA and lane-direct paths.  24 groups (at most one per CU) run as fed
+    pairs (md5_update_ctx_fed) where a group's bulk is 16-B aligned, on the
+    loader otherwise; 300 groups always take the loader.  Three rounds,
+    every context byte against the reference after each."""
     ref = HostRef()
-    rng = np.random.default_rng(4242)
-    n = 64 * 24
+    rng = np.random.default_rng(4242 + groups)
+    n = 64 * groups
     data = gen.xorshift_array(12 << 20, seed=91)
     d = _dev(data, cuda)
     ctx_h = np.zeros((n, 88), np.uint8)
