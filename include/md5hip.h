@@ -113,7 +113,10 @@ int md5hip_digest_desc_variant(const void *d_base, const uint64_t *d_offsets,
  *                      device array (one update per context per call; 0 = none);
  *   md5hip_final_ctx   digest i (16 B, 16-B aligned array) as MD5Final, ctx i
  *                      zeroed (md5.c:221-265).
- * Calls on one stream apply in order, so k updates are k launches.
+ * Calls on one stream apply in order, so k updates are k launches.  An update
+ * over at most 64 contexts per CU lasts one context's serial chain and runs its
+ * whole blocks as fed pairs: keep each context's data 16-B
+ * aligned past its pending bytes to stay on that path.
  */
 struct MD5Context;
 int md5hip_init_ctx(struct MD5Context *d_ctxs, uint64_t n, void *stream);
