@@ -30,7 +30,12 @@
 extern "C" {
 #endif
 
-#define MD5HIP_ABI_VERSION 2
+/* ABI 3 (round 4): md5_batch_submit_device_after (an ordering flag apart from
+ * the producer stream, so the null stream can be ordered on); round 3 had
+ * already grown MD5HIP_DESC_NUM_VARIANTS 6 -> 7 (FED) and CRC32HIP_NUM_VARIANTS
+ * 7 -> 8 (SPLIT) -- appended values, compatible -- and made the pool route a
+ * submission whole (same results; set_digest no longer drains). */
+#define MD5HIP_ABI_VERSION 3
 
 /* Fixed-length kernels for md5hip_digest_fixed_variant.  ABI 2: the round-1
  * A/B variants (values 2-9) moved to the diagnostic library (md5_diag.hip);
@@ -336,6 +341,17 @@ int md5_batch_submit_device(md5hip_batcher *b, const uint64_t *d_ptrs, const uin
 int md5_batch_submit_device_on(md5hip_batcher *b, const uint64_t *d_ptrs, const uint32_t *lens,
                                uint64_t n, unsigned char *digests, int digests_on_device,
                                void *producer_stream, uint64_t *ticket);
+/* ABI 3: the same with the ordering named apart from the stream, so that the
+ * null stream can be the producer: order != 0 = after all work enqueued on
+ * producer_stream before the call, where producer_stream NULL is the null
+ * (default) stream of the batcher's device -- the stream HIP and torch use
+ * when the producer names none, which the batcher's non-blocking streams do
+ * NOT wait for on their own; order == 0 = no ordering (producer_stream is
+ * ignored).  md5_batch_submit_device_on(.., s, ..) is this with
+ * order = (s != NULL). */
+int md5_batch_submit_device_after(md5hip_batcher *b, const uint64_t *d_ptrs, const uint32_t *lens,
+                                  uint64_t n, unsigned char *digests, int digests_on_device,
+                                  void *producer_stream, int order, uint64_t *ticket);
 /* Block until submission `ticket` has delivered its digests: 0 or -errno.
  * A ticket still coalescing in the open slot is launched at once when
  * nothing is in flight (no linger); otherwise its slot goes out as soon as a

@@ -1,0 +1,68 @@
+#!/usr/bin/env python3
+"""The netcache checksum call site at the reference's scale, measured with
+build/c/asio_scale (tests/c/asio_scale.c: T threads each submitting a vector
+of B blocks of L bytes synchronously; latency, CPU per call, every digest
+checked against the oracle).
+
+  --matrix threads  VERDICT r03 item 1: 8 / 64 / 256 synchronous callers of
+                    64 x 16 KiB on one batcher and on a pool over (0, 0)
+  --matrix chunk    VERDICT r03 item 2: netcache's shipped chunk_size 128 KiB
+                    (httpd.c:8627) and 1 MiB next to 16 KiB, vectors of 8 and
+                    64 blocks, 1 / 8 / 64 callers, through the batcher and on
+                    the calling thread (product MD5Init/Update/Final)
+
+Writes one JSON file (--out) with every run; prints each run as it ends.
+usage: asio_scale.py --matrix threads|chunk [--secs 3] [--out FILE]"""
+import argparse
+import json
+import os
+import subprocess
+import sys
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+EXE = os.path.join(REPO, "build", "c", "asio_scale")
+
+
+def run(target, threads, blocks, L, secs, timeout=150):
+    cmd = [EXE, target, str(threads), str(blocks), str(L), str(secs)]
+    t0 = time.time()
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout)
+    line = out.stdout.strip().splitlines()[-1] if out.stdout.strip() else "{}"
+    rec = json.loads(line)
+    rec["exit"] = out.returncode
+    rec["run_s"] = round(time.time() - t0, 1)
+    if out.returncode != 0:
+        rec["stderr"] = out.stderr[-2000:]
+    print(json.dumps(rec), flush=True)
+    return rec
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--matrix", choices=["threads", "chunk"], required=True)
+    ap.add_argument("--secs", type=float, default=3.0)
+    ap.add_argument("--out", default=None)
+    a = ap.parse_args()
+    runs = []
+    if a.matrix == "threads":
+        for target in ("batcher", "pool"):
+            for T in (8, 64, 256):
+                runs.append(run(target, T, 64, 16384, a.secs))
+    else:
+        for L in (16384, 131072, 1 << 20):
+            for B in (8, 64):
+                for T in (1, 8, 64):
+                    for target in ("batcher", "host"):
+                        runs.append(run(target, T, B, L, a.secs))
+    res = {"matrix": a.matrix, "secs": a.secs, "runs": runs,
+           "all_digests_equal_oracle": all(r.get("mismatches", 1) == 0 and r.get("exit") == 0 for r in runs)}
+    if a.out:
+        os.makedirs(os.path.dirname(os.path.abspath(a.out)), exist_ok=True)
+        with open(a.out, "w") as f:
+            json.dump(res, f, indent=1)
+    return 0 if res["all_digests_equal_oracle"] else 1
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -132,6 +132,7 @@ def lib():
         "md5hip_pool_get_stats": (i, [vp, ctypes.POINTER(MD5HipPoolStats)]),
         "md5hip_pool_device_stats": (i, [vp, u32, ctypes.POINTER(MD5HipBatcherStats)]),
         "md5_batch_submit_device_on": (i, [vp, vp, vp, u64, vp, i, vp, vp]),
+        "md5_batch_submit_device_after": (i, [vp, vp, vp, u64, vp, i, vp, i, vp]),
         "nc_canned_digest_size": (u64, [u32, u32]),
         "nc_digest_update": (i, [vp, u64, u32, u64, u64, vp]),
         "nc_digest_verify": (i, [vp, u64, u32, u64, vp]),
@@ -175,7 +176,8 @@ EXPORTS = ["MD5Init", "MD5Update", "MD5Final", "nc_MD5Init", "nc_MD5Update", "nc
            "md5_batch_submit_device", "md5_batch_flush", "md5hip_init_ctx", "md5hip_update_ctx",
            "md5hip_final_ctx", "md5hip_pool_set_split", "md5hip_pool_submit_async",
            "md5hip_pool_submit_iov_async", "md5hip_pool_wait", "md5hip_pool_poll",
-           "md5hip_pool_get_stats", "md5hip_pool_device_stats", "md5_batch_submit_device_on"]
+           "md5hip_pool_get_stats", "md5hip_pool_device_stats", "md5_batch_submit_device_on",
+           "md5_batch_submit_device_after"]
 
 
 def check(fn, rc):

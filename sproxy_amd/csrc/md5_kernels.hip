@@ -165,9 +165,11 @@ extern "C" {
 int md5hip_abi_version(void) { return MD5HIP_ABI_VERSION; }
 
 // md5_internal.h: the CRC variant for a descriptor batch whose mean chunk
-// length the caller knows (the batcher does).
+// length the caller knows (the batcher does).  Not split = XDMA16 named
+// explicitly: AUTO would decide again with the length unknown
+// (kCrcSplitPerCu per CU) and split short-chunk batches past the crossover.
 __attribute__((visibility("hidden"))) int md5hip_crc_desc_choice(uint64_t n, uint64_t mean_len) {
-  return crc_split_fits(n, mean_len ? mean_len : 1) ? CRC32HIP_SPLIT : CRC32HIP_AUTO;
+  return crc_split_fits(n, mean_len ? mean_len : 1) ? CRC32HIP_SPLIT : CRC32HIP_XDMA16;
 }
 // (with fastcrc the batcher passes 2n windows of fastcrc bytes; windows under
 // kCrcSplitMinWindow keep the window kernels whatever the variant says)

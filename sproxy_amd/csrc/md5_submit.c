@@ -218,7 +218,16 @@ struct slot {
     uint64_t opened_us, launched_us;  /* first chunk reserved / went in flight */
     uint64_t gen;                     /* launches of this slot so far (a waiter's check) */
     uint64_t load;                    /* this slot's share of b->load_bytes */
+    /* callers blocked on tickets held here sleep on `cv` (nwait of them):
+     * broadcast when the slot retires, signalled once when it goes in flight
+     * (one sleeper then watches the launch).  watch: WATCH_NONE / _ACTIVE (one
+     * waiter sleeps through or spins on this launch) / _GAVE_UP (the spin
+     * ended first: the progress thread retires it, polling fast) */
+    pthread_cond_t cv;
+    uint32_t nwait;
+    int watch;
 };
+enum { WATCH_NONE = 0, WATCH_ACTIVE, WATCH_GAVE_UP };
 
 struct md5hip_batcher {
     int device;
@@ -245,8 +254,8 @@ struct md5hip_batcher {
     pthread_cond_t work_cv;   /* a slot went in flight / stop */
     pthread_t progress;
     int progress_started, stop;
-    int waiters;              /* threads blocked on a ticket: poll the launches fast */
-    hipEvent_t after_ev;      /* recorded on a producer's stream (md5_batch_submit_device_on) */
+    int poll_fast;            /* the progress thread polls launches every 10 us now */
+    hipEvent_t after_ev;     /* recorded on a producer's stream (md5_batch_submit_device_on) */
 };
 
 #define CK(x) do { if ((x) != hipSuccess) { rc = -ENODEV; goto fail; } } while (0)
@@ -450,6 +459,7 @@ static int slot_enqueue(md5hip_batcher *b, struct slot *sl)
 static void slot_reset(struct slot *sl)
 {
     sl->state = SLOT_FREE;
+    sl->watch = WATCH_NONE;
     sl->mode = MODE_NONE;
     sl->writers = sl->full = sl->flush = sl->err = sl->direct = 0;
     sl->n = sl->used = sl->nseg = sl->ndma = sl->ndsc = 0;
@@ -481,13 +491,18 @@ static void slot_retire(md5hip_batcher *b, struct slot *sl, int err)
         b->launch_ema_us = b->launch_ema_us > 0 ? 0.75 * b->launch_ema_us + 0.25 * d : d;
     }
     slot_reset(sl);
-    pthread_cond_broadcast(&b->done_cv);
+    if (sl->nwait) pthread_cond_broadcast(&sl->cv);   /* its waiters only */
+    pthread_cond_broadcast(&b->done_cv);              /* slot_take / drain / destroy */
 }
 
 /* Launch slot `sl` if it may go now (mu held). */
 static void slot_try_launch(md5hip_batcher *b, struct slot *sl)
 {
     if (sl->state != SLOT_OPEN || sl->writers) return;
+    /* callers blocked on its tickets: no linger once the device is idle (as
+     * md5_batch_wait's hasten, re-applied whenever the slot is looked at,
+     * since they sleep until it goes) */
+    if (sl->nwait && b->inflight == 0) sl->flush = 1;
     if (sl->n == 0) {                 /* nothing reserved (all chunks failed) */
         if (b->open == (int)(sl - b->s)) b->open = -1;
         slot_retire(b, sl, sl->err);
@@ -514,6 +529,7 @@ static void slot_try_launch(md5hip_batcher *b, struct slot *sl)
     if (sl->n > b->st.max_chunks_per_launch) b->st.max_chunks_per_launch = sl->n;
     if (sl->tickets_in > 1) b->st.coalesced_launches++;
     if (sl->tickets_in > b->st.max_tickets_per_launch) b->st.max_tickets_per_launch = sl->tickets_in;
+    if (sl->nwait) pthread_cond_signal(&sl->cv);      /* one sleeper becomes its watcher */
     pthread_cond_broadcast(&b->work_cv);
 }
 
@@ -544,23 +560,39 @@ static struct slot *slot_take(md5hip_batcher *b, int mode, int kind, uint32_t fa
 }
 
 /* The OPEN slot that accepts chunks of `mode` and digest `kind` (mu held). */
+/* The open slot is re-examined after every wait for a free one: another
+ * submitter may have opened one meanwhile, and taking a second slot then
+ * would leave the first OPEN but no longer b->open -- launched by nobody
+ * (its asynchronous tickets stranded until a wait on them). */
 static struct slot *slot_open(md5hip_batcher *b, int mode, int kind, uint32_t fastcrc)
 {
-    if (b->open >= 0) {
-        struct slot *o = &b->s[b->open];
-        const int compatible = (o->mode == mode || mode == MODE_NONE || o->mode == MODE_NONE) &&
-                               o->kind == (uint32_t)kind && o->fastcrc == fastcrc;
-        if (!o->full && compatible && o->nsegs < b->segcap) {
-            if (o->mode == MODE_NONE) o->mode = mode;
-            return o;
+    for (;;) {
+        if (b->open >= 0) {
+            struct slot *o = &b->s[b->open];
+            const int compatible = (o->mode == mode || mode == MODE_NONE || o->mode == MODE_NONE) &&
+                                   o->kind == (uint32_t)kind && o->fastcrc == fastcrc;
+            if (!o->full && compatible && o->nsegs < b->segcap) {
+                if (o->mode == MODE_NONE) o->mode = mode;
+                return o;
+            }
+            o->full = 1;                 /* closes: launched once its writers are done */
+            b->open = -1;
+            slot_try_launch(b, o);
         }
-        o->full = 1;                 /* closes: launched once its writers are done */
-        b->open = -1;
-        slot_try_launch(b, o);
+        for (uint32_t k = 0; k < b->nslots; k++) {
+            struct slot *sl = &b->s[k];
+            if (sl->state != SLOT_FREE) continue;
+            slot_reset(sl);
+            sl->state = SLOT_OPEN;
+            sl->mode = mode;
+            sl->kind = (uint32_t)kind;
+            sl->fastcrc = fastcrc;
+            sl->dsz = kind == MD5HIP_DIGEST_CRC32 ? 4 : 16;
+            b->open = (int)k;
+            return sl;
+        }
+        pthread_cond_wait(&b->done_cv, &b->mu);       /* all busy: wait for a retire */
     }
-    struct slot *sl = slot_take(b, mode, kind, fastcrc);
-    b->open = (int)(sl - b->s);
-    return sl;
 }
 
 /* ------------------------------------------------------------------------
@@ -578,6 +610,7 @@ static void *progress_main(void *arg)
     unsigned idle_us = 20;
     while (!b->stop) {
         int any = 0;
+        b->poll_fast = 0;
         for (uint32_t k = 0; k < b->nslots; k++) {
             struct slot *sl = &b->s[k];
             if (sl->state != SLOT_INFLIGHT) continue;
@@ -615,10 +648,16 @@ static void *progress_main(void *arg)
                     o->seen_n = o->n;
                 }
             }
-            /* poll interval: 20 -> 200 us while nobody waits; a blocked
-             * waiter pins it at 10 us, so a short launch is not delivered up
-             * to 200 us late */
-            const unsigned us = b->waiters ? 10u : idle_us;
+            /* poll interval: 20 -> 200 us while nobody waits; blocked callers
+             * pin it at 10 us (a short launch is not delivered up to 200 us
+             * late) unless each of their launches has a watcher of its own:
+             * callers on an open slot (it goes when a launch retires), or on
+             * a launch with no watcher yet or whose watcher's spin ran out */
+            int fast = 0;
+            for (uint32_t k = 0; k < b->nslots; k++)
+                fast |= b->s[k].nwait && !(b->s[k].state == SLOT_INFLIGHT && b->s[k].watch == WATCH_ACTIVE);
+            b->poll_fast = fast;
+            const unsigned us = fast ? 10u : idle_us;
             struct timespec ts;
             clock_gettime(CLOCK_REALTIME, &ts);
             ts.tv_nsec += (long)us * 1000;
@@ -632,14 +671,21 @@ static void *progress_main(void *arg)
 }
 
 /* ------------------------------------------------------------------------
- * A blocked caller watches its own launch.  Waiting on done_cv alone, a
- * synchronous call returns up to one progress-thread poll (10 us) plus a
- * condition-variable wake-up after its kernel ends; for a netcache vector
- * (a ~140 us kernel) that was 20-30 us of each call.  So a thread blocked on
- * ticket t whose launch is in flight and expected to end soon (recent
- * launches' wall time) polls that launch's event itself and retires the slot
- * when it completes; a launch expected to run much longer is slept through
- * first.  The spin is bounded; past it the thread blocks on done_cv as before.
+ * Blocked callers.  A caller blocked on ticket t sleeps on the condition
+ * variable of a slot holding t, so a retire wakes only that slot's callers
+ * (the netcache ASIO pool runs 4-512 threads into this site at once,
+ * asio_mgr.c:86-91, :205, :1050-1057, and a coalesced launch holds many of
+ * their vectors).  Waiting for the progress thread alone, a synchronous call
+ * returns up to one poll (10 us) plus a wake-up after its kernel ends -- for
+ * a netcache vector (a ~140 us kernel) 20-30 us of each call -- so ONE caller
+ * per launch watches it: a launch expected to end soon (recent launches' wall
+ * time) has its event polled by that caller, who retires the slot the moment
+ * it completes; a longer one is slept through first.  Every other caller on
+ * the launch sleeps until the retire.  The spin is bounded; past it the
+ * watcher sleeps too and the progress thread (polling fast meanwhile)
+ * retires the launch.  Every sleep re-checks its condition under b->mu, and
+ * every state change that ends one (retire, launch) is made under b->mu and
+ * broadcast or signalled, so no wake-up is lost.
  * ------------------------------------------------------------------------ */
 enum { WATCH_SPIN_US = 300, WATCH_LEAD_US = 200 };
 
@@ -650,19 +696,18 @@ static void cpu_relax(void)
 #endif
 }
 
-/* mu held on entry and exit; 1 = progress may have been made (re-check the
- * ticket), 0 = nothing to watch (block on done_cv). */
-static int watch_own_launch(md5hip_batcher *b, uint64_t t)
+/* Watch in-flight slot `sl` (mu held on entry and exit, watch == NONE). */
+static void watch_launch(md5hip_batcher *b, struct slot *sl)
 {
-    struct slot *sl = NULL;
-    for (uint32_t k = 0; k < b->nslots && !sl; k++)
-        if (b->s[k].state == SLOT_INFLIGHT && seg_has(&b->s[k], t)) sl = &b->s[k];
-    if (!sl) return 0;
-    const uint64_t gen = sl->gen, now = now_us();
-    const uint64_t end = sl->launched_us + (uint64_t)b->launch_ema_us;
-    if (end > now + WATCH_SPIN_US) {            /* long launch: sleep most of it */
-        wait_cv_us(b, &b->done_cv, end - now - WATCH_LEAD_US);
-        return 1;
+    const uint64_t gen = sl->gen;
+    sl->watch = WATCH_ACTIVE;
+    for (;;) {                                  /* long launch: sleep most of it */
+        const uint64_t now = now_us(), end = sl->launched_us + (uint64_t)b->launch_ema_us;
+        if (end <= now + WATCH_SPIN_US) break;
+        sl->nwait++;
+        wait_cv_us(b, &sl->cv, end - now - WATCH_LEAD_US);
+        sl->nwait--;
+        if (sl->state != SLOT_INFLIGHT || sl->gen != gen) return;     /* retired meanwhile */
     }
     const hipEvent_t ev = sl->done;
     pthread_mutex_unlock(&b->mu);
@@ -671,15 +716,54 @@ static int watch_own_launch(md5hip_batcher *b, uint64_t t)
     while ((e = hipEventQuery(ev)) == hipErrorNotReady && now_us() - t0 < WATCH_SPIN_US + WATCH_LEAD_US)
         cpu_relax();
     pthread_mutex_lock(&b->mu);
-    if (e == hipErrorNotReady) return 0;
-    /* the same launch still in flight (the progress thread may have retired
-     * it, and the slot may even be in flight again with other work) */
-    if (sl->state == SLOT_INFLIGHT && sl->gen == gen) {
-        slot_retire(b, sl, e == hipSuccess ? 0 : -EIO);
-        if (b->open >= 0) slot_try_launch(b, &b->s[b->open]);
-        pthread_cond_broadcast(&b->work_cv);
+    /* the same launch still in flight? (the progress thread may have retired
+     * it, and the slot may even be in flight again with other work: then
+     * `watch` belongs to that launch and is left alone) */
+    if (sl->state != SLOT_INFLIGHT || sl->gen != gen) return;
+    if (e == hipErrorNotReady) {
+        sl->watch = WATCH_GAVE_UP;              /* nobody spins on it again */
+        return;
     }
-    return 1;
+    slot_retire(b, sl, e == hipSuccess ? 0 : -EIO);
+    if (b->open >= 0) slot_try_launch(b, &b->s[b->open]);
+    pthread_cond_broadcast(&b->work_cv);
+}
+
+/* Block until ticket t is complete (mu held on entry and exit); its error.
+ * flush: launch an open slot holding t at once (a synchronous submission);
+ * else hasten it (md5_batch_wait: at once only while nothing is in flight). */
+static int wait_ticket(md5hip_batcher *b, uint64_t t, int flush)
+{
+    int err = 0;
+    while (!tk_done(b, t, &err)) {
+        struct slot *in = NULL, *open = NULL;
+        for (uint32_t k = 0; k < b->nslots; k++) {
+            struct slot *sl = &b->s[k];
+            if (sl->state == SLOT_FREE || !seg_has(sl, t)) continue;
+            if (sl->state == SLOT_OPEN) {
+                if (flush || b->inflight == 0) sl->flush = 1;
+                slot_try_launch(b, sl);
+            }
+            if (sl->state == SLOT_INFLIGHT && !in) in = sl;
+            else if (sl->state == SLOT_OPEN && !open) open = sl;
+        }
+        if (tk_done(b, t, &err)) break;
+        if (in && in->watch == WATCH_NONE) {
+            watch_launch(b, in);
+            continue;
+        }
+        struct slot *sl = in ? in : open;
+        if (!sl) {                  /* not held by any slot yet (cannot happen for a
+                                       returned ticket): re-check shortly */
+            wait_cv_us(b, &b->done_cv, 1000);
+            continue;
+        }
+        sl->nwait++;
+        if (!b->poll_fast) pthread_cond_broadcast(&b->work_cv);   /* it may need to now */
+        pthread_cond_wait(&sl->cv, &b->mu);
+        sl->nwait--;
+    }
+    return err;
 }
 
 /* ------------------------------------------------------------------------
@@ -702,6 +786,7 @@ static void batcher_free(md5hip_batcher *b)
         free(sl->segs);
         free(sl->hh);
         hipHostFree(sl->h_bkt); hipFree(sl->d_bkt);
+        pthread_cond_destroy(&sl->cv);
     }
     free(b->s);
     if (b->after_ev) hipEventDestroy(b->after_ev);
@@ -766,6 +851,7 @@ static int batcher_new(int device, uint64_t slice_bytes, uint32_t nslots, uint64
     b->s = calloc(nslots, sizeof *b->s);
     /* ticket 0 = "nothing": complete at once */
     if (!b->s || tk_ring_init(&b->tk, 1)) { rc = -ENOMEM; goto fail; }
+    for (uint32_t k = 0; k < nslots; k++) pthread_cond_init(&b->s[k].cv, NULL);
     CK(hipEventCreateWithFlags(&b->after_ev, hipEventDisableTiming));
     for (uint32_t k = 0; k < nslots; k++) {
         struct slot *sl = &b->s[k];
@@ -858,12 +944,15 @@ int md5hip_batcher_set_digest(md5hip_batcher *b, int kind, uint32_t fastcrc)
     } else {
         return -EINVAL;
     }
+    struct dev_guard g;
+    if (dev_enter(&g, b->device)) return -ENODEV;  /* drain may launch the open slot */
     pthread_mutex_lock(&b->mu);
     drain(b);                                    /* never change kind under queued work */
     b->kind = kind;
     b->fastcrc = fastcrc;
     b->dsz = dsz;
     pthread_mutex_unlock(&b->mu);
+    dev_leave(&g);
     return 0;
 }
 
@@ -889,10 +978,13 @@ int md5hip_batcher_set_gather(md5hip_batcher *b, int mode)
 int md5hip_batcher_set_inflight(md5hip_batcher *b, uint32_t target)
 {
     if (!b || target == 0 || target > b->nslots) return -EINVAL;
+    struct dev_guard g;
+    if (dev_enter(&g, b->device)) return -ENODEV;
     pthread_mutex_lock(&b->mu);
     b->target = target;
     if (b->open >= 0) slot_try_launch(b, &b->s[b->open]);
     pthread_mutex_unlock(&b->mu);
+    dev_leave(&g);
     return 0;
 }
 
@@ -1140,13 +1232,13 @@ static long reserve(md5hip_batcher *b, struct slot *sl, const struct chunk_src *
  *               synchronous entries)
  *   kind    < 0: the batcher's current digest kind; else this submission's
  *           own (it never changes the batcher's setting)
- *   after   != NULL: the producer's stream -- every slot taking chunks of
- *           this submission waits on the producer's work enqueued so far
- *           before its kernel (an event recorded on `after`, waited on by
- *           the slot's stream) */
+ *   after   != NULL: *after is the producer's stream (NULL there = the null
+ *           stream) -- every slot taking chunks of this submission waits on
+ *           the producer's work enqueued so far before its kernel (an event
+ *           recorded on *after, waited on by the slot's stream) */
 static int submit(md5hip_batcher *b, const struct chunk_src *src, uint64_t n, unsigned char *digests,
                   int on_device, int async, uint64_t *ticket, int kind, uint32_t fastcrc,
-                  hipStream_t after)
+                  const hipStream_t *after)
 {
     const int urgent = async != 1;
     for (uint64_t i = 0; i < n; i++) {
@@ -1175,7 +1267,7 @@ static int submit(md5hip_batcher *b, const struct chunk_src *src, uint64_t n, un
         fastcrc = b->fastcrc;
     }
     rc = tk_new(b, &t);
-    if (rc == 0 && after && hipEventRecord(b->after_ev, after) != hipSuccess) {
+    if (rc == 0 && after && hipEventRecord(b->after_ev, *after) != hipSuccess) {
         tk_put(b, t, 0);
         rc = -EINVAL;                              /* not a stream of this device */
     }
@@ -1205,7 +1297,7 @@ static int submit(md5hip_batcher *b, const struct chunk_src *src, uint64_t n, un
          * let another producer record the event meanwhile), before this
          * slot's kernel can be enqueued: the kernel runs after the producer's
          * work enqueued up to here */
-        if (after && (hipEventRecord(b->after_ev, after) != hipSuccess ||
+        if (after && (hipEventRecord(b->after_ev, *after) != hipSuccess ||
                       hipStreamWaitEvent(sl->stream, b->after_ev, 0) != hipSuccess) && !sl->err)
             sl->err = -EIO;
         if ((rc = seg_push(sl, (struct seg){t, at, m, digests + (size_t)dsz * i, on_device}))) {
@@ -1228,19 +1320,7 @@ static int submit(md5hip_batcher *b, const struct chunk_src *src, uint64_t n, un
     tk_put(b, t, rc);                        /* the submission's own reference */
     if (ticket) *ticket = t;
     if (!async || rc) {
-        int err = 0;
-        b->waiters++;
-        pthread_cond_broadcast(&b->work_cv);        /* the progress thread polls fast now */
-        while (!tk_done(b, t, &err)) {
-            for (uint32_t k = 0; k < b->nslots; k++)
-                if (b->s[k].state == SLOT_OPEN && seg_has(&b->s[k], t)) {
-                    b->s[k].flush = 1;       /* a synchronous caller: at once */
-                    slot_try_launch(b, &b->s[k]);
-                }
-            if (!tk_done(b, t, &err) && !watch_own_launch(b, t))
-                pthread_cond_wait(&b->done_cv, &b->mu);
-        }
-        b->waiters--;
+        const int err = wait_ticket(b, t, 1);        /* a synchronous caller: at once */
         if (!rc) rc = err;
     }
     pthread_mutex_unlock(&b->mu);
@@ -1263,26 +1343,20 @@ static void hasten(md5hip_batcher *b, uint64_t ticket)
         }
 }
 
+/* Wait, poll and flush may launch the open slot from the caller's thread
+ * (slot_enqueue's device-keyed state: the BALANCED counter, CU counts), so
+ * they run on the batcher's device like submit -- a pool waits on a ticket
+ * of one device from a thread whose current device is another. */
 int md5_batch_wait(md5hip_batcher *b, uint64_t ticket)
 {
     if (!b) return -EINVAL;
     if (ticket == 0) return 0;               /* "nothing submitted" */
+    struct dev_guard g;
+    if (dev_enter(&g, b->device)) return -ENODEV;
     pthread_mutex_lock(&b->mu);
-    int rc = 0, err = 0;
-    if (ticket >= b->tk.hi) {
-        rc = -EINVAL;
-    } else {
-        b->waiters++;
-        pthread_cond_broadcast(&b->work_cv);        /* the progress thread polls fast now */
-        while (!tk_done(b, ticket, &err)) {
-            hasten(b, ticket);
-            if (!tk_done(b, ticket, &err) && !watch_own_launch(b, ticket))
-                pthread_cond_wait(&b->done_cv, &b->mu);
-        }
-        b->waiters--;
-        rc = err;
-    }
+    const int rc = ticket >= b->tk.hi ? -EINVAL : wait_ticket(b, ticket, 0);
     pthread_mutex_unlock(&b->mu);
+    dev_leave(&g);
     return rc;
 }
 
@@ -1290,6 +1364,8 @@ int md5_batch_poll(md5hip_batcher *b, uint64_t ticket)
 {
     if (!b) return -EINVAL;
     if (ticket == 0) return 1;
+    struct dev_guard g;
+    if (dev_enter(&g, b->device)) return -ENODEV;
     pthread_mutex_lock(&b->mu);
     int rc, err = 0;
     if (ticket >= b->tk.hi) {
@@ -1301,12 +1377,15 @@ int md5_batch_poll(md5hip_batcher *b, uint64_t ticket)
         rc = 0;
     }
     pthread_mutex_unlock(&b->mu);
+    dev_leave(&g);
     return rc;
 }
 
 int md5_batch_flush(md5hip_batcher *b)
 {
     if (!b) return -EINVAL;
+    struct dev_guard g;
+    if (dev_enter(&g, b->device)) return -ENODEV;
     pthread_mutex_lock(&b->mu);
     if (b->open >= 0) {
         struct slot *o = &b->s[b->open];
@@ -1314,6 +1393,7 @@ int md5_batch_flush(md5hip_batcher *b)
         slot_try_launch(b, o);
     }
     pthread_mutex_unlock(&b->mu);
+    dev_leave(&g);
     return 0;
 }
 
@@ -1461,12 +1541,7 @@ static int host_fixed(md5hip_batcher *b, int kind, uint32_t fastcrc, const void 
     tk_put(b, t, rc);
     if (ticket) *ticket = t;
     if (!ticket || rc) {
-        int err = 0;
-        b->waiters++;
-        pthread_cond_broadcast(&b->work_cv);
-        while (!tk_done(b, t, &err))
-            if (!watch_own_launch(b, t)) pthread_cond_wait(&b->done_cv, &b->mu);
-        b->waiters--;
+        const int err = wait_ticket(b, t, 1);
         if (!rc) rc = err;
     }
     pthread_mutex_unlock(&b->mu);
@@ -1474,9 +1549,9 @@ static int host_fixed(md5hip_batcher *b, int kind, uint32_t fastcrc, const void 
     return rc;
 }
 
-int md5_batch_submit_device_on(md5hip_batcher *b, const uint64_t *d_ptrs, const uint32_t *lens,
-                               uint64_t n, unsigned char *digests, int digests_on_device,
-                               void *producer_stream, uint64_t *ticket)
+int md5_batch_submit_device_after(md5hip_batcher *b, const uint64_t *d_ptrs, const uint32_t *lens,
+                                  uint64_t n, unsigned char *digests, int digests_on_device,
+                                  void *producer_stream, int order, uint64_t *ticket)
 {
     if (ticket) *ticket = 0;
     if (!b) return -EINVAL;
@@ -1485,8 +1560,17 @@ int md5_batch_submit_device_on(md5hip_batcher *b, const uint64_t *d_ptrs, const 
     for (uint64_t i = 0; i < n; i++)
         if (!d_ptrs[i] && lens[i]) return -EINVAL;
     const struct chunk_src src = {NULL, lens, NULL, NULL, d_ptrs};
+    const hipStream_t after = (hipStream_t)producer_stream;
     return submit(b, &src, n, digests, digests_on_device != 0, ticket != NULL, ticket, -1, 0,
-                  (hipStream_t)producer_stream);
+                  order ? &after : NULL);
+}
+
+int md5_batch_submit_device_on(md5hip_batcher *b, const uint64_t *d_ptrs, const uint32_t *lens,
+                               uint64_t n, unsigned char *digests, int digests_on_device,
+                               void *producer_stream, uint64_t *ticket)
+{
+    return md5_batch_submit_device_after(b, d_ptrs, lens, n, digests, digests_on_device,
+                                         producer_stream, producer_stream != NULL, ticket);
 }
 
 int md5hip_batch_host_fixed(md5hip_batcher *b, const void *h_base, uint64_t n, uint32_t len,

@@ -340,6 +340,7 @@ class Batcher:
                wait="md5_batch_wait", poll="md5_batch_poll", flush="md5_batch_flush",
                submit_device_async="md5_batch_submit_device_async",
                submit_device="md5_batch_submit_device", submit_device_on="md5_batch_submit_device_on",
+               submit_device_after="md5_batch_submit_device_after",
                set_inflight="md5hip_batcher_set_inflight",
                set_linger="md5hip_batcher_set_linger", stats="md5hip_batcher_get_stats")
 
@@ -498,20 +499,23 @@ class Batcher:
         return P, L, out, 0
 
     def _producer(self, after):
-        """The producer stream handle for md5_batch_submit_device_on:
-        'current' = torch's current stream on the batcher's device."""
+        """(stream handle, order) for md5_batch_submit_device_after:
+        'current' = torch's current stream on the batcher's device -- its
+        handle is 0 (NULL) when that is the default stream, which the library
+        then orders on as the null stream, never as "no ordering"; None = no
+        ordering."""
         if isinstance(after, str):
             if after != "current":
                 raise ValueError("after: 'current', None or a stream")
             if torch is None:
-                return None
-            return torch.cuda.current_stream(self.device).cuda_stream
+                raise RuntimeError("after='current' needs torch; pass a stream handle or None")
+            return torch.cuda.current_stream(self.device).cuda_stream, 1
         if after is None:
-            return None
-        return getattr(after, "cuda_stream", after)
+            return None, 0
+        return getattr(after, "cuda_stream", after), 1
 
     def submit_device_async(self, ptrs, lens, out=None, after="current") -> "Batcher.Pending":
-        """md5_batch_submit_device_on: chunk i = (device address ptrs[i],
+        """md5_batch_submit_device_after: chunk i = (device address ptrs[i],
         lens[i]); digests into `out` -- a device tensor (digests stay on the
         device) or, by default, a host array returned by .wait().  The kernel
         runs after the work already enqueued on `after` (default: torch's
@@ -520,15 +524,15 @@ class Batcher:
         P, L, o, on_dev = self._dev_args(ptrs, lens, out)
         t = ctypes.c_uint64()
         dst = o.data_ptr() if on_dev else o.ctypes.data
-        check(*self._call("submit_device_on", P.ctypes.data, L.ctypes.data, P.size, dst, on_dev,
-                          self._producer(after), ctypes.byref(t)))
+        check(*self._call("submit_device_after", P.ctypes.data, L.ctypes.data, P.size, dst, on_dev,
+                          *self._producer(after), ctypes.byref(t)))
         return Batcher.Pending(self, t.value, o, P.size, (P, L, o), on_dev)
 
     def submit_device(self, ptrs, lens, out=None, after="current"):
         P, L, o, on_dev = self._dev_args(ptrs, lens, out)
         dst = o.data_ptr() if on_dev else o.ctypes.data
-        check(*self._call("submit_device_on", P.ctypes.data, L.ctypes.data, P.size, dst, on_dev,
-                          self._producer(after), None))
+        check(*self._call("submit_device_after", P.ctypes.data, L.ctypes.data, P.size, dst, on_dev,
+                          *self._producer(after), None))
         return o if on_dev else self._ret(o, P.size)
 
     def flush(self):

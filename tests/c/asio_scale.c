@@ -1,0 +1,269 @@
+/*
+ * tests/c/asio_scale.c -- the netcache checksum call site at the reference's
+ * own thread scale, as a plain-C program over the C ABI (test and
+ * measurement infrastructure; not part of the product).
+ *
+ * netcache's ASIO pool runs 4-512 threads (asio_mgr.c:86, :91, started at
+ * :205), and every one of them calls the block checksum on its completed
+ * vector at once (asio_mgr.c:1050-1057); httpd runs 32 MHD workers by
+ * default (httpd.c:8630) and chunk_size defaults to 128 KiB (httpd.c:8627).
+ * Here T threads each submit a vector of B blocks of L bytes synchronously,
+ * over and over, for S seconds:
+ *   batcher  md5_batch_submit on ONE shared batcher (md5hip_batcher_create)
+ *   pool     md5hip_pool_submit on a pool over device 0 listed twice
+ *   host     MD5Init/MD5Update/MD5Final of the product library (md5_stream.c)
+ *            per block on the calling thread -- the alternative the call
+ *            site has, timed the same way
+ * Each thread owns its own vector (distinct bytes); every call's digests are
+ * compared with the oracle's (oracle/md5_oracle.c, linked in as the checker
+ * and computed once per thread before timing).  Per call it records the wall
+ * latency and the calling thread's CPU time (CLOCK_THREAD_CPUTIME_ID, the
+ * clock of getrusage(RUSAGE_THREAD), around the call); the process CPU time
+ * over the timed window (CLOCK_PROCESS_CPUTIME_ID, which includes the
+ * batchers' progress threads and the HIP runtime's) is reported per call too.  Prints one JSON object.
+ *
+ * usage: asio_scale TARGET THREADS BLOCKS BLOCK_BYTES SECS [SLICE_MIB NSLOTS]
+ * Exit 0 = every digest equal to the oracle's; 1 = a mismatch or error;
+ * 77 = no usable HIP device.
+ */
+#define _GNU_SOURCE
+#include <errno.h>
+#include <pthread.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+
+#include "md5.h"
+#include "md5hip.h"
+
+void oracle_md5(const void *data, uint64_t len, unsigned char digest[16]);
+void oracle_xorshift_fill(void *dst, uint64_t nbytes, uint64_t seed);
+
+enum target { T_BATCHER, T_POOL, T_HOST };
+
+static enum target g_target;
+static int g_threads, g_blocks;
+static uint32_t g_len;
+static double g_secs;
+static md5hip_batcher *g_b;
+static md5hip_pool *g_p;
+static pthread_barrier_t g_start, g_warm, g_go;
+static double g_t_end;          /* set between g_warm and g_go */
+
+static double now(void)
+{
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return ts.tv_sec + ts.tv_nsec * 1e-9;
+}
+
+/* user + system CPU of the calling thread / the process: the clocks behind
+ * getrusage(RUSAGE_THREAD / RUSAGE_SELF), read at scheduler resolution
+ * (getrusage rounds to the tick on kernels without precise accounting) */
+static double cpu_clock(clockid_t id)
+{
+    struct timespec ts;
+    clock_gettime(id, &ts);
+    return ts.tv_sec + ts.tv_nsec * 1e-9;
+}
+static double thread_cpu(void) { return cpu_clock(CLOCK_THREAD_CPUTIME_ID); }
+static double process_cpu(void) { return cpu_clock(CLOCK_PROCESS_CPUTIME_ID); }
+
+struct job {
+    int t;
+    unsigned char *buf;
+    const void **ptrs;
+    uint32_t *lens;
+    unsigned char (*want)[16], (*got)[16];
+    double *lat, *cpu;           /* per timed call */
+    size_t ncalls, cap;
+    int rc, bad;
+};
+
+static int one_call(struct job *j)
+{
+    switch (g_target) {
+    case T_BATCHER:
+        return md5_batch_submit(g_b, j->ptrs, j->lens, (uint64_t)g_blocks, &j->got[0][0]);
+    case T_POOL:
+        return md5hip_pool_submit(g_p, j->ptrs, j->lens, (uint64_t)g_blocks, &j->got[0][0]);
+    case T_HOST:
+        for (int i = 0; i < g_blocks; i++) {
+            struct MD5Context c;
+            MD5Init(&c);
+            MD5Update(&c, j->ptrs[i], j->lens[i]);
+            MD5Final(j->got[i], &c);
+        }
+        return 0;
+    }
+    return -EINVAL;
+}
+
+static void *worker(void *arg)
+{
+    struct job *j = arg;
+    const size_t vec = (size_t)g_blocks * g_len;
+    j->buf = malloc(vec + 64);
+    j->ptrs = malloc(sizeof(void *) * g_blocks);
+    j->lens = malloc(sizeof(uint32_t) * g_blocks);
+    j->want = malloc(16 * (size_t)g_blocks);
+    j->got = malloc(16 * (size_t)g_blocks);
+    if (!j->buf || !j->ptrs || !j->lens || !j->want || !j->got) {
+        j->rc = -ENOMEM;
+        pthread_barrier_wait(&g_start);
+        pthread_barrier_wait(&g_warm);
+        pthread_barrier_wait(&g_go);
+        return NULL;
+    }
+    oracle_xorshift_fill(j->buf, vec + 64, 0x5A11ull + (uint64_t)j->t * 7919u);
+    for (int i = 0; i < g_blocks; i++) {
+        /* a short last block, as a vector's tail block often is (blk_io.c:377) */
+        j->lens[i] = i == g_blocks - 1 && g_blocks > 1 ? g_len - 1000u * (uint32_t)(1 + j->t % 7) : g_len;
+        j->ptrs[i] = j->buf + (size_t)i * g_len;
+        oracle_md5(j->ptrs[i], j->lens[i], j->want[i]);
+    }
+    pthread_barrier_wait(&g_start);
+    for (int w = 0; w < 2 && !j->rc; w++) {               /* warm-up calls, checked */
+        j->rc = one_call(j);
+        if (!j->rc && memcmp(j->got, j->want, 16 * (size_t)g_blocks)) j->bad++;
+    }
+    pthread_barrier_wait(&g_warm);
+    pthread_barrier_wait(&g_go);
+    const double t_end = g_t_end;
+    while (!j->rc && now() < t_end) {
+        memset(j->got, 0, 16 * (size_t)g_blocks);
+        const double c0 = thread_cpu(), t0 = now();
+        const int rc = one_call(j);
+        const double t1 = now(), c1 = thread_cpu();
+        if (rc) {
+            j->rc = rc;
+            break;
+        }
+        if (memcmp(j->got, j->want, 16 * (size_t)g_blocks)) j->bad++;
+        if (j->ncalls == j->cap) {
+            j->cap = j->cap ? 2 * j->cap : 1024;
+            j->lat = realloc(j->lat, sizeof(double) * j->cap);
+            j->cpu = realloc(j->cpu, sizeof(double) * j->cap);
+            if (!j->lat || !j->cpu) { j->rc = -ENOMEM; break; }
+        }
+        j->lat[j->ncalls] = (t1 - t0) * 1e6;
+        j->cpu[j->ncalls] = (c1 - c0) * 1e6;
+        j->ncalls++;
+    }
+    free(j->buf);
+    return NULL;
+}
+
+static int cmp_d(const void *a, const void *b)
+{
+    const double x = *(const double *)a, y = *(const double *)b;
+    return x < y ? -1 : x > y;
+}
+
+static double pct(const double *v, size_t n, double p)
+{
+    if (!n) return 0;
+    size_t k = (size_t)(p / 100.0 * (double)(n - 1) + 0.5);
+    return v[k < n ? k : n - 1];
+}
+
+int main(int argc, char **argv)
+{
+    if (argc < 6) {
+        fprintf(stderr, "usage: %s batcher|pool|host THREADS BLOCKS BLOCK_BYTES SECS [SLICE_MIB NSLOTS]\n", argv[0]);
+        return 2;
+    }
+    g_target = !strcmp(argv[1], "pool") ? T_POOL : !strcmp(argv[1], "host") ? T_HOST : T_BATCHER;
+    g_threads = atoi(argv[2]);
+    g_blocks = atoi(argv[3]);
+    g_len = (uint32_t)strtoul(argv[4], NULL, 0);
+    g_secs = atof(argv[5]);
+    const uint64_t slice = argc > 6 ? strtoull(argv[6], NULL, 0) << 20 : 0;
+    const uint32_t nslots = argc > 7 ? (uint32_t)atoi(argv[7]) : 0;
+    if (g_threads < 1 || g_threads > 1024 || g_blocks < 1 || g_len < 8000 || g_secs <= 0) return 2;
+    int rc = 0;
+    if (g_target == T_BATCHER) rc = md5hip_batcher_create(0, slice, nslots, &g_b);
+    if (g_target == T_POOL) {
+        const int devs[2] = {0, 0};
+        rc = md5hip_pool_create(devs, 2, slice, nslots, &g_p);
+    }
+    if (rc == -ENODEV) {
+        printf("{\"error\": \"no usable HIP device\", \"rc\": %d}\n", rc);
+        return 77;
+    }
+    if (rc) {
+        printf("{\"error\": \"create\", \"rc\": %d}\n", rc);
+        return 1;
+    }
+    struct job *jobs = calloc((size_t)g_threads, sizeof *jobs);
+    pthread_t *th = calloc((size_t)g_threads, sizeof *th);
+    pthread_barrier_init(&g_start, NULL, (unsigned)g_threads + 1);
+    pthread_barrier_init(&g_warm, NULL, (unsigned)g_threads + 1);
+    pthread_barrier_init(&g_go, NULL, (unsigned)g_threads + 1);
+    pthread_attr_t at;
+    pthread_attr_init(&at);
+    pthread_attr_setstacksize(&at, 256u << 10);
+    for (int t = 0; t < g_threads; t++) {
+        jobs[t].t = t;
+        if (pthread_create(&th[t], &at, worker, &jobs[t])) {
+            printf("{\"error\": \"pthread_create\", \"thread\": %d}\n", t);
+            return 1;
+        }
+    }
+    pthread_barrier_wait(&g_start);               /* oracle digests done */
+    pthread_barrier_wait(&g_warm);                /* warm-up calls done */
+    const double p0 = process_cpu(), w0 = now();
+    g_t_end = w0 + g_secs;
+    pthread_barrier_wait(&g_go);                  /* (the barrier orders g_t_end) */
+    for (int t = 0; t < g_threads; t++) pthread_join(th[t], NULL);
+    const double wall = now() - w0, pcpu = process_cpu() - p0;
+    size_t total = 0;
+    int bad = 0, err = 0;
+    double bytes = 0;
+    for (int t = 0; t < g_threads; t++) {
+        total += jobs[t].ncalls;
+        if (jobs[t].lens)
+            for (int i = 0; i < g_blocks; i++) bytes += (double)jobs[t].ncalls * jobs[t].lens[i];
+        bad += jobs[t].bad;
+        if (jobs[t].rc && !err) err = jobs[t].rc;
+    }
+    double *lat = malloc(sizeof(double) * (total ? total : 1)), *cpu = malloc(sizeof(double) * (total ? total : 1));
+    size_t k = 0;
+    double cpu_sum = 0;
+    for (int t = 0; t < g_threads; t++)
+        for (size_t c = 0; c < jobs[t].ncalls; c++, k++) {
+            lat[k] = jobs[t].lat[c];
+            cpu[k] = jobs[t].cpu[c];
+            cpu_sum += cpu[k];
+        }
+    qsort(lat, total, sizeof *lat, cmp_d);
+    qsort(cpu, total, sizeof *cpu, cmp_d);
+    struct md5hip_batcher_stats st = {0};
+    if (g_b) md5hip_batcher_get_stats(g_b, &st);
+    if (g_p) {
+        struct md5hip_batcher_stats s2;
+        for (uint32_t g = 0; g < 2; g++)
+            if (md5hip_pool_device_stats(g_p, g, &s2) == 0) {
+                st.launches += s2.launches;
+                st.coalesced_launches += s2.coalesced_launches;
+                if (s2.max_tickets_per_launch > st.max_tickets_per_launch)
+                    st.max_tickets_per_launch = s2.max_tickets_per_launch;
+            }
+    }
+    printf("{\"target\": \"%s\", \"threads\": %d, \"blocks\": %d, \"block_bytes\": %u, \"secs\": %.3f, "
+           "\"calls\": %zu, \"lat_us\": {\"p50\": %.1f, \"p90\": %.1f, \"p99\": %.1f, \"max\": %.1f}, "
+           "\"thread_cpu_us_per_call\": {\"mean\": %.2f, \"p50\": %.2f, \"p99\": %.2f}, "
+           "\"process_cpu_us_per_call\": %.2f, \"process_cpu_cores\": %.2f, \"gib_s\": %.3f, "
+           "\"launches\": %llu, \"coalesced_launches\": %llu, \"max_tickets_per_launch\": %llu, "
+           "\"mismatches\": %d, \"rc\": %d}\n",
+           argv[1], g_threads, g_blocks, g_len, wall, total, pct(lat, total, 50), pct(lat, total, 90),
+           pct(lat, total, 99), total ? lat[total - 1] : 0.0, total ? cpu_sum / (double)total : 0.0,
+           pct(cpu, total, 50), pct(cpu, total, 99), total ? pcpu * 1e6 / (double)total : 0.0, pcpu / wall,
+           bytes / wall / (double)(1u << 30), (unsigned long long)st.launches,
+           (unsigned long long)st.coalesced_launches, (unsigned long long)st.max_tickets_per_launch, bad, err);
+    if (g_b) md5hip_batcher_destroy(g_b);
+    if (g_p) md5hip_pool_destroy(g_p);
+    return bad || err || total == 0 ? 1 : 0;
+}

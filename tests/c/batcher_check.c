@@ -11,8 +11,18 @@
  * checks every digest against the library's host MD5 computed up front; one
  * more thread keeps changing the batchers' knobs (inflight target, linger,
  * gather mode, pool split) and another registers, uses and unregisters a
- * private page range.  Exits 0 when
- * every check holds.
+ * private page range.  The pool spans devices 0, 1 and 2, and every copy
+ * or kernel must be enqueued from a thread whose current device is its
+ * stream's (fake_hip_wrong_device stays 0): waits and polls on another
+ * device's ticket included.
+ *
+ * Before that, the blocked-caller phase: 64 threads wait on tickets that all
+ * sit in ONE open slot behind a held launch; when the launch is released the
+ * slot goes in flight, one of them watches it, and (every other round) that
+ * watcher's spin ends on NotReady just as the kernel finishes and the
+ * progress thread retires the launch (fake_hip_slow_query) -- every waiter
+ * must return with correct digests within the round's deadline (the lost
+ * wake-up of round 3 hung here).  Exits 0 when every check holds.
  */
 #include <errno.h>
 #include <pthread.h>
@@ -21,6 +31,7 @@
 #include <stdlib.h>
 #include <string.h>
 #include <time.h>
+#include <unistd.h>
 
 #include "md5.h"
 #include "md5hip.h"
@@ -37,6 +48,9 @@ static uint32_t g_crc[NCH];
 static md5hip_batcher *g_b, *g_q, *g_crcb;
 static md5hip_pool *g_pool;
 extern uint32_t fake_hip_fail_len;
+extern unsigned long fake_hip_wrong_device;
+extern int fake_hip_hold, fake_hip_slow_query;
+void fake_hip_mark_thread(void);
 static int g_stop;
 #define STOPPED() __atomic_load_n(&g_stop, __ATOMIC_RELAXED)
 #define STOP() __atomic_store_n(&g_stop, 1, __ATOMIC_RELAXED)
@@ -160,8 +174,10 @@ static void *worker(void *arg)
             /* device digests (16-B aligned in place, or odd: scattered) */
             unsigned char *raw = malloc(16 * (size_t)n + 20);
             unsigned char *d = raw + (rnd(&s) & 1 ? 0 : 4);
-            rc = md5_batch_submit_device_on(g_q, dptrs, lens, (uint64_t)n, d, 1, rnd(&s) & 1 ? (void *)g_q : NULL,
-                                            NULL);
+            const uint64_t how = rnd(&s) % 3;      /* no ordering / a producer stream / the null stream */
+            rc = how == 2 ? md5_batch_submit_device_after(g_q, dptrs, lens, (uint64_t)n, d, 1, NULL, 1, NULL)
+                          : md5_batch_submit_device_on(g_q, dptrs, lens, (uint64_t)n, d, 1,
+                                                       how ? (void *)g_q : NULL, NULL);
             if (rc || !check_md5((unsigned char (*)[16])d, idx, n)) fail("submit_device_on", t, rc);
             free(raw);
             break;
@@ -309,6 +325,111 @@ static void *registrar(void *arg)
     return NULL;
 }
 
+/* ---------------------------------------------------------- blocked callers */
+#define WT 64      /* waiters on one slot */
+#define WN 8       /* chunks per waiter */
+static md5hip_batcher *g_w;
+static pthread_barrier_t g_wbar;
+
+struct wjob {
+    int t, round, n, rc, bad;
+    int idx[WN];
+    unsigned char dig[WN][16];
+    uint64_t tk;
+};
+
+static void *waiter(void *arg)
+{
+    struct wjob *j = arg;
+    uint64_t s = 0xA5A5ull * (uint64_t)(j->t + 1) + (uint64_t)j->round * 131u;
+    const void *ptrs[WN];
+    uint32_t lens[WN];
+    j->n = 1 + (int)(rnd(&s) % WN);
+    for (int i = 0; i < j->n; i++) {
+        int k;
+        do k = (int)(rnd(&s) % NCH); while (g_lens[k] > 3000);
+        j->idx[i] = k;
+        ptrs[i] = g_heap + g_offs[k];
+        lens[i] = g_lens[k];
+    }
+    j->rc = md5_batch_submit_async(g_w, ptrs, lens, (uint64_t)j->n, &j->dig[0][0], &j->tk);
+    pthread_barrier_wait(&g_wbar);          /* every ticket is in the open slot */
+    fake_hip_mark_thread();
+    if (!j->rc) j->rc = md5_batch_wait(g_w, j->tk);
+    j->bad = !check_md5(j->dig, j->idx, j->n);
+    return NULL;
+}
+
+static int blocked_callers(int rounds)
+{
+    int rc = md5hip_batcher_create(0, 4u << 20, 2, &g_w);      /* 2 slots: inflight target 1 */
+    if (rc) { printf("FAIL waiter batcher %d\n", rc); return 1; }
+    for (int r = 0; r < rounds; r++) {
+        __atomic_store_n(&fake_hip_hold, 1, __ATOMIC_RELAXED);
+        /* a held launch in flight, so the waiters' chunks coalesce in the open slot */
+        const void *bp = g_heap;
+        uint32_t bl = 100;
+        unsigned char bd[16];
+        uint64_t bt;
+        if ((rc = md5_batch_submit_async(g_w, &bp, &bl, 1, bd, &bt)) || (rc = md5_batch_flush(g_w))) {
+            printf("FAIL blocker %d\n", rc);
+            return 1;
+        }
+        pthread_barrier_init(&g_wbar, NULL, WT + 1);
+        static struct wjob jobs[WT];
+        pthread_t th[WT];
+        for (int t = 0; t < WT; t++) {
+            jobs[t] = (struct wjob){.t = t, .round = r};
+            pthread_create(&th[t], NULL, waiter, &jobs[t]);
+        }
+        pthread_barrier_wait(&g_wbar);
+        struct timespec ts = {0, 20000000};            /* let them all block */
+        nanosleep(&ts, NULL);
+        struct md5hip_batcher_stats st;
+        md5hip_batcher_get_stats(g_w, &st);
+        const uint64_t launches0 = st.launches;
+        __atomic_store_n(&fake_hip_slow_query, r & 1, __ATOMIC_RELAXED);
+        __atomic_store_n(&fake_hip_hold, 0, __ATOMIC_RELAXED);
+        const double t0 = now();
+        for (int t = 0; t < WT; t++) pthread_join(th[t], NULL);
+        const double dt = now() - t0;
+        __atomic_store_n(&fake_hip_slow_query, 0, __ATOMIC_RELAXED);
+        pthread_barrier_destroy(&g_wbar);
+        if ((rc = md5_batch_wait(g_w, bt))) { printf("FAIL blocker wait %d\n", rc); return 1; }
+        md5hip_batcher_get_stats(g_w, &st);
+        for (int t = 0; t < WT; t++)
+            if (jobs[t].rc || jobs[t].bad) {
+                printf("FAIL waiter %d round %d: rc %d bad %d\n", t, r, jobs[t].rc, jobs[t].bad);
+                return 1;
+            }
+        /* the 64 tickets went out together: one launch after the blocker */
+        if (st.launches != launches0 + 1 || st.max_tickets_per_launch < WT) {
+            printf("FAIL round %d: %llu launches for the waiters, max %llu tickets per launch\n", r,
+                   (unsigned long long)(st.launches - launches0), (unsigned long long)st.max_tickets_per_launch);
+            return 1;
+        }
+        if (dt > 5.0) { printf("FAIL round %d took %.1f s\n", r, dt); return 1; }
+    }
+    md5hip_batcher_destroy(g_w);
+    printf("blocked callers: %d rounds x %d waiters on one slot ok\n", rounds, WT);
+    return 0;
+}
+
+/* a hang is a failure, not a stuck test */
+static void *watchdog(void *arg)
+{
+    const double secs = *(const double *)arg;
+    const double t0 = now();
+    while (now() - t0 < secs) {
+        struct timespec ts = {0, 50000000};
+        nanosleep(&ts, NULL);
+    }
+    printf("FAIL hang: still running after %.0f s\n", secs);
+    fflush(stdout);
+    _exit(3);
+    return NULL;
+}
+
 int main(int argc, char **argv)
 {
     const double secs = argc > 1 ? atof(argv[1]) : 4.0;
@@ -340,6 +461,12 @@ int main(int argc, char **argv)
         return 1;
     }
     md5hip_batcher_set_digest(g_crcb, MD5HIP_DIGEST_CRC32, 0);
+    static double wd_secs;
+    wd_secs = secs + 60.0;
+    pthread_t wd;
+    pthread_create(&wd, NULL, watchdog, &wd_secs);
+    pthread_detach(wd);
+    if (blocked_callers(12)) return 1;
     /* error paths, one thread: a chunk over the slice, a never-issued
      * ticket, a launch that fails (sync and async; the failure is kept for
      * a second wait and does not touch later submissions) */
@@ -400,6 +527,10 @@ int main(int argc, char **argv)
     free(g_heap);
     free(g_pageable);
     if (g_fail) return 1;
+    if (fake_hip_wrong_device) {
+        printf("FAIL %lu copies/kernels enqueued from a thread on another device\n", fake_hip_wrong_device);
+        return 1;
+    }
     printf("batcher %llu submissions %llu launches %llu coalesced; queue %llu / %llu / %llu; "
            "pool %llu whole %llu split\n",
            (unsigned long long)bs.submissions, (unsigned long long)bs.launches,

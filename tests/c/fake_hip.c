@@ -12,7 +12,19 @@
  *     flight for a while and the batcher's progress thread, coalescing and
  *     out-of-order completion all run;
  *   - the "kernels" compute the digests on the CPU with the library's own
- *     host MD5 (md5_stream.c) and CRC-32 (nc_digest.c).
+ *     host MD5 (md5_stream.c) and CRC-32 (nc_digest.c);
+ *   - a stream remembers the device current at its creation, and every copy
+ *     or "kernel" enqueued on it from a thread whose current device differs
+ *     is counted in fake_hip_wrong_device (the real runtime keys state such
+ *     as the BALANCED counter and CU counts on hipGetDevice);
+ *   - test controls: fake_hip_hold keeps every event NotReady; for an
+ *     event recorded while fake_hip_slow_query is set, the first query made from a
+ *     thread marked by fake_hip_mark_thread() takes 600 us and answers
+ *     NotReady while the event turns ready for every other caller (until
+ *     then it answers NotReady to unmarked threads) -- a
+ *     waiter's bounded spin then ends on NotReady just after the kernel
+ *     finished, and the progress thread retires the launch before the waiter
+ *     holds the lock again (the lost-wakeup race of a blocked caller).
  * Nothing here is part of the product.
  */
 #include <errno.h>
@@ -20,6 +32,7 @@
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
 #include <hip/hip_runtime_api.h>
 
@@ -31,12 +44,24 @@
 struct ihipEvent_t {
     int left;                     /* queries still answered NotReady */
     unsigned seed;
+    int slow;                     /* recorded while fake_hip_slow_query was set */
+    int slow_done;                /* the slow query of this record happened */
 };
 struct ihipStream_t {
-    int dummy;
+    int device;
 };
 
 static __thread int t_device;
+static __thread int t_marked;
+unsigned long fake_hip_wrong_device;
+int fake_hip_hold, fake_hip_slow_query;
+void fake_hip_mark_thread(void) { t_marked = 1; }
+
+static void on_stream(hipStream_t stream)
+{
+    if (stream && stream->device != t_device)
+        __atomic_fetch_add(&fake_hip_wrong_device, 1, __ATOMIC_RELAXED);
+}
 /* a launch holding a chunk of this length fails with -EIO (error paths) */
 uint32_t fake_hip_fail_len = 0xffffffffu;
 static pthread_mutex_t g_ev_mu = PTHREAD_MUTEX_INITIALIZER;
@@ -57,7 +82,9 @@ hipError_t hipStreamCreateWithFlags(hipStream_t *stream, unsigned int flags)
 {
     (void)flags;
     *stream = calloc(1, sizeof(struct ihipStream_t));
-    return *stream ? hipSuccess : hipErrorOutOfMemory;
+    if (!*stream) return hipErrorOutOfMemory;
+    (*stream)->device = t_device;
+    return hipSuccess;
 }
 hipError_t hipStreamDestroy(hipStream_t stream) { free(stream); return hipSuccess; }
 hipError_t hipStreamWaitEvent(hipStream_t stream, hipEvent_t event, unsigned int flags) { (void)stream; (void)event; (void)flags; return hipSuccess; }
@@ -77,12 +104,30 @@ hipError_t hipEventRecord(hipEvent_t event, hipStream_t stream)
     pthread_mutex_lock(&g_ev_mu);
     event->seed = event->seed * 1103515245u + 12345u;
     event->left = (int)((event->seed >> 16) % 4u);
+    event->slow = __atomic_load_n(&fake_hip_slow_query, __ATOMIC_RELAXED);
+    event->slow_done = 0;
     pthread_mutex_unlock(&g_ev_mu);
     return hipSuccess;
 }
 hipError_t hipEventQuery(hipEvent_t event)
 {
     pthread_mutex_lock(&g_ev_mu);
+    if (__atomic_load_n(&fake_hip_hold, __ATOMIC_RELAXED)) {
+        pthread_mutex_unlock(&g_ev_mu);
+        return hipErrorNotReady;
+    }
+    if (event->slow && !event->slow_done && !t_marked) {
+        pthread_mutex_unlock(&g_ev_mu);             /* running until a marked thread has looked */
+        return hipErrorNotReady;
+    }
+    if (event->slow && !event->slow_done && t_marked) {
+        event->slow_done = 1;
+        event->left = 0;                          /* ready for everyone else from now */
+        pthread_mutex_unlock(&g_ev_mu);
+        const struct timespec ts = {0, 600000};
+        nanosleep(&ts, NULL);
+        return hipErrorNotReady;                  /* ... but this caller saw it running */
+    }
     const int ready = event->left == 0;
     if (!ready) event->left--;
     pthread_mutex_unlock(&g_ev_mu);
@@ -90,6 +135,10 @@ hipError_t hipEventQuery(hipEvent_t event)
 }
 hipError_t hipEventSynchronize(hipEvent_t event)
 {
+    while (__atomic_load_n(&fake_hip_hold, __ATOMIC_RELAXED)) {
+        const struct timespec ts = {0, 100000};
+        nanosleep(&ts, NULL);
+    }
     pthread_mutex_lock(&g_ev_mu);
     event->left = 0;
     pthread_mutex_unlock(&g_ev_mu);
@@ -99,7 +148,7 @@ hipError_t hipEventSynchronize(hipEvent_t event)
 hipError_t hipMemcpyAsync(void *dst, const void *src, size_t sizeBytes, hipMemcpyKind kind, hipStream_t stream)
 {
     (void)kind;
-    (void)stream;
+    on_stream(stream);
     if (sizeBytes) memmove(dst, src, sizeBytes);
     return hipSuccess;
 }
@@ -122,7 +171,7 @@ static uint32_t blk_crc(const unsigned char *p, uint32_t len, uint32_t F)
 int md5hip_digest_fixed(const void *d_base, uint64_t n, uint32_t len, uint64_t stride,
                         unsigned char *d_digests, void *stream)
 {
-    (void)stream;
+    on_stream((hipStream_t)stream);
     for (uint64_t i = 0; i < n; i++) md5_of((const unsigned char *)d_base + i * stride, len, d_digests + 16 * i);
     return 0;
 }
@@ -130,7 +179,7 @@ int md5hip_digest_fixed(const void *d_base, uint64_t n, uint32_t len, uint64_t s
 int crc32hip_fixed(const void *d_base, uint64_t n, uint32_t len, uint64_t stride, uint32_t fastcrc,
                    uint32_t *d_crcs, void *stream)
 {
-    (void)stream;
+    on_stream((hipStream_t)stream);
     for (uint64_t i = 0; i < n; i++) d_crcs[i] = blk_crc((const unsigned char *)d_base + i * stride, len, fastcrc);
     return 0;
 }
@@ -139,7 +188,7 @@ int md5hip_digest_desc_variant(const void *d_base, const uint64_t *d_offsets, co
                                const uint32_t *d_order, uint64_t n, unsigned char *d_digests,
                                void *stream, int variant)
 {
-    (void)stream;
+    on_stream((hipStream_t)stream);
     (void)variant;
     if (((uintptr_t)d_digests & 15u) != 0) return -EINVAL;
     for (uint64_t k = 0; k < n; k++)
@@ -155,7 +204,7 @@ int md5hip_digest_desc_variant(const void *d_base, const uint64_t *d_offsets, co
 int crc32hip_desc(const void *d_base, const uint64_t *d_offsets, const uint32_t *d_lens,
                   const uint32_t *d_order, uint64_t n, uint32_t fastcrc, uint32_t *d_crcs, void *stream)
 {
-    (void)stream;
+    on_stream((hipStream_t)stream);
     for (uint64_t k = 0; k < n; k++) {
         const uint64_t c = d_order ? d_order[k] : k;
         if (c >= n) return -EINVAL;
@@ -174,12 +223,12 @@ int crc32hip_desc_variant(const void *d_base, const uint64_t *d_offsets, const u
 
 int md5hip_crc_desc_choice(uint64_t n, uint64_t mean_len)
 {
-    return (mean_len >= 2048 ? n <= 128 * 256 : n <= 12 * 256) ? 7 : 0;
+    return (mean_len >= 2048 ? n <= 128 * 256 : n <= 12 * 256) ? 7 : 6;
 }
 
 int md5hip_gather_launch(const struct md5hip_seg *d_segs, uint64_t nseg, unsigned char *d_dst, void *stream)
 {
-    (void)stream;
+    on_stream((hipStream_t)stream);
     for (uint64_t k = 0; k < nseg; k++)
         memmove((void *)((uintptr_t)d_dst + d_segs[k].dst), (const void *)(uintptr_t)d_segs[k].src, d_segs[k].len);
     return 0;
@@ -215,7 +264,7 @@ int md5hip_plan_hist(const uint32_t *hist, uint32_t kmax, uint64_t n, uint32_t *
 int md5hip_order_device(const uint32_t *d_lens, uint64_t n, uint32_t kmax, uint32_t *d_bucket_next,
                         uint32_t *d_order, void *stream)
 {
-    (void)stream;
+    on_stream((hipStream_t)stream);
     for (uint64_t i = 0; i < n; i++) {
         const uint32_t k = (d_lens[i] >> 6) + 1;
         if (k > kmax) continue;

@@ -1,0 +1,61 @@
+"""The synchronous call site at the reference's thread scale: netcache's ASIO
+pool runs 4-512 threads into the block checksum at once (asio_mgr.c:86-91,
+:205, :1050-1057).  build/c/asio_scale (tests/c/asio_scale.c, plain C over
+the C ABI) runs T threads, each submitting 64 x 16 KiB vectors synchronously
+on ONE batcher or on a pool over (0, 0), and checks every call's digests
+against the oracle.
+
+One caller per in-flight launch polls its event; every other blocked caller
+sleeps on its slot and is woken by the retire (md5_submit.c wait_ticket /
+watch_launch), so the CPU a call costs must not grow with the number of
+callers: at 256 threads it stays within 1.5x of the 8-thread figure (the
+VERDICT r03 bound; measured figures in profiles/r04/asio_scale_threads.json).
+The CPU-only test checks that the probe fails loudly without a device."""
+import json
+import os
+import subprocess
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+EXE = os.path.join(REPO, "build", "c", "asio_scale")
+
+
+def _run(*args, timeout=120):
+    if not os.path.exists(EXE):
+        pytest.fail(f"{EXE} missing: run __graft_entry__.build() (make -C tests/c)")
+    out = subprocess.run([EXE, *map(str, args)], capture_output=True, text=True, timeout=timeout)
+    rec = json.loads(out.stdout.strip().splitlines()[-1])
+    return out.returncode, rec
+
+
+def test_asio_probe_without_device_fails_loudly():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a HIP device is visible")
+    rc, rec = _run("batcher", 4, 8, 16384, 0.2)
+    assert rc == 77 and rec["rc"] == -19
+
+
+def test_asio_probe_host_target_matches_oracle():
+    """The host leg (product MD5Init/Update/Final on the calling thread)
+    runs anywhere; its digests are checked against the oracle like the
+    device legs'."""
+    rc, rec = _run("host", 2, 4, 16384, 0.2)
+    assert rc == 0 and rec["mismatches"] == 0 and rec["calls"] > 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("target", ["batcher", "pool"])
+def test_asio_scale_cpu_per_call_bounded(cuda, target):
+    res = {}
+    for T in (8, 64, 256):
+        rc, rec = _run(target, T, 64, 16384, 2.0)
+        assert rc == 0 and rec["mismatches"] == 0 and rec["rc"] == 0, rec
+        assert rec["calls"] >= T, rec
+        res[T] = rec
+    c8 = res[8]["thread_cpu_us_per_call"]["mean"]
+    c256 = res[256]["thread_cpu_us_per_call"]["mean"]
+    assert c256 <= 1.5 * c8, (c8, c256)
+    # the launches coalesce more callers as they grow
+    assert res[256]["max_tickets_per_launch"] > res[8]["max_tickets_per_launch"]

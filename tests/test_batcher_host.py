@@ -8,9 +8,13 @@ page lists, verify, host_fixed, device-resident with host or device digests
 and a producer stream, pool whole and split, CRC-32, netcache header
 verification on the shared MD5 batcher, explicit flush) while one thread
 changes the knobs and another registers, uses and unregisters a private
-page range; a failing launch is injected once.  Runs under ASan+UBSan and
-under ThreadSanitizer (which found the unlocked gather-mode read in submit(),
-now atomic)."""
+page range; a failing launch is injected once; the pool spans three devices
+and every copy or kernel must be enqueued from its stream's device (waits
+and polls on another device's ticket included).  First, 64 blocked callers
+wait on one slot for 12 rounds, every other round with the watcher's spin
+ending on NotReady just as the launch completes (the round-3 lost wake-up,
+which hangs that phase).  Runs under ASan+UBSan and under ThreadSanitizer
+(which found the unlocked gather-mode read in submit(), now atomic)."""
 import os
 import shutil
 import subprocess
@@ -38,6 +42,7 @@ def _build_and_run(name, san, env_extra, secs):
     out = subprocess.run([exe, str(secs)], capture_output=True, text=True, env=env, timeout=300)
     assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-3000:]
     assert out.stdout.strip().endswith("batcher ok")
+    assert "blocked callers: 12 rounds x 64 waiters on one slot ok" in out.stdout
 
 
 def test_batcher_under_asan():

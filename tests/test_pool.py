@@ -251,6 +251,40 @@ def test_device_submit_ordered_after_producer_stream(cuda):
         assert np.array_equal(out.cpu().numpy(), want)
 
 
+def test_device_submit_ordered_after_default_stream(cuda):
+    """after='current' while torch's DEFAULT stream is current (handle 0):
+    the kernel still runs after the producer's work on the null stream
+    (md5_batch_submit_device_after, order=1).  Round 3 passed the 0 handle
+    to md5_batch_submit_device_on, which reads NULL as "no ordering", and the
+    batcher's non-blocking streams do not wait for the null stream: the
+    kernel read the chunks before the producer wrote them."""
+    n, Lc = 2048, 16384
+    host = gen.xorshift_array(n * Lc, seed=343)
+    src = torch.from_numpy(host).to(cuda)
+    torch.cuda.synchronize()
+    want = gen.oracle_digests_fixed(host, n, Lc)
+    dst = torch.zeros_like(src)
+    ptrs = np.arange(n, dtype=np.uint64) * np.uint64(Lc) + np.uint64(dst.data_ptr())
+    lens = np.full(n, Lc, np.uint32)
+    assert torch.cuda.current_stream(cuda).cuda_stream == 0, "torch's default stream is the null stream"
+    with m.Queue(device=0) as q:
+        for rep in range(3):
+            dst.zero_()
+            torch.cuda.synchronize()
+            torch.cuda._sleep(20_000_000)          # a producer still busy on the null stream ...
+            dst.copy_(src)                         # ... whose last step writes the chunks
+            if rep < 2:
+                got = q.submit_device(ptrs, lens)              # after = current = default
+            else:
+                out = torch.empty((n, 16), dtype=torch.uint8, device=cuda)
+                q.submit_device_async(ptrs, lens, out=out).wait()
+                got = out.cpu().numpy()
+            assert np.array_equal(got, want), rep
+        # after=None is still "no ordering": the caller synchronizes first
+        torch.cuda.synchronize()
+        assert np.array_equal(q.submit_device(ptrs, lens, after=None), want)
+
+
 def test_queue_crc32_device_submit(cuda):
     """A CRC-32 queue returns (n,) u32 digests from device submissions; a
     wrong-sized or foreign `out` is rejected before any device work."""
