@@ -31,7 +31,8 @@ extern "C" {
 #endif
 
 /* ABI 3 (round 4): md5_batch_submit_device_after (an ordering flag apart from
- * the producer stream, so the null stream can be ordered on); round 3 had
+ * the producer stream, so the null stream can be ordered on), the LINES
+ * descriptor kernel and md5hip_plan_desc_at (appended); round 3 had
  * already grown MD5HIP_DESC_NUM_VARIANTS 6 -> 7 (FED) and CRC32HIP_NUM_VARIANTS
  * 7 -> 8 (SPLIT) -- appended values, compatible -- and made the pool route a
  * submission whole (same results; set_digest no longer drains). */
@@ -97,7 +98,11 @@ enum md5hip_desc_variant {
                                4 VALU per step instead of 5; groups holding an unaligned
                                chunk start (or no chunk of >= 128 B) go LANE.  The
                                planner's choice for small batches (round 3) */
-    MD5HIP_DESC_NUM_VARIANTS = 7
+    MD5HIP_DESC_LINES = 7,  /* XDMA whose waves holding a chunk that does not start on a
+                               128-B line load whole lines, each once, instead of
+                               chunk-relative 128-B stages straddling two lines (ABI 3;
+                               md5hip_plan_desc_at's choice for such batches) */
+    MD5HIP_DESC_NUM_VARIANTS = 8
 };
 int md5hip_digest_desc_variant(const void *d_base, const uint64_t *d_offsets,
                                const uint32_t *d_lens, const uint32_t *d_order, uint64_t n,
@@ -201,6 +206,12 @@ int md5hip_arena_free(void *d_ptr);
  * long), so their serial chains bound the launch; else XDMA.
  */
 int md5hip_plan_desc(const uint32_t *lens, uint64_t n, uint32_t *order);
+/* ABI 3: the same for chunks whose device addresses (or offsets from a
+ * 128-B-aligned base) the caller holds on the host, addrs[i]: an XDMA batch
+ * becomes MD5HIP_DESC_LINES when more than half its bytes lie in chunks that
+ * start 16-B but not 128-B aligned (device-resident blocks packed at 16 B),
+ * whose chunk-relative 128-B stages would straddle lines. */
+int md5hip_plan_desc_at(const uint32_t *lens, const uint64_t *addrs, uint64_t n, uint32_t *order);
 
 /* Planning without sorting on the host, for producers that count lengths as
  * chunks arrive (the batcher does): hist[k] = number of chunks whose key

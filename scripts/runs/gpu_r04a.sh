@@ -1,16 +1,22 @@
 #!/bin/bash
-# Round-4 call A: the blocked-caller rework (one watcher per launch, per-slot
-# sleeps), the null-stream ordering fix and the device-entry fixes on the GPU;
-# the call site at ASIO scale (8/64/256 threads) with the round-3 batcher
-# (build/abr04/old) beside it; the chunk_size matrix (16 KiB / 128 KiB / 1 MiB).
+# Round-4 call A: the call site at ASIO scale (8/64/256 threads) with the
+# round-3 batcher (build/abr04/old) beside it; the GPU tests of the
+# blocked-caller rework, the null-stream ordering fix and the LINES loader;
+# XDMA vs LINES timing and HBM bytes; where a drained c3q step's time goes,
+# and the c3q line; the chunk_size matrix.
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
 O=gpurun_out/r04a
 mkdir -p $O
-timeout -k 10 600 python3 -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu \
-  tests/test_pool.py tests/test_asio_scale.py tests/test_c_site.py tests/test_queue.py > $O/pytest.log 2>&1
+timeout -k 10 200 python3 -u scripts/asio_scale.py --matrix threads --secs 3 --out $O/asio_threads.json > $O/asio_threads.log 2>&1 || { echo "threads matrix failed"; tail -3 $O/asio_threads.log; exit 1; }
+LD_LIBRARY_PATH=$PWD/build/abr04/old timeout -k 10 200 python3 -u scripts/asio_scale.py --matrix threads --secs 3 --out $O/asio_threads_r03lib.json > $O/asio_threads_r03lib.log 2>&1 || { echo "r03 threads matrix failed"; tail -3 $O/asio_threads_r03lib.log; exit 1; }
+timeout -k 10 400 python3 -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu \
+  tests/test_lines.py tests/test_pool.py tests/test_asio_scale.py tests/test_c_site.py tests/test_queue.py > $O/pytest.log 2>&1
 rc=$?; tail -5 $O/pytest.log; [ $rc = 0 ] || { echo "pytest failed $rc"; exit 1; }
-timeout -k 10 300 python3 -u scripts/asio_scale.py --matrix threads --secs 3 --out $O/asio_threads.json > $O/asio_threads.log 2>&1 || { echo "threads matrix failed"; tail -3 $O/asio_threads.log; exit 1; }
-LD_LIBRARY_PATH=$PWD/build/abr04/old timeout -k 10 300 python3 -u scripts/asio_scale.py --matrix threads --secs 3 --out $O/asio_threads_r03lib.json > $O/asio_threads_r03lib.log 2>&1 || { echo "r03 threads matrix failed"; tail -3 $O/asio_threads_r03lib.log; exit 1; }
-timeout -k 10 500 python3 -u scripts/asio_scale.py --matrix chunk --secs 2 --out $O/asio_chunk.json > $O/asio_chunk.log 2>&1 || { echo "chunk matrix failed"; tail -3 $O/asio_chunk.log; exit 1; }
+timeout -k 10 200 python3 -u scripts/lines_ab.py > $O/lines_ab.log 2>&1 || { echo "lines_ab failed"; tail -3 $O/lines_ab.log; exit 1; }
+timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --kernel-trace --stats --output-format csv -d $O/pmc_lines -o pmc -- python3 scripts/lines_ab.py --rounds 2 --shapes packed16,packed128 > $O/pmc_lines.log 2>&1 || { echo "pmc lines failed"; exit 1; }
+timeout -s KILL 150 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d $O/c3q_trace -o trace -- python3 scripts/c3q_breakdown.py --steps 6 --out $O/c3q_stamps.json > $O/c3q_breakdown.log 2>&1 || { echo "c3q breakdown failed"; tail -3 $O/c3q_breakdown.log; exit 1; }
+python3 scripts/c3q_breakdown.py --join $O/c3q_trace --stamps $O/c3q_stamps.json --out $O/c3q_breakdown.json >> $O/c3q_breakdown.log 2>&1
+timeout -k 10 200 python3 bench.py --config c3q --steps 10 --no-cpu-baseline > $O/c3q.json 2> $O/c3q.err || { echo "c3q bench failed"; tail -3 $O/c3q.err; exit 1; }
+timeout -k 10 330 python3 -u scripts/asio_scale.py --matrix chunk --secs 2 --out $O/asio_chunk.json > $O/asio_chunk.log 2>&1 || { echo "chunk matrix failed"; tail -3 $O/asio_chunk.log; exit 1; }
 echo done

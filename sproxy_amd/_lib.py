@@ -80,6 +80,7 @@ def lib():
         "md5hip_digest_desc_variant": (i, [vp, vp, vp, vp, u64, vp, vp, i]),
         "md5hip_plan_order": (i, [vp, u64, vp]),
         "md5hip_plan_desc": (i, [vp, u64, vp]),
+        "md5hip_plan_desc_at": (i, [vp, vp, u64, vp]),
         "md5hip_arena_alloc": (i, [i, u64, vp]),
         "md5hip_arena_free": (i, [vp]),
         "crc32hip_fixed": (i, [vp, u64, u32, u64, u32, vp, vp]),
@@ -177,7 +178,7 @@ EXPORTS = ["MD5Init", "MD5Update", "MD5Final", "nc_MD5Init", "nc_MD5Update", "nc
            "md5hip_final_ctx", "md5hip_pool_set_split", "md5hip_pool_submit_async",
            "md5hip_pool_submit_iov_async", "md5hip_pool_wait", "md5hip_pool_poll",
            "md5hip_pool_get_stats", "md5hip_pool_device_stats", "md5_batch_submit_device_on",
-           "md5_batch_submit_device_after"]
+           "md5_batch_submit_device_after", "md5hip_plan_desc_at"]
 
 
 def check(fn, rc):

@@ -28,6 +28,12 @@ int md5hip_gather_launch(const struct md5hip_seg *d_segs, uint64_t nseg, unsigne
 __attribute__((visibility("hidden")))
 int md5hip_crc_desc_choice(uint64_t n, uint64_t mean_len);
 
+/* MD5 descriptor variant for a planned batch of `bytes` payload of which
+ * `unlined_bytes` lie in chunks starting 16-B but not 128-B aligned: XDMA
+ * becomes LINES past half (md5_kernels.hip). */
+__attribute__((visibility("hidden")))
+int md5hip_lines_choice(int variant, uint64_t unlined_bytes, uint64_t bytes);
+
 /* Batched verify with a digest kind of its own (md5_submit.c): the
  * batcher's setting is not touched, so concurrent submitters keep theirs. */
 struct md5hip_batcher;

@@ -443,9 +443,17 @@ __device__ __forceinline__ void wait_vmcnt() {
   else asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
 }
 
+// kShift (kDma, one image): a wave holding a chunk that does not start on a
+// 128-B line loads whole LINES instead of chunk-relative 128-B stages, each
+// line once; a lane rotates its line reads by its chunk's 16-B offset s and
+// takes a window's last s pieces from the next line (one line of registers
+// more, 32 v_cndmask per 128 B).  Chunk-relative stages of such a chunk
+// straddle two lines and share one with the next stage, which L2 evicts
+// between the two visits under 16 waves per CU (16-B-packed ragged blocks:
+// 1.29x the payload read from HBM).
 template <int CP, class H, uint32_t kLong = 0, int D = 1, bool kHalf = false, bool kPeel = true,
           bool kDma = false, class Src = DescArrays, bool kLongPair = true, int NB = 1, int W = 1,
-          bool kHashOff = false>
+          bool kHashOff = false, bool kShift = false>
 __device__ __forceinline__ void desc_xpose_group(H& h, const uint8_t* __restrict__ base,
                                                  const Src& src, uint64_t n,
                                                  uint64_t first, typename H::Out* __restrict__ out,
@@ -660,7 +668,8 @@ __device__ __forceinline__ void desc_xpose_group(H& h, const uint8_t* __restrict
       // line leave L2 before the next stage asks for it (16-B-packed ragged
       // blocks: 1.83x HBM bytes, 1.35x time), so such waves load with the
       // default policy (profiles/r02_desc_cache_policy_ab.json).
-      const bool lined = __ballot(((uint32_t)off & 127u) != 0 && live && nst != 0) == 0;
+      const bool lined =
+          __ballot(((uint32_t)(uintptr_t)chunk & 127u) != 0 && live && nst != 0) == 0;
       // Until the first row runs out (stage rmin), no row's stage index is
       // clamped and the stage offset is wave-uniform: one 64-bit add per row
       // with the offset in SGPRs instead of min + shift + add (16 VALU fewer
@@ -699,7 +708,78 @@ __device__ __forceinline__ void desc_xpose_group(H& h, const uint8_t* __restrict
           }
         }
       };
-      if (CP == 0 || !lined) run(std::integral_constant<int, 0>{});
+      // kShift: whole lines.  Row r's line L is the 128-B line L of its chunk's
+      // line-aligned base; window k (chunk bytes [128k, 128k + 128)) is line k
+      // from piece s on, then line k + 1's first s pieces.  A lane reads line
+      // L rotated by s (piece q of the read = line piece (q + s) & 7), so
+      // window k's piece q is line k's read for q + s < 8, line k+1's after.
+      // Lines 0..smax (a row with s > 0 needs line nst; one with s = 0 is
+      // clamped to its own last stage).
+      auto run_lines = [&]() __attribute__((always_inline)) {
+        // rptr / rlast re-pointed at lines (their stage values are dead here)
+        const uint64_t ca = (uint64_t)(uintptr_t)chunk;
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+          uint32_t row = (uint32_t)r * 8u + (lane >> 3);
+          const uint32_t rn = (uint32_t)__shfl((int)nst, (int)row, 64);
+          if (rn == 0) row = mrow;
+          const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)ca, (int)row, 64);
+          const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(ca >> 32), (int)row, 64);
+          const uint32_t part = (lane & 7u) ^ ((row >> 1) & 7u);      // source swizzle (xpose)
+          rptr[r] = reinterpret_cast<const uint8_t*>(
+              (uintptr_t)((((uint64_t)hi << 32) | (lo & ~127u)) + part * 16u));
+          rlast[r] = (rn ? rn : smax) - 1u + ((lo & 127u) != 0u);
+        }
+        auto issue = [&](uint32_t L) __attribute__((always_inline)) {
+          if (L <= rmin) {                                     // wave-uniform, no row clamped
+            const uint64_t so = (uint64_t)L << 7;
+#pragma unroll
+            for (int r = 0; r < 8; ++r)
+              __builtin_amdgcn_global_load_lds(rptr[r] + so, limg + r * 1024, 16, 0, 0);
+          } else {
+#pragma unroll
+            for (int r = 0; r < 8; ++r)
+              __builtin_amdgcn_global_load_lds(rptr[r] + (min(L, rlast[r]) << 7), limg + r * 1024, 16,
+                                               0, 0);
+          }
+        };
+        const uint32_t sh = ((uint32_t)ca >> 4) & 7u;
+        auto read_rot = [&](uint4 (&R)[2][4]) __attribute__((always_inline)) {
+#pragma unroll
+          for (int q = 0; q < 8; ++q) {
+            const u32x4 v = *reinterpret_cast<const u32x4*>(myrow + ((((q + sh) & 7u) ^ g) * 16));
+            R[q >> 2][q & 3] = make_uint4(v.x, v.y, v.z, v.w);
+          }
+        };
+        uint4 ra[2][4], rb[2][4];
+        issue(0);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        read_rot(ra);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        issue(1);
+        // window k: `cur` (line k) completed in place from `nxt` (line k + 1,
+        // read here; the next window's `cur`)
+        auto step = [&](uint32_t k, uint4 (&cur)[2][4], uint4 (&nxt)[2][4]) __attribute__((always_inline)) {
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          read_rot(nxt);
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // reads done before the refill
+          if (k + 2 <= smax) issue(k + 2);
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int q = 0; q < 8; ++q)
+            if ((uint32_t)q + sh >= 8u) cur[q >> 2][q & 3] = nxt[q >> 2][q & 3];
+          if (k < nst) {
+            h.block(st, cur[0]);
+            h.block(st, cur[1]);
+          }
+        };
+        for (uint32_t k = 0; k < smax; k += 2) {
+          step(k, ra, rb);
+          if (k + 1 < smax) step(k + 1, rb, ra);
+        }
+      };
+      if (kShift && !lined) run_lines();
+      else if (CP == 0 || !lined) run(std::integral_constant<int, 0>{});
       else run(std::integral_constant<int, CP>{});
     } else {
     // D-stage register ring (2*D blocks of prefetch per lane)
@@ -733,7 +813,8 @@ __device__ __forceinline__ void desc_xpose_group(H& h, const uint8_t* __restrict
   }
 }
 
-template <int CP, class H = Md5Hasher<true>, uint32_t kLong = 0, int D = 1, bool kDma = false>
+template <int CP, class H = Md5Hasher<true>, uint32_t kLong = 0, int D = 1, bool kDma = false,
+          bool kShift = false>
 __device__ __forceinline__ void desc_xpose_body(const uint8_t* __restrict__ base,
                                                 const uint64_t* __restrict__ offs,
                                                 const uint32_t* __restrict__ lens,
@@ -743,8 +824,8 @@ __device__ __forceinline__ void desc_xpose_body(const uint8_t* __restrict__ base
   H h;
   const uint64_t first = ((uint64_t)blockIdx.x * blockDim.x) + (threadIdx.x & ~63u);
   if (first >= n) return;
-  desc_xpose_group<CP, H, kLong, D, false, true, kDma>(h, base, DescArrays{offs, lens, order}, n,
-                                                      first, out, img, nlong);
+  desc_xpose_group<CP, H, kLong, D, false, true, kDma, DescArrays, true, 1, 1, false, kShift>(
+      h, base, DescArrays{offs, lens, order}, n, first, out, img, nlong);
 }
 
 // Occupancy: 81 VGPRs and the 8 KiB image would allow 5 one-wave workgroups
@@ -761,6 +842,20 @@ md5_desc_xdma(const uint8_t* __restrict__ base, const uint64_t* __restrict__ off
   __shared__ __attribute__((aligned(16))) uint8_t img[8192];
   asm volatile("" ::: "v127");
   desc_xpose_body<2, Md5Hasher<true>, 0, 1, true>(base, offs, lens, order, n, out, img);
+}
+
+// LINES: XDMA for batches whose chunks mostly do not start on a 128-B line
+// (device-resident chunks packed at 16 B): waves holding such a chunk load
+// whole lines, each once (kShift), instead of chunk-relative stages that
+// straddle two lines (1.29x the payload from HBM under XDMA).  The second
+// line of registers costs occupancy (3 waves per SIMD instead of 4), so
+// line-aligned batches keep XDMA: md5hip_plan_desc_at chooses.
+__global__ void __launch_bounds__(64)
+md5_desc_lines(const uint8_t* __restrict__ base, const uint64_t* __restrict__ offs,
+               const uint32_t* __restrict__ lens, const uint32_t* __restrict__ order, uint64_t n,
+               uint4* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) uint8_t img[8192];
+  desc_xpose_body<2, Md5Hasher<true>, 0, 1, true, true>(base, offs, lens, order, n, out, img);
 }
 
 __global__ void __launch_bounds__(64)

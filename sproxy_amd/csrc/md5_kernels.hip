@@ -203,7 +203,8 @@ int md5hip_digest_desc_variant(const void* d_base, const uint64_t* d_offsets,
   if (!d_base || !d_offsets || !d_lens || !d_digests) return -EINVAL;
   if (((uintptr_t)d_digests & 15u) != 0) return -EINVAL;
   if (variant != MD5HIP_DESC_AUTO && variant != MD5HIP_DESC_LANE && variant != MD5HIP_DESC_HYBRID &&
-      variant != MD5HIP_DESC_XDMA && variant != MD5HIP_DESC_BALANCED && variant != MD5HIP_DESC_FED)
+      variant != MD5HIP_DESC_XDMA && variant != MD5HIP_DESC_BALANCED && variant != MD5HIP_DESC_FED &&
+      variant != MD5HIP_DESC_LINES)
     return -EINVAL;
   if (int e = device_ok()) return e;
   const uint64_t g = (n + 63) / 64;
@@ -235,6 +236,11 @@ int md5hip_digest_desc_variant(const void* d_base, const uint64_t* d_offsets,
     // chain + feeder wave per 64-chunk group (md5_kernels.h md5_desc_fed)
     hipLaunchKernelGGL(md5_desc_fed<false>, dim3((uint32_t)g), dim3(128), 0, s, base, d_offsets,
                        d_lens, d_order, n, (uint64_t)0, 0u, (uint4*)d_digests);
+    return launched();
+  }
+  if (variant == MD5HIP_DESC_LINES) {
+    hipLaunchKernelGGL(md5_desc_lines, dim3((uint32_t)g), dim3(64), 0, s, base, d_offsets, d_lens,
+                       d_order, n, (uint4*)d_digests);
     return launched();
   }
   if (variant == MD5HIP_DESC_AUTO || variant == MD5HIP_DESC_XDMA) {
@@ -672,6 +678,27 @@ int md5hip_plan_desc(const uint32_t* lens, uint64_t n, uint32_t* order) {
   const uint64_t depth = (uint64_t)cu_count() * 128u;
   const uint64_t p = depth < n - 1 ? depth : n - 1;
   return plan_choice(bmax, median, total, lens[order[p]] >> 6);
+}
+
+// md5_internal.h: XDMA becomes LINES when more than half the batch's bytes
+// lie in chunks that start 16-B but not 128-B aligned (their stages would
+// straddle lines).  Line-aligned and uniform batches keep XDMA, whose four
+// waves per SIMD LINES' extra line of registers does not allow.
+__attribute__((visibility("hidden"))) int md5hip_lines_choice(int variant, uint64_t unlined_bytes,
+                                                              uint64_t bytes) {
+  return variant == MD5HIP_DESC_XDMA && 2 * unlined_bytes > bytes ? MD5HIP_DESC_LINES : variant;
+}
+
+int md5hip_plan_desc_at(const uint32_t* lens, const uint64_t* addrs, uint64_t n, uint32_t* order) {
+  if (!addrs && n) return -EINVAL;
+  const int v = md5hip_plan_desc(lens, n, order);
+  if (v != MD5HIP_DESC_XDMA) return v;
+  uint64_t bytes = 0, unlined = 0;
+  for (uint64_t i = 0; i < n; ++i) {
+    bytes += lens[i];
+    if ((addrs[i] & 127u) != 0 && (addrs[i] & 15u) == 0) unlined += lens[i];
+  }
+  return md5hip_lines_choice(v, unlined, bytes);
 }
 
 int md5hip_plan_hist(const uint32_t* hist, uint32_t kmax, uint64_t n, uint32_t* bucket_start) {

@@ -218,6 +218,9 @@ struct slot {
     uint64_t opened_us, launched_us;  /* first chunk reserved / went in flight */
     uint64_t gen;                     /* launches of this slot so far (a waiter's check) */
     uint64_t load;                    /* this slot's share of b->load_bytes */
+    /* payload bytes, and those in device-resident chunks starting 16-B but not
+     * 128-B aligned (md5hip_lines_choice: LINES instead of XDMA) */
+    uint64_t payload, unlined;
     /* callers blocked on tickets held here sleep on `cv` (nwait of them):
      * broadcast when the slot retires, signalled once when it goes in flight
      * (one sleeper then watches the launch).  watch: WATCH_NONE / _ACTIVE (one
@@ -366,7 +369,8 @@ static int slot_prepare(md5hip_batcher *b, struct slot *sl)
         if (hipMemcpyAsync(sl->d_ord, sl->h_ord, 4 * n, hipMemcpyHostToDevice, sl->stream)) return -EIO;
     }
     if (sl->unsorted) sl->use_order = 1;
-    sl->plan_var = dvar;
+    /* host-staged chunks sit on 128-B lines; device-resident ones as placed */
+    sl->plan_var = md5hip_lines_choice(dvar, sl->unlined, sl->payload);
     sl->planned_n = n;
     return 0;
 }
@@ -467,6 +471,7 @@ static void slot_reset(struct slot *sl)
     sl->tickets_in = 0;
     sl->copied_n = sl->planned_n = sl->seen_n = 0;
     sl->load = 0;
+    sl->payload = sl->unlined = 0;
     sl->last_key = UINT32_MAX;
     sl->unsorted = sl->use_order = 0;
     if (sl->hh) memset(sl->hh, 0, sizeof(uint32_t) * ((size_t)sl->hkmax + 1));
@@ -1137,6 +1142,51 @@ static void gather_range(const struct chunk_src *src, uint64_t first, uint64_t m
 /* ------------------------------------------------------------------------
  * Submission
  * ------------------------------------------------------------------------ */
+/* Device-resident chunks [i, i + m) into slot `sl` (mu held, m fits): the
+ * descriptors, payload and key histogram in one pass with the running
+ * values in registers -- no bytes to stage, so a burst of C3 vectors
+ * (~80 K chunks each) costs the device no idle time beyond this loop
+ * (bench.py --config c3q `drained`). */
+static void reserve_device(md5hip_batcher *b, struct slot *sl, const struct chunk_src *src, uint64_t i,
+                           uint64_t m)
+{
+    uint64_t *ho = sl->h_off + sl->n;
+    uint32_t *hl = sl->h_len + sl->n;
+    uint32_t *hh = sl->hh;
+    const uint64_t *dp = src->dptrs + i;
+    const uint32_t *ln = src->lens + i;
+    const uint64_t dbase = (uint64_t)(uintptr_t)sl->d_data;
+    uint64_t pay = 0, unl = 0;
+    uint32_t last = sl->last_key, kmax = sl->hkmax;
+    int unsorted = sl->unsorted, hovf = sl->hovf;
+    for (uint64_t k = 0; k < m; k++) {
+        const uint64_t p = dp[k];
+        const uint32_t L = ln[k];
+        ho[k] = p - dbase;
+        hl[k] = L;
+        pay += L;
+        unl += ((p & 127u) != 0 && (p & 15u) == 0) ? L : 0;
+        const uint32_t key = (L >> 6) + 1;           /* L < 2^32: no overflow */
+        unsorted |= key > last;
+        last = key;
+        if (key > MD5HIP_HIST_KMAX) {
+            hovf = 1;
+        } else {
+            hh[key]++;
+            if (key > kmax) kmax = key;
+        }
+    }
+    sl->last_key = last;
+    sl->hkmax = kmax;
+    sl->unsorted = unsorted;
+    sl->hovf = hovf;
+    sl->payload += pay;
+    sl->unlined += unl;
+    sl->load += pay + 64 * m;
+    __atomic_store_n(&b->load_bytes, b->load_bytes + pay + 64 * m, __ATOMIC_RELAXED);
+    sl->n += m;
+}
+
 /* Reserve chunks [i, n) of `src` into the open slot (mu held): descriptors,
  * staging offsets, zero-copy tables.  Returns the number reserved (the slot
  * is marked full when a chunk did not fit) or -errno. */
@@ -1145,13 +1195,17 @@ static long reserve(md5hip_batcher *b, struct slot *sl, const struct chunk_src *
 {
     const int dev = b->device;
     uint64_t j = i;
-    if (zc) pthread_rwlock_rdlock(&g_reg_lock);
     if (sl->n == 0 && i < n) sl->opened_us = now_us();
+    if (src->dptrs) {
+        const uint64_t m = n - i < b->maxn - sl->n ? n - i : b->maxn - sl->n;
+        reserve_device(b, sl, src, i, m);
+        if (i + m < n) sl->full = 1;
+        return (long)m;
+    }
+    if (zc) pthread_rwlock_rdlock(&g_reg_lock);
     while (j < n && sl->n < b->maxn) {
         const uint64_t L = src_len(src, j);
-        if (src->dptrs) {                                      /* device-resident: no bytes */
-            sl->h_off[sl->n] = src->dptrs[j] - (uint64_t)(uintptr_t)sl->d_data;
-        } else {
+        {   /* host bytes (device-resident chunks: reserve_device above) */
             /* chunks packed on 128-B lines: the LDS-DMA loaders read 128-B
              * stages, and a stage off the line shares a line with the next
              * one (the nt policy is then off, md5_kernels.h) */
@@ -1204,6 +1258,7 @@ static long reserve(md5hip_batcher *b, struct slot *sl, const struct chunk_src *
         }
         sl->h_len[sl->n] = (uint32_t)L;
         sl->load += L + 64;
+        sl->payload += L;
         __atomic_store_n(&b->load_bytes, b->load_bytes + L + 64, __ATOMIC_RELAXED);
         {
             const uint64_t k = (L >> 6) + 1;
@@ -1241,10 +1296,10 @@ static int submit(md5hip_batcher *b, const struct chunk_src *src, uint64_t n, un
                   const hipStream_t *after)
 {
     const int urgent = async != 1;
-    for (uint64_t i = 0; i < n; i++) {
+    for (uint64_t i = 0; !src->dptrs && i < n; i++) {   /* device chunks: uint32 lengths, no staging */
         const uint64_t L = src_len(src, i);
         if (L > 0xffffffffull) return -E2BIG;
-        if (!src->dptrs && (L + 127) / 128 * 128 > b->cap) return -E2BIG;
+        if ((L + 127) / 128 * 128 > b->cap) return -E2BIG;
     }
     struct dev_guard g;
     if (dev_enter(&g, b->device)) return -ENODEV;

@@ -128,7 +128,7 @@ def digest_fixed(data, n: int = None, length: int = None, stride: int = None, ou
 
 
 DESC_VARIANTS = {"auto": 0, "lane": 1, "hybrid": 3, "xdma": 4, "balanced": 5,
-                 "fed": 6}   # enum md5hip_desc_variant
+                 "fed": 6, "lines": 7}   # enum md5hip_desc_variant
 
 
 def digest_desc(base, offsets, lens, order=None, out=None, stream=None, variant=0):
@@ -274,6 +274,21 @@ def plan_desc(lens):
     v = lib().md5hip_plan_desc(L.ctypes.data, L.size, order.ctypes.data)
     if v < 0:
         raise MD5HipError("md5hip_plan_desc", v)
+    return order[:L.size], {x: k for k, x in DESC_VARIANTS.items()}[v]
+
+
+def plan_desc_at(lens, addrs):
+    """(order, variant name): md5hip_plan_desc_at -- as plan_desc, for chunks
+    at the given device addresses (or offsets from a 128-B-aligned base):
+    'lines' for an XDMA batch mostly of chunks off their 128-B lines."""
+    L = np.ascontiguousarray(lens, dtype=np.uint32)
+    A = np.ascontiguousarray(addrs, dtype=np.uint64)
+    if A.size != L.size:
+        raise ValueError("one address per length")
+    order = np.empty(max(L.size, 1), dtype=np.uint32)
+    v = lib().md5hip_plan_desc_at(L.ctypes.data, A.ctypes.data, L.size, order.ctypes.data)
+    if v < 0:
+        raise MD5HipError("md5hip_plan_desc_at", v)
     return order[:L.size], {x: k for k, x in DESC_VARIANTS.items()}[v]
 
 
@@ -667,7 +682,7 @@ def pool_plan(lens, nparts: int) -> np.ndarray:
 
 
 __all__ = ["init_ctx", "update_ctx", "final_ctx", "MD5Context", "MD5Init", "MD5Update", "MD5Final", "MD5_DIGEST_SIZE", "MD5HipError", "arena_empty",
-           "plan_desc",
+           "plan_desc", "plan_desc_at",
            "md5", "digest_fixed", "digest_desc", "crc32_fixed", "crc32_desc", "plan_order", "fill_synthetic", "Batcher",
            "Pool", "Queue", "pool_plan", "CRC_VARIANTS", "DESC_VARIANTS",
            "register_host", "unregister_host",

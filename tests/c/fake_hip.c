@@ -221,6 +221,11 @@ int crc32hip_desc_variant(const void *d_base, const uint64_t *d_offsets, const u
     return crc32hip_desc(d_base, d_offsets, d_lens, d_order, n, fastcrc, d_crcs, stream);
 }
 
+int md5hip_lines_choice(int variant, uint64_t unlined_bytes, uint64_t bytes)
+{
+    return variant == MD5HIP_DESC_XDMA && 2 * unlined_bytes > bytes ? MD5HIP_DESC_LINES : variant;
+}
+
 int md5hip_crc_desc_choice(uint64_t n, uint64_t mean_len)
 {
     return (mean_len >= 2048 ? n <= 128 * 256 : n <= 12 * 256) ? 7 : 6;

@@ -119,7 +119,7 @@ def test_argument_errors_before_device_work():
     assert L.md5hip_digest_desc(None, None, None, None, 3, None, None) == EINVAL
     assert L.md5hip_digest_desc_variant(None, None, None, None, 0, None, None, 1) == 0
     assert L.md5hip_digest_desc_variant(ctypes.c_void_p(16), ctypes.c_void_p(16), ctypes.c_void_p(16),
-                                        None, 3, ctypes.c_void_p(16), None, 7) == EINVAL
+                                        None, 3, ctypes.c_void_p(16), None, 8) == EINVAL   # 8 = MD5HIP_DESC_NUM_VARIANTS
     assert L.md5hip_fill_synthetic(ctypes.c_void_p(16), 15, 1, None) == EINVAL
     h = ctypes.c_void_p()
     assert L.md5hip_batcher_create(0, 1 << 20, 99, ctypes.byref(h)) == EINVAL

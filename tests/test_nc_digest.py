@@ -64,10 +64,23 @@ def test_header_verify_rules():
     g = bytearray(h)
     g[16] ^= 1                                                # stored crc itself
     assert not nd.header_verify(g)
-    g = bytearray(h)
-    g[8:12] = struct.pack("<i", 19)                           # header_size below the fixed part
-    assert not nd.header_verify(g) and nd.header_crc(g) == 0
     assert nd.header_crc(bytearray(h) + b"trailing") == nd.header_crc(h)   # only header_size bytes
+
+
+def test_header_size_below_fixed_part_is_a_deliberate_divergence():
+    """DELIBERATE DIVERGENCE from the reference (DESIGN.md
+    §9): dm_verify_header (diskcache.c:3676-3689) CRCs header_size bytes with
+    no lower bound -- for 0 <= header_size < 20 a CRC over only part of the
+    fixed header (the zeroed crc / disk_header_size / flag fields partly
+    outside it), and for a negative header_size a length the reference never
+    guards.  Here a header whose header_size is below the 20-byte fixed part
+    (or negative) is rejected: header_verify false, header_crc 0, seal
+    -EINVAL.  Not parity: a corrupt size field is refused, not hashed."""
+    h, _ = _golden_headers()[3]
+    for hs in (19, 4, 0, -1, -(1 << 31)):
+        g = bytearray(h)
+        g[8:12] = struct.pack("<i", hs)
+        assert not nd.header_verify(g) and nd.header_crc(g) == 0, hs
 
 
 def test_host_crc32_matches_reference_vectors():
