@@ -5,7 +5,9 @@ of B blocks of L bytes synchronously; latency, CPU per call, every digest
 checked against the oracle).
 
   --matrix threads  VERDICT r03 item 1: 8 / 64 / 256 synchronous callers of
-                    64 x 16 KiB on one batcher and on a pool over (0, 0)
+                    64 x 16 KiB on one batcher and on a pool over (0, 0), from
+                    pageable memory (host copy into the pinned staging) and
+                    from registered pages (zero-copy: the queue's own cost)
   --matrix chunk    VERDICT r03 item 2: netcache's shipped chunk_size 128 KiB
                     (httpd.c:8627) and 1 MiB next to 16 KiB, vectors of 8 and
                     64 blocks, 1 / 8 / 64 callers, through the batcher and on
@@ -24,8 +26,8 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 EXE = os.path.join(REPO, "build", "c", "asio_scale")
 
 
-def run(target, threads, blocks, L, secs, timeout=150):
-    cmd = [EXE, target, str(threads), str(blocks), str(L), str(secs)]
+def run(target, threads, blocks, L, secs, mode="pageable", timeout=150):
+    cmd = [EXE, target, str(threads), str(blocks), str(L), str(secs), mode]
     t0 = time.time()
     out = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout)
     line = out.stdout.strip().splitlines()[-1] if out.stdout.strip() else "{}"
@@ -46,9 +48,10 @@ def main():
     a = ap.parse_args()
     runs = []
     if a.matrix == "threads":
-        for target in ("batcher", "pool"):
-            for T in (8, 64, 256):
-                runs.append(run(target, T, 64, 16384, a.secs))
+        for mode in ("registered", "pageable"):
+            for target in ("batcher", "pool"):
+                for T in (8, 64, 256):
+                    runs.append(run(target, T, 64, 16384, a.secs, mode))
     else:
         for L in (16384, 131072, 1 << 20):
             for B in (8, 64):

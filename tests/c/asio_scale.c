@@ -14,15 +14,23 @@
  *   host     MD5Init/MD5Update/MD5Final of the product library (md5_stream.c)
  *            per block on the calling thread -- the alternative the call
  *            site has, timed the same way
- * Each thread owns its own vector (distinct bytes); every call's digests are
- * compared with the oracle's (oracle/md5_oracle.c, linked in as the checker
- * and computed once per thread before timing).  Per call it records the wall
+ * Each thread owns R vectors of distinct bytes and submits them in turn, R
+ * chosen so that all threads' vectors together span at least 2 GiB: every
+ * call's source is cold in the host caches whatever the thread count (with
+ * one vector per thread, 8 threads' 8 MiB would stay in L3 and their
+ * staging copies would look cheaper than 256 threads').  MODE pageable (the
+ * default: the batcher copies the blocks into its pinned staging) or
+ * registered (each thread's vectors md5hip_host_register'ed: zero-copy, the
+ * device pulls them, no host copy -- what is left per call is the queue's
+ * own cost).  Every call's digests are compared with the oracle's
+ * (oracle/md5_oracle.c, linked in as the checker and computed once per
+ * vector before timing).  Per call it records the wall
  * latency and the calling thread's CPU time (CLOCK_THREAD_CPUTIME_ID, the
  * clock of getrusage(RUSAGE_THREAD), around the call); the process CPU time
  * over the timed window (CLOCK_PROCESS_CPUTIME_ID, which includes the
  * batchers' progress threads and the HIP runtime's) is reported per call too.  Prints one JSON object.
  *
- * usage: asio_scale TARGET THREADS BLOCKS BLOCK_BYTES SECS [SLICE_MIB NSLOTS]
+ * usage: asio_scale TARGET THREADS BLOCKS BLOCK_BYTES SECS [MODE [SLICE_MIB NSLOTS]]
  * Exit 0 = every digest equal to the oracle's; 1 = a mismatch or error;
  * 77 = no usable HIP device.
  */
@@ -33,6 +41,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sys/resource.h>
 #include <time.h>
 
 #include "md5.h"
@@ -51,6 +60,8 @@ static md5hip_batcher *g_b;
 static md5hip_pool *g_p;
 static pthread_barrier_t g_start, g_warm, g_go;
 static double g_t_end;          /* set between g_warm and g_go */
+static int g_nvec = 1;          /* vectors per thread (R) */
+static int g_register;          /* MODE registered */
 
 static double now(void)
 {
@@ -72,11 +83,11 @@ static double thread_cpu(void) { return cpu_clock(CLOCK_THREAD_CPUTIME_ID); }
 static double process_cpu(void) { return cpu_clock(CLOCK_PROCESS_CPUTIME_ID); }
 
 struct job {
-    int t;
-    unsigned char *buf;
-    const void **ptrs;
-    uint32_t *lens;
-    unsigned char (*want)[16], (*got)[16];
+    int t, cur;                  /* cur: the vector of the next call */
+    unsigned char *buf;          /* g_nvec vectors of BLOCKS x BLOCK_BYTES */
+    const void **ptrs;           /* g_nvec x BLOCKS */
+    uint32_t *lens;              /* BLOCKS (the same for every vector of a thread) */
+    unsigned char (*want)[16], (*got)[16];   /* want: g_nvec x BLOCKS */
     double *lat, *cpu;           /* per timed call */
     size_t ncalls, cap;
     int rc, bad;
@@ -84,16 +95,17 @@ struct job {
 
 static int one_call(struct job *j)
 {
+    const void **ptrs = j->ptrs + (size_t)j->cur * g_blocks;
     switch (g_target) {
     case T_BATCHER:
-        return md5_batch_submit(g_b, j->ptrs, j->lens, (uint64_t)g_blocks, &j->got[0][0]);
+        return md5_batch_submit(g_b, ptrs, j->lens, (uint64_t)g_blocks, &j->got[0][0]);
     case T_POOL:
-        return md5hip_pool_submit(g_p, j->ptrs, j->lens, (uint64_t)g_blocks, &j->got[0][0]);
+        return md5hip_pool_submit(g_p, ptrs, j->lens, (uint64_t)g_blocks, &j->got[0][0]);
     case T_HOST:
         for (int i = 0; i < g_blocks; i++) {
             struct MD5Context c;
             MD5Init(&c);
-            MD5Update(&c, j->ptrs[i], j->lens[i]);
+            MD5Update(&c, ptrs[i], j->lens[i]);
             MD5Final(j->got[i], &c);
         }
         return 0;
@@ -101,33 +113,40 @@ static int one_call(struct job *j)
     return -EINVAL;
 }
 
+/* the call's digests against the oracle's for its vector; then the next vector */
+static int check_next(struct job *j)
+{
+    const int bad = memcmp(j->got, j->want + (size_t)j->cur * g_blocks, 16 * (size_t)g_blocks) != 0;
+    j->cur = (j->cur + 1) % g_nvec;
+    return bad;
+}
+
 static void *worker(void *arg)
 {
     struct job *j = arg;
     const size_t vec = (size_t)g_blocks * g_len;
-    j->buf = malloc(vec + 64);
-    j->ptrs = malloc(sizeof(void *) * g_blocks);
+    j->buf = malloc(vec * g_nvec + 64);
+    j->ptrs = malloc(sizeof(void *) * g_blocks * g_nvec);
     j->lens = malloc(sizeof(uint32_t) * g_blocks);
-    j->want = malloc(16 * (size_t)g_blocks);
+    j->want = malloc(16 * (size_t)g_blocks * g_nvec);
     j->got = malloc(16 * (size_t)g_blocks);
-    if (!j->buf || !j->ptrs || !j->lens || !j->want || !j->got) {
-        j->rc = -ENOMEM;
-        pthread_barrier_wait(&g_start);
-        pthread_barrier_wait(&g_warm);
-        pthread_barrier_wait(&g_go);
-        return NULL;
-    }
-    oracle_xorshift_fill(j->buf, vec + 64, 0x5A11ull + (uint64_t)j->t * 7919u);
-    for (int i = 0; i < g_blocks; i++) {
-        /* a short last block, as a vector's tail block often is (blk_io.c:377) */
-        j->lens[i] = i == g_blocks - 1 && g_blocks > 1 ? g_len - 1000u * (uint32_t)(1 + j->t % 7) : g_len;
-        j->ptrs[i] = j->buf + (size_t)i * g_len;
-        oracle_md5(j->ptrs[i], j->lens[i], j->want[i]);
+    if (!j->buf || !j->ptrs || !j->lens || !j->want || !j->got) j->rc = -ENOMEM;
+    if (!j->rc) {
+        oracle_xorshift_fill(j->buf, vec * g_nvec + 64, 0x5A11ull + (uint64_t)j->t * 7919u);
+        for (int i = 0; i < g_blocks; i++)   /* a short last block, as a vector's tail often is (blk_io.c:377) */
+            j->lens[i] = i == g_blocks - 1 && g_blocks > 1 ? g_len - 1000u * (uint32_t)(1 + j->t % 7) : g_len;
+        for (int v = 0; v < g_nvec; v++)
+            for (int i = 0; i < g_blocks; i++) {
+                const size_t k = (size_t)v * g_blocks + i;
+                j->ptrs[k] = j->buf + v * vec + (size_t)i * g_len;
+                oracle_md5(j->ptrs[k], j->lens[i], j->want[k]);
+            }
+        if (g_register) j->rc = md5hip_host_register(j->buf, vec * g_nvec + 64);
     }
     pthread_barrier_wait(&g_start);
     for (int w = 0; w < 2 && !j->rc; w++) {               /* warm-up calls, checked */
         j->rc = one_call(j);
-        if (!j->rc && memcmp(j->got, j->want, 16 * (size_t)g_blocks)) j->bad++;
+        if (!j->rc) j->bad += check_next(j);
     }
     pthread_barrier_wait(&g_warm);
     pthread_barrier_wait(&g_go);
@@ -141,7 +160,7 @@ static void *worker(void *arg)
             j->rc = rc;
             break;
         }
-        if (memcmp(j->got, j->want, 16 * (size_t)g_blocks)) j->bad++;
+        j->bad += check_next(j);
         if (j->ncalls == j->cap) {
             j->cap = j->cap ? 2 * j->cap : 1024;
             j->lat = realloc(j->lat, sizeof(double) * j->cap);
@@ -152,7 +171,6 @@ static void *worker(void *arg)
         j->cpu[j->ncalls] = (c1 - c0) * 1e6;
         j->ncalls++;
     }
-    free(j->buf);
     return NULL;
 }
 
@@ -172,7 +190,8 @@ static double pct(const double *v, size_t n, double p)
 int main(int argc, char **argv)
 {
     if (argc < 6) {
-        fprintf(stderr, "usage: %s batcher|pool|host THREADS BLOCKS BLOCK_BYTES SECS [SLICE_MIB NSLOTS]\n", argv[0]);
+        fprintf(stderr, "usage: %s batcher|pool|host THREADS BLOCKS BLOCK_BYTES SECS [pageable|registered [SLICE_MIB NSLOTS]]\n",
+                argv[0]);
         return 2;
     }
     g_target = !strcmp(argv[1], "pool") ? T_POOL : !strcmp(argv[1], "host") ? T_HOST : T_BATCHER;
@@ -180,9 +199,15 @@ int main(int argc, char **argv)
     g_blocks = atoi(argv[3]);
     g_len = (uint32_t)strtoul(argv[4], NULL, 0);
     g_secs = atof(argv[5]);
-    const uint64_t slice = argc > 6 ? strtoull(argv[6], NULL, 0) << 20 : 0;
-    const uint32_t nslots = argc > 7 ? (uint32_t)atoi(argv[7]) : 0;
+    g_register = argc > 6 && !strcmp(argv[6], "registered");
+    const uint64_t slice = argc > 7 ? strtoull(argv[7], NULL, 0) << 20 : 0;
+    const uint32_t nslots = argc > 8 ? (uint32_t)atoi(argv[8]) : 0;
     if (g_threads < 1 || g_threads > 1024 || g_blocks < 1 || g_len < 8000 || g_secs <= 0) return 2;
+    {   /* all threads' vectors span >= 2 GiB (cold sources) */
+        const double vec = (double)g_blocks * g_len, ws = 2.0 * (1u << 30);
+        g_nvec = (int)(ws / (vec * g_threads) + 0.999);
+        if (g_nvec < 1) g_nvec = 1;
+    }
     int rc = 0;
     if (g_target == T_BATCHER) rc = md5hip_batcher_create(0, slice, nslots, &g_b);
     if (g_target == T_POOL) {
@@ -214,11 +239,16 @@ int main(int argc, char **argv)
     }
     pthread_barrier_wait(&g_start);               /* oracle digests done */
     pthread_barrier_wait(&g_warm);                /* warm-up calls done */
+    struct rusage ru0, ru1;
+    getrusage(RUSAGE_SELF, &ru0);
     const double p0 = process_cpu(), w0 = now();
     g_t_end = w0 + g_secs;
     pthread_barrier_wait(&g_go);                  /* (the barrier orders g_t_end) */
     for (int t = 0; t < g_threads; t++) pthread_join(th[t], NULL);
     const double wall = now() - w0, pcpu = process_cpu() - p0;
+    getrusage(RUSAGE_SELF, &ru1);
+    const double usr = (ru1.ru_utime.tv_sec - ru0.ru_utime.tv_sec) + (ru1.ru_utime.tv_usec - ru0.ru_utime.tv_usec) * 1e-6;
+    const double sys = (ru1.ru_stime.tv_sec - ru0.ru_stime.tv_sec) + (ru1.ru_stime.tv_usec - ru0.ru_stime.tv_usec) * 1e-6;
     size_t total = 0;
     int bad = 0, err = 0;
     double bytes = 0;
@@ -252,18 +282,25 @@ int main(int argc, char **argv)
                     st.max_tickets_per_launch = s2.max_tickets_per_launch;
             }
     }
-    printf("{\"target\": \"%s\", \"threads\": %d, \"blocks\": %d, \"block_bytes\": %u, \"secs\": %.3f, "
+    printf("{\"target\": \"%s\", \"mode\": \"%s\", \"vectors_per_thread\": %d, \"threads\": %d, "
+           "\"blocks\": %d, \"block_bytes\": %u, \"secs\": %.3f, "
            "\"calls\": %zu, \"lat_us\": {\"p50\": %.1f, \"p90\": %.1f, \"p99\": %.1f, \"max\": %.1f}, "
            "\"thread_cpu_us_per_call\": {\"mean\": %.2f, \"p50\": %.2f, \"p99\": %.2f}, "
-           "\"process_cpu_us_per_call\": %.2f, \"process_cpu_cores\": %.2f, \"gib_s\": %.3f, "
+           "\"process_cpu_us_per_call\": %.2f, \"process_cpu_cores\": %.2f, "
+           "\"process_user_sys_us_per_call\": [%.2f, %.2f], \"gib_s\": %.3f, "
            "\"launches\": %llu, \"coalesced_launches\": %llu, \"max_tickets_per_launch\": %llu, "
            "\"mismatches\": %d, \"rc\": %d}\n",
-           argv[1], g_threads, g_blocks, g_len, wall, total, pct(lat, total, 50), pct(lat, total, 90),
+           argv[1], g_register ? "registered" : "pageable", g_nvec, g_threads, g_blocks, g_len, wall, total, pct(lat, total, 50), pct(lat, total, 90),
            pct(lat, total, 99), total ? lat[total - 1] : 0.0, total ? cpu_sum / (double)total : 0.0,
            pct(cpu, total, 50), pct(cpu, total, 99), total ? pcpu * 1e6 / (double)total : 0.0, pcpu / wall,
+           total ? usr * 1e6 / (double)total : 0.0, total ? sys * 1e6 / (double)total : 0.0,
            bytes / wall / (double)(1u << 30), (unsigned long long)st.launches,
            (unsigned long long)st.coalesced_launches, (unsigned long long)st.max_tickets_per_launch, bad, err);
     if (g_b) md5hip_batcher_destroy(g_b);
     if (g_p) md5hip_pool_destroy(g_p);
+    for (int t = 0; t < g_threads; t++) {
+        if (g_register && jobs[t].buf) md5hip_host_unregister(jobs[t].buf);
+        free(jobs[t].buf);
+    }
     return bad || err || total == 0 ? 1 : 0;
 }

@@ -79,9 +79,10 @@ def test_lines_kernel_matches_oracle(cuda, case):
 @pytest.mark.gpu
 def test_queue_device_submit_packed16_matches_oracle(cuda):
     """Device-resident netcache blocks packed at 16 B through the queue: the
-    slot's plan takes LINES (md5hip_lines_choice); digests equal the oracle."""
+    slot's plan takes LINES (md5hip_lines_choice); digests equal the oracle.
+    (768 groups: past the small-batch planners' two groups per CU.)"""
     import torch
-    n = 256 * 64 * 2
+    n = 256 * 64 * 3
     lens = [16384] * n
     rng = np.random.default_rng(7)
     for i in range(0, n, 8):
