@@ -246,7 +246,10 @@ int md5hip_fill_synthetic(void *d_dst, uint64_t nbytes, uint64_t seed, void *str
  * its pinned staging, device-resident chunks add only a descriptor -- and
  * the slot is launched as ONE planned descriptor batch when it is full, when
  * fewer than `inflight target` slots are running (an idle device takes work
- * at once), or when a caller waits on, polls or flushes a ticket in it.
+ * at once), when it is chained behind a launch about to end
+ * (md5hip_batcher_set_chain), or when a caller waits on, polls or flushes a
+ * ticket in it while nothing runs (a synchronous submission is such a wait:
+ * on a busy device it coalesces with the other callers' work).
  * While the device is busy, everything submitted meanwhile is therefore
  * coalesced into the next launch.  A progress thread per batcher retires
  * finished slots, delivers digests and launches the open slot.
@@ -285,6 +288,13 @@ int md5hip_batcher_set_inflight(md5hip_batcher *b, uint32_t target);
  * flush on one of its tickets, a full slot or a synchronous submission still
  * launches at once.  Default max_us 5000; 0 = launch at once. */
 int md5hip_batcher_set_linger(md5hip_batcher *b, uint32_t max_us);
+/* ABI 3: chained launches (default on).  With the pipeline at its target and
+ * the running launch due to end within min(2 ms, a quarter of a launch), the
+ * open slot -- planned, no chunk arrived since the last poll -- is launched
+ * at once with its hash kernel waiting on the running launch's event, so it
+ * starts when that one ends instead of after the host has seen it end (a C3
+ * stream step lost ~1.3 ms to that).  0 turns it off. */
+int md5hip_batcher_set_chain(md5hip_batcher *b, int on);
 
 struct md5hip_batcher_stats {
     uint64_t submissions;             /* tickets issued */

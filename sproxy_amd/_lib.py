@@ -92,6 +92,7 @@ def lib():
         "md5hip_queue_create": (i, [i, u64, u32, ctypes.POINTER(vp)]),
         "md5hip_batcher_set_inflight": (i, [vp, u32]),
         "md5hip_batcher_set_linger": (i, [vp, u32]),
+        "md5hip_batcher_set_chain": (i, [vp, i]),
         "md5hip_plan_hist": (i, [vp, u32, u64, vp]),
         "md5hip_order_device": (i, [vp, u64, u32, vp, vp, vp]),
         "md5hip_batcher_get_stats": (i, [vp, ctypes.POINTER(MD5HipBatcherStats)]),
@@ -178,7 +179,7 @@ EXPORTS = ["MD5Init", "MD5Update", "MD5Final", "nc_MD5Init", "nc_MD5Update", "nc
            "md5hip_final_ctx", "md5hip_pool_set_split", "md5hip_pool_submit_async",
            "md5hip_pool_submit_iov_async", "md5hip_pool_wait", "md5hip_pool_poll",
            "md5hip_pool_get_stats", "md5hip_pool_device_stats", "md5_batch_submit_device_on",
-           "md5_batch_submit_device_after", "md5hip_plan_desc_at"]
+           "md5_batch_submit_device_after", "md5hip_plan_desc_at", "md5hip_batcher_set_chain"]
 
 
 def check(fn, rc):

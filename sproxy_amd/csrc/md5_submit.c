@@ -229,6 +229,12 @@ struct slot {
     pthread_cond_t cv;
     uint32_t nwait;
     int watch;
+    /* chained launch: its hash kernel waits on the last launch's event
+     * (device-side order), so it starts the moment that one ends instead of
+     * after the host has seen it end and enqueued it (~1.3 ms per C3 step,
+     * profiles/r04b/c3q_gaps.json); chain_at = when it should start */
+    hipEvent_t chain_ev;
+    uint64_t chain_at;
 };
 enum { WATCH_NONE = 0, WATCH_ACTIVE, WATCH_GAVE_UP };
 
@@ -258,10 +264,16 @@ struct md5hip_batcher {
     pthread_t progress;
     int progress_started, stop;
     int poll_fast;            /* the progress thread polls launches every 10 us now */
+    int chain;                /* chain the open slot behind the running launch (default 1) */
     hipEvent_t after_ev;     /* recorded on a producer's stream (md5_batch_submit_device_on) */
 };
 
 #define CK(x) do { if ((x) != hipSuccess) { rc = -ENODEV; goto fail; } } while (0)
+
+/* the earliest a slot is chained behind the running launch: this long
+ * before that launch's expected end (at most; a quarter of a launch for
+ * short ones), so late submissions still coalesce into it */
+#define CHAIN_LEAD_MAX_US 2000.0
 
 static uint64_t now_us(void)
 {
@@ -383,6 +395,7 @@ static int slot_enqueue(md5hip_batcher *b, struct slot *sl)
     if (sl->mode == MODE_FIXED) {
         if (hipMemcpyAsync(sl->d_data, sl->fx_src, sl->fx_bytes, hipMemcpyHostToDevice, sl->stream))
             return -EIO;
+        if (sl->chain_ev && hipStreamWaitEvent(sl->stream, sl->chain_ev, 0) != hipSuccess) return -EIO;
         rc = sl->kind == MD5HIP_DIGEST_CRC32
                  ? crc32hip_fixed(sl->d_data, n, sl->fx_len, sl->fx_stride, sl->fastcrc,
                                   (uint32_t *)sl->d_dig, sl->stream)
@@ -423,6 +436,9 @@ static int slot_enqueue(md5hip_batcher *b, struct slot *sl)
             dst = g0->user;
             sl->direct = 1;
         }
+        /* a chained launch: bytes in and plan made beside the running
+         * launch, the hash kernel after it */
+        if (sl->chain_ev && hipStreamWaitEvent(sl->stream, sl->chain_ev, 0) != hipSuccess) return -EIO;
         const uint32_t *ord = sl->use_order ? sl->d_ord : NULL;
         const uint64_t *doff = sl->desc_direct ? sl->dh_off : sl->d_off;
         const uint32_t *dlen = sl->desc_direct ? sl->dh_len : sl->d_len;
@@ -464,6 +480,8 @@ static void slot_reset(struct slot *sl)
 {
     sl->state = SLOT_FREE;
     sl->watch = WATCH_NONE;
+    sl->chain_ev = NULL;
+    sl->chain_at = 0;
     sl->mode = MODE_NONE;
     sl->writers = sl->full = sl->flush = sl->err = sl->direct = 0;
     sl->n = sl->used = sl->nseg = sl->ndma = sl->ndsc = 0;
@@ -492,7 +510,8 @@ static void slot_retire(md5hip_batcher *b, struct slot *sl, int err)
     sl->load = 0;
     if (sl->state == SLOT_INFLIGHT) {
         b->inflight--;
-        const double d = (double)(now_us() - sl->launched_us);
+        const uint64_t t = now_us();               /* a chained launch's start is estimated */
+        const double d = t > sl->launched_us ? (double)(t - sl->launched_us) : 0.0;
         b->launch_ema_us = b->launch_ema_us > 0 ? 0.75 * b->launch_ema_us + 0.25 * d : d;
     }
     slot_reset(sl);
@@ -513,7 +532,7 @@ static void slot_try_launch(md5hip_batcher *b, struct slot *sl)
         slot_retire(b, sl, sl->err);
         return;
     }
-    if (!(sl->full || sl->flush || b->inflight < b->target)) return;
+    if (!(sl->full || sl->flush || sl->chain_ev || b->inflight < b->target)) return;
     if (!sl->full && !sl->flush && b->inflight == 0 && now_us() - sl->opened_us < linger_us(b)) {
         pthread_cond_broadcast(&b->work_cv);        /* the progress thread times the linger */
         return;
@@ -526,6 +545,7 @@ static void slot_try_launch(md5hip_batcher *b, struct slot *sl)
     }
     sl->state = SLOT_INFLIGHT;
     sl->launched_us = now_us();
+    if (sl->chain_ev && sl->chain_at > sl->launched_us) sl->launched_us = sl->chain_at;   /* its real start */
     sl->gen++;
     b->inflight++;
     b->st.launches++;
@@ -652,6 +672,28 @@ static void *progress_main(void *arg)
                     }
                     o->seen_n = o->n;
                 }
+                /* planned and quiet, the pipeline at its target, and the last
+                 * launch due to end within min(2 ms, a quarter of a launch):
+                 * chain it there (its kernel waits on that launch's event).
+                 * Not behind a launch overdue by more than that: its end is
+                 * unknown, and the open slot keeps coalescing until it retires */
+                if (b->chain && o->state == SLOT_OPEN && o->n && !o->writers && !o->err && !o->chain_ev &&
+                    o->mode != MODE_FIXED && o->planned_n == o->n && b->inflight == b->target &&
+                    b->launch_ema_us > 0) {
+                    struct slot *last = NULL;
+                    for (uint32_t k = 0; k < b->nslots; k++)
+                        if (b->s[k].state == SLOT_INFLIGHT && (!last || b->s[k].launched_us > last->launched_us))
+                            last = &b->s[k];
+                    const double lead = b->launch_ema_us / 4 < CHAIN_LEAD_MAX_US ? b->launch_ema_us / 4
+                                                                                 : CHAIN_LEAD_MAX_US;
+                    const uint64_t end = last ? last->launched_us + (uint64_t)b->launch_ema_us : 0;
+                    const uint64_t now = now_us();
+                    if (last && (double)now + lead >= (double)end && (double)now <= (double)end + lead) {
+                        o->chain_ev = last->done;
+                        o->chain_at = end > now ? end : now;
+                        slot_try_launch(b, o);
+                    }
+                }
             }
             /* poll interval: 20 -> 200 us while nobody waits; blocked callers
              * pin it at 10 us (a short launch is not delivered up to 200 us
@@ -735,9 +777,11 @@ static void watch_launch(md5hip_batcher *b, struct slot *sl)
 }
 
 /* Block until ticket t is complete (mu held on entry and exit); its error.
- * flush: launch an open slot holding t at once (a synchronous submission);
- * else hasten it (md5_batch_wait: at once only while nothing is in flight). */
-static int wait_ticket(md5hip_batcher *b, uint64_t t, int flush)
+ * An open slot holding t is hastened: launched at once while nothing is in
+ * flight (no linger), else by the usual policy (md5_batch_wait's rule; a
+ * synchronous submission's too, so that callers arriving while the device is
+ * busy coalesce into one launch instead of one launch each). */
+static int wait_ticket(md5hip_batcher *b, uint64_t t)
 {
     int err = 0;
     while (!tk_done(b, t, &err)) {
@@ -746,7 +790,7 @@ static int wait_ticket(md5hip_batcher *b, uint64_t t, int flush)
             struct slot *sl = &b->s[k];
             if (sl->state == SLOT_FREE || !seg_has(sl, t)) continue;
             if (sl->state == SLOT_OPEN) {
-                if (flush || b->inflight == 0) sl->flush = 1;
+                if (b->inflight == 0) sl->flush = 1;
                 slot_try_launch(b, sl);
             }
             if (sl->state == SLOT_INFLIGHT && !in) in = sl;
@@ -852,6 +896,7 @@ static int batcher_new(int device, uint64_t slice_bytes, uint32_t nslots, uint64
     b->gather = MD5HIP_GATHER_AUTO;
     b->target = nslots > 2 ? 2 : 1;
     b->linger_max_us = 5000;
+    b->chain = 1;
     b->open = -1;
     b->s = calloc(nslots, sizeof *b->s);
     /* ticket 0 = "nothing": complete at once */
@@ -999,6 +1044,15 @@ int md5hip_batcher_set_linger(md5hip_batcher *b, uint32_t max_us)
     pthread_mutex_lock(&b->mu);
     b->linger_max_us = max_us;
     pthread_cond_broadcast(&b->work_cv);
+    pthread_mutex_unlock(&b->mu);
+    return 0;
+}
+
+int md5hip_batcher_set_chain(md5hip_batcher *b, int on)
+{
+    if (!b) return -EINVAL;
+    pthread_mutex_lock(&b->mu);
+    b->chain = on != 0;
     pthread_mutex_unlock(&b->mu);
     return 0;
 }
@@ -1369,13 +1423,18 @@ static int submit(md5hip_batcher *b, const struct chunk_src *src, uint64_t n, un
             sl->writers--;
         }
         i += m;
-        if (urgent && i >= n) sl->flush = 1;  /* the caller waits right away */
+        /* the caller waits right away: no linger on an idle device; on a
+         * busy one the slot keeps coalescing (it goes when fewer than
+         * `target` launches run, is chained behind the running one, or goes
+         * when that retires) -- forcing every synchronous call out at once
+         * made one launch per vector at ASIO scale (profiles/r04b/) */
+        if (urgent && i >= n && b->inflight == 0) sl->flush = 1;
         slot_try_launch(b, sl);
     }
     tk_put(b, t, rc);                        /* the submission's own reference */
     if (ticket) *ticket = t;
     if (!async || rc) {
-        const int err = wait_ticket(b, t, 1);        /* a synchronous caller: at once */
+        const int err = wait_ticket(b, t);
         if (!rc) rc = err;
     }
     pthread_mutex_unlock(&b->mu);
@@ -1409,7 +1468,7 @@ int md5_batch_wait(md5hip_batcher *b, uint64_t ticket)
     struct dev_guard g;
     if (dev_enter(&g, b->device)) return -ENODEV;
     pthread_mutex_lock(&b->mu);
-    const int rc = ticket >= b->tk.hi ? -EINVAL : wait_ticket(b, ticket, 0);
+    const int rc = ticket >= b->tk.hi ? -EINVAL : wait_ticket(b, ticket);
     pthread_mutex_unlock(&b->mu);
     dev_leave(&g);
     return rc;
@@ -1596,7 +1655,7 @@ static int host_fixed(md5hip_batcher *b, int kind, uint32_t fastcrc, const void 
     tk_put(b, t, rc);
     if (ticket) *ticket = t;
     if (!ticket || rc) {
-        const int err = wait_ticket(b, t, 1);
+        const int err = wait_ticket(b, t);
         if (!rc) rc = err;
     }
     pthread_mutex_unlock(&b->mu);

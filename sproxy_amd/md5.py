@@ -357,7 +357,8 @@ class Batcher:
                submit_device="md5_batch_submit_device", submit_device_on="md5_batch_submit_device_on",
                submit_device_after="md5_batch_submit_device_after",
                set_inflight="md5hip_batcher_set_inflight",
-               set_linger="md5hip_batcher_set_linger", stats="md5hip_batcher_get_stats")
+               set_linger="md5hip_batcher_set_linger", set_chain="md5hip_batcher_set_chain",
+               stats="md5hip_batcher_get_stats")
 
     def __init__(self, device: int = 0, slice_bytes: int = 0, nslots: int = 0,
                  kind: int = 0, fastcrc: int = 0):
@@ -561,6 +562,11 @@ class Batcher:
         """Idle pipeline: hold an async submission's slot up to
         min(max_us, 1/8 of recent launch time) for more work (0 = never)."""
         check(*self._call("set_linger", max_us))
+
+    def set_chain(self, on: bool):
+        """Chained launches (default on): the next slot's kernel queued behind
+        the running launch's event just before it ends."""
+        check(*self._call("set_chain", 1 if on else 0))
 
     def stats(self) -> dict:
         st = MD5HipBatcherStats()

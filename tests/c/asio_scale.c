@@ -203,8 +203,9 @@ int main(int argc, char **argv)
     const uint64_t slice = argc > 7 ? strtoull(argv[7], NULL, 0) << 20 : 0;
     const uint32_t nslots = argc > 8 ? (uint32_t)atoi(argv[8]) : 0;
     if (g_threads < 1 || g_threads > 1024 || g_blocks < 1 || g_len < 8000 || g_secs <= 0) return 2;
-    {   /* all threads' vectors span >= 2 GiB (cold sources) */
-        const double vec = (double)g_blocks * g_len, ws = 2.0 * (1u << 30);
+    {   /* all threads' vectors span >= 2 GiB (cold sources; ASIO_WS_MIB overrides) */
+        const char *e = getenv("ASIO_WS_MIB");
+        const double vec = (double)g_blocks * g_len, ws = (e ? atof(e) : 2048.0) * (1u << 20);
         g_nvec = (int)(ws / (vec * g_threads) + 0.999);
         if (g_nvec < 1) g_nvec = 1;
     }

@@ -290,6 +290,7 @@ static void *knobs(void *arg)
     while (!STOPPED()) {
         md5hip_batcher_set_inflight(g_b, 1 + (uint32_t)(rnd(&s) % 3));
         md5hip_batcher_set_linger(g_q, (uint32_t)(rnd(&s) % 400));
+        md5hip_batcher_set_chain(g_b, (int)(rnd(&s) & 1));
         md5hip_batcher_set_gather(g_b, (int)(rnd(&s) % 4));
         md5hip_pool_set_gather(g_pool, (int)(rnd(&s) % 4));
         md5hip_pool_set_split(g_pool, (rnd(&s) % 2) ? 0 : 256u << 10);
@@ -364,9 +365,16 @@ static int blocked_callers(int rounds)
 {
     int rc = md5hip_batcher_create(0, 4u << 20, 2, &g_w);      /* 2 slots: inflight target 1 */
     if (rc) { printf("FAIL waiter batcher %d\n", rc); return 1; }
+    /* the held launch outlives every estimate of its end: no chaining (the
+     * 64 tickets must stay in the open slot until it is released) */
+    if ((rc = md5hip_batcher_set_chain(g_w, 0))) { printf("FAIL set_chain %d\n", rc); return 1; }
     for (int r = 0; r < rounds; r++) {
+        struct md5hip_batcher_stats st;
+        md5hip_batcher_get_stats(g_w, &st);
+        const uint64_t launches0 = st.launches;
         __atomic_store_n(&fake_hip_hold, 1, __ATOMIC_RELAXED);
-        /* a held launch in flight, so the waiters' chunks coalesce in the open slot */
+        /* a held launch in flight, so the waiters' chunks coalesce in the open slot
+         * (which may be chained behind it before the release) */
         const void *bp = g_heap;
         uint32_t bl = 100;
         unsigned char bd[16];
@@ -385,9 +393,6 @@ static int blocked_callers(int rounds)
         pthread_barrier_wait(&g_wbar);
         struct timespec ts = {0, 20000000};            /* let them all block */
         nanosleep(&ts, NULL);
-        struct md5hip_batcher_stats st;
-        md5hip_batcher_get_stats(g_w, &st);
-        const uint64_t launches0 = st.launches;
         __atomic_store_n(&fake_hip_slow_query, r & 1, __ATOMIC_RELAXED);
         __atomic_store_n(&fake_hip_hold, 0, __ATOMIC_RELAXED);
         const double t0 = now();
@@ -402,8 +407,8 @@ static int blocked_callers(int rounds)
                 printf("FAIL waiter %d round %d: rc %d bad %d\n", t, r, jobs[t].rc, jobs[t].bad);
                 return 1;
             }
-        /* the 64 tickets went out together: one launch after the blocker */
-        if (st.launches != launches0 + 1 || st.max_tickets_per_launch < WT) {
+        /* the 64 tickets went out together: the blocker's launch and one more */
+        if (st.launches != launches0 + 2 || st.max_tickets_per_launch < WT) {
             printf("FAIL round %d: %llu launches for the waiters, max %llu tickets per launch\n", r,
                    (unsigned long long)(st.launches - launches0), (unsigned long long)st.max_tickets_per_launch);
             return 1;
