@@ -39,7 +39,8 @@ extern "C" {
 #define MD5HIP_ABI_VERSION 3
 
 /* Fixed-length kernels for md5hip_digest_fixed_variant.  ABI 2: the round-1
- * A/B variants (values 2-9) moved to the diagnostic library (md5_diag.hip);
+ * A/B variants (values 2-9) moved to the diagnostic library (removed in round 4;
+ * git history at 993ee7d, sproxy_amd/csrc/md5_diag.hip);
  * the library ships the default and one fallback, and no environment
  * variable re-routes a launch. */
 enum md5hip_variant {
@@ -83,7 +84,7 @@ enum md5hip_desc_variant {
     MD5HIP_DESC_AUTO = 0,   /* the default: XDMA */
     MD5HIP_DESC_LANE = 1,   /* each lane streams its own chunk (8-block register ring):
                                the planner's choice for small batches */
-    /* 2: the register-staged XPOSE loader, moved to the diagnostic library */
+    /* 2: the register-staged XPOSE loader, retired (round-1 A/B) */
     MD5HIP_DESC_HYBRID = 3, /* XDMA, but the first waves (one per CU) go lane-direct when
                                they hold a chunk >= 256 KiB (md5hip_plan_desc's choice for
                                batches whose longest chunks bound the launch) */
@@ -147,7 +148,7 @@ int md5hip_final_ctx(struct MD5Context *d_ctxs, uint64_t n, unsigned char *d_dig
 int crc32hip_fixed(const void *d_base, uint64_t n, uint32_t len, uint64_t stride,
                    uint32_t fastcrc, uint32_t *d_crcs, void *stream);
 /* CRC-32 kernels for crc32hip_fixed_variant (ABI 2: values 1-5, the round-1
- * A/B variants, moved to the diagnostic library). */
+ * A/B variants, retired; their measurements stay in profiles/). */
 enum crc32hip_variant {
     CRC32HIP_AUTO = 0,      /* the default: XDMA16 */
     CRC32HIP_XDMA16 = 6,    /* slicing-by-4 over 16 v_perm-addressed LDS table copies, 8 KiB

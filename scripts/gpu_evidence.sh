@@ -1,6 +1,7 @@
 #!/bin/bash
 # Round evidence in one call: full GPU parity suite, smoke, every bench config,
-# rocprofv3 kernel trace of the default bench command, PMC passes (HBM bytes).
+# rocprofv3 kernel trace of the default bench command, PMC passes (HBM bytes,
+# VALU busy; scripts/gpu_pmc_traffic.sh).
 cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out/ev
 export TMPDIR=/tmp
@@ -18,6 +19,6 @@ timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/pro
 echo "rocprof bench rc=$r"; tail -1 $O/prof_bench.log; ok $r || exit $r
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_crc -o crc -- python3 bench.py --config crc --no-cpu-baseline > $O/prof_crc.log 2>&1; r=$?
 echo "rocprof crc rc=$r"; ok $r || exit $r
-bash scripts/pmc_passes.sh $O/pmc --only ${PMC_ONLY:-xdma1nt,xpose1nt,crc_xdma16,compute_only,load_xpose1} > $O/pmc.log 2>&1; r=$?
+bash scripts/gpu_pmc_traffic.sh $O/pmc > $O/pmc.log 2>&1; r=$?
 echo "pmc rc=$r"; tail -3 $O/pmc.log
 find $O -name "*stats*.csv" | head

@@ -21,8 +21,7 @@ import torch
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
-sys.path.insert(0, os.path.join(REPO, "scripts", "diag"))
-from c3_trace_x import batch  # noqa: E402
+import bench  # noqa: E402
 from sproxy_amd import md5 as m  # noqa: E402
 
 vp, u64, ci = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int
@@ -34,6 +33,21 @@ def load(path):
     L.md5hip_init_ctx.argtypes = [vp, u64, vp]
     L.md5hip_digest_desc_variant.argtypes = [vp, vp, vp, vp, u64, vp, vp, ci]
     return L
+
+
+def batch(K, seed0):
+    """K C3 batches (bench.py's lengths) in one arena: (arena, lens, offsets,
+    longest-first order, planned variant)."""
+    lk = [bench.c3_lens(16 << 30, seed0 + 31 * j) for j in range(K)]
+    ok_ = [bench.c3_offsets(x)[0] for x in lk]
+    spans = [(bench.c3_offsets(x)[1] + 15) // 16 * 16 for x in lk]
+    starts = np.concatenate([[0], np.cumsum(spans)[:-1]])
+    big = m.arena_empty(int(sum(spans)))
+    m.fill_synthetic(big, seed=0xC3D)
+    L = np.concatenate(lk)
+    O = np.concatenate([o + s for o, s in zip(ok_, starts)])
+    order, var = m.plan_desc(L.astype(np.uint32))
+    return big, L, O, order, var
 
 
 def timed(f):

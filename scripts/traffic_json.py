@@ -10,7 +10,7 @@ usage: traffic_json.py FETCH_DIR WRITE_DIR WORKLOAD [--valu VALU_DIR] [--out pro
   config tag the bytes belong to (e.g. c2@1048576x16384).  VALU_DIR: a pass
   of SQ_ACTIVE_INST_VALU SQ_INSTS_VALU GRBM_GUI_ACTIVE (SURVEY §8(d) asks for
   VALUBusy beside the HBM roofline): valu_busy = SQ_ACTIVE_INST_VALU quad-
-  cycles over (1024 SIMDs x GRBM_GUI_ACTIVE / 8 XCDs / 4), as pmc_summary.py.
+  cycles over (1024 SIMDs x GRBM_GUI_ACTIVE / 8 XCDs / 4).
 HBM bytes per launch (MI355X_MICROARCH.md HBM section, gfx950): read =
 2 x 1024 x FETCH_SIZE, write = 1024 x WRITE_SIZE, mean over the kernel's
 dispatches."""

@@ -175,7 +175,7 @@ __attribute__((visibility("hidden"))) int md5hip_crc_desc_choice(uint64_t n, uin
 // kCrcSplitMinWindow keep the window kernels whatever the variant says)
 
 // The shipped kernels are fixed: the round-1 A/B variants live in the
-// diagnostic library (md5_diag.hip, md5_kernels_ab.h), and no environment
+// diagnostic library (removed in round 4; git history at 993ee7d), and no environment
 // variable re-routes a product launch.
 int md5hip_resolve_variant(int v) { return v == MD5HIP_AUTO ? MD5HIP_XDMA1NT : v; }
 int crc32hip_resolve_variant(int v) { return v == CRC32HIP_AUTO ? CRC32HIP_XDMA16 : v; }
