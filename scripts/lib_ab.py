@@ -84,8 +84,11 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rounds", type=int, default=9)
     ap.add_argument("--extra", nargs="*", default=[], help="name=path of more builds to compare")
+    ap.add_argument("--old", default="build/ab/libmd5hip_old.so", help="the baseline build")
+    ap.add_argument("--only", default="", help="comma list of workloads (ctx,ragged16,c3k3_balanced,c3k6_balanced,c3_hybrid)")
     a = ap.parse_args()
-    libs = {"old": load(os.path.join(REPO, "build", "ab", "libmd5hip_old.so"))}
+    only = set(a.only.split(",")) if a.only else None
+    libs = {"old": load(os.path.join(REPO, a.old))}
     for extra in a.extra:               # name=path, between old and new
         k, v = extra.split("=", 1)
         libs[k] = load(os.path.join(REPO, v))
@@ -94,6 +97,18 @@ def main():
     res = {}
 
     # ctx: 1 M contexts x 16 KiB (one update launch; contexts re-initialised per run)
+    if only is None or "ctx" in only:
+        ctx_ab(libs, st, res, a.rounds)
+    if only is None or "ragged16" in only:
+        ragged_ab(libs, st, res, a.rounds)
+    for K, name, var in ((3, "c3k3_balanced", 5), (6, "c3k6_balanced", 5), (1, "c3_hybrid", 3)):
+        if only is None or name in only:
+            c3_ab(libs, st, res, a.rounds, K, name, var)
+    print(json.dumps(res))
+
+
+def ctx_ab(libs, st, res, rounds):
+    """1 M contexts x 16 KiB (one update launch; contexts re-initialised per run)"""
     n, L = 1 << 20, 16384
     data = torch.empty(n * L, dtype=torch.uint8, device="cuda")
     m.fill_synthetic(data, seed=0xC7)
@@ -104,12 +119,14 @@ def main():
     def run_ctx(Lb):
         rc = Lb.md5hip_init_ctx(ctx.data_ptr(), n, st)
         return rc or Lb.md5hip_update_ctx(ctx.data_ptr(), ptrs.data_ptr(), lens.data_ptr(), n, st)
-    res["ctx"] = ab(libs, run_ctx, lambda: ctx, a.rounds)
+    res["ctx"] = ab(libs, run_ctx, lambda: ctx, rounds)
     print(json.dumps({"ctx": res["ctx"]}), flush=True)
     del data, ctx, ptrs, lens
     torch.cuda.empty_cache()
 
-    # ragged netcache blocks packed at 16 B (descriptor XDMA)
+
+def ragged_ab(libs, st, res, rounds):
+    """ragged netcache blocks packed at 16 B (descriptor XDMA)"""
     rng = np.random.default_rng(5)
     S, nb = 16384, 983040                       # ~15 GiB
     bl = np.full(nb, S, dtype=np.int64)
@@ -125,37 +142,28 @@ def main():
     dig = torch.empty((nb, 16), dtype=torch.uint8, device="cuda")
     run_r = lambda Lb: Lb.md5hip_digest_desc_variant(arena.data_ptr(), dO.data_ptr(), dL.data_ptr(),  # noqa
                                                      dR.data_ptr(), nb, dig.data_ptr(), st, 4)
-    res["ragged16"] = ab(libs, run_r, lambda: dig, a.rounds)
+    res["ragged16"] = ab(libs, run_r, lambda: dig, rounds)
     print(json.dumps({"ragged16": res["ragged16"]}), flush=True)
     del arena, dO, dL, dR, dig
     torch.cuda.empty_cache()
 
-    # 3 coalesced C3 batches, BALANCED
-    big, Lk, O, order, var = batch(3, 1000)
+
+def c3_ab(libs, st, res, rounds, K, name, var):
+    """K coalesced C3 batches (bench.py's lengths) launched with `var`
+    (5 = BALANCED, the queue's choice for coalesced batches; 3 = HYBRID for one)"""
+    big, Lk, O, order, _ = batch(K, 1000)
     nk = Lk.size
     dO = torch.from_numpy(O).cuda()
     dL = torch.from_numpy(Lk.astype(np.int32)).cuda()
     dR = torch.from_numpy(order.astype(np.int32)).cuda()
     dig = torch.empty((nk, 16), dtype=torch.uint8, device="cuda")
     run_b = lambda Lb: Lb.md5hip_digest_desc_variant(big.data_ptr(), dO.data_ptr(), dL.data_ptr(),  # noqa
-                                                     dR.data_ptr(), nk, dig.data_ptr(), st, 5)
-    res["c3k3_balanced"] = ab(libs, run_b, lambda: dig, a.rounds)
-    print(json.dumps({"c3k3_balanced": res["c3k3_balanced"]}), flush=True)
+                                                     dR.data_ptr(), nk, dig.data_ptr(), st, var)
+    res[name] = ab(libs, run_b, lambda: dig, rounds)
+    res[name]["payload_bytes"] = int(Lk.sum())
+    print(json.dumps({name: res[name]}), flush=True)
     del big, dO, dL, dR, dig
     torch.cuda.empty_cache()
-
-    # the single C3 batch, HYBRID (its short-chunk waves use the same loader)
-    big, Lk, O, order, var = batch(1, 1000)
-    nk = Lk.size
-    dO = torch.from_numpy(O).cuda()
-    dL = torch.from_numpy(Lk.astype(np.int32)).cuda()
-    dR = torch.from_numpy(order.astype(np.int32)).cuda()
-    dig = torch.empty((nk, 16), dtype=torch.uint8, device="cuda")
-    run_h = lambda Lb: Lb.md5hip_digest_desc_variant(big.data_ptr(), dO.data_ptr(), dL.data_ptr(),  # noqa
-                                                     dR.data_ptr(), nk, dig.data_ptr(), st, 3)
-    res["c3_hybrid"] = ab(libs, run_h, lambda: dig, a.rounds)
-    print(json.dumps({"c3_hybrid": res["c3_hybrid"]}), flush=True)
-    print(json.dumps(res))
 
 
 if __name__ == "__main__":

@@ -2,7 +2,7 @@
 # Round-4 call C: synchronous submits coalesce on a busy device, chained
 # launches.  The whole GPU suite; the call site at ASIO scale; c3q with
 # chaining on and off (interleaved) and its launch gaps; the single-caller
-# queue latency.
+# queue latency; BALANCED with two images (A/B build build/abr04/bal2).
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
 O=gpurun_out/r04c
@@ -19,4 +19,5 @@ done
 timeout -s KILL 200 rocprofv3 --kernel-trace --output-format csv -d $O/c3q_trace -o trace -- python3 bench.py --config c3q --steps 10 --no-cpu-baseline > $O/c3q_traced.json 2> $O/c3q_traced.err || { echo "c3q traced failed"; exit 1; }
 python3 scripts/queue_gaps.py $O/c3q_trace > $O/c3q_gaps.json 2>&1
 timeout -k 10 200 python3 scripts/latency_probe.py --iters 200 > $O/queue_latency.json 2> $O/queue_latency.err || { echo "latency probe failed"; exit 1; }
+timeout -k 10 300 python3 -u scripts/lib_ab.py --rounds 9 --old sproxy_amd/lib/libmd5hip.so --extra bal2=build/abr04/bal2/libmd5hip.so --only c3k3_balanced,c3k6_balanced > $O/balanced_ab.log 2>&1 || { echo "balanced A/B failed"; tail -3 $O/balanced_ab.log; exit 1; }
 echo done

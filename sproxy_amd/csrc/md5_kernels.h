@@ -609,6 +609,92 @@ __device__ __forceinline__ void desc_xpose_group(H& h, const uint8_t* __restrict
       };
       if (CP == 0 || !lined) run(std::integral_constant<int, 0>{});
       else run(std::integral_constant<int, CP>{});
+    } else if constexpr (kDma && NB == 2 && W == 1) {
+      // Two 8 KiB images for a LONE wave on its SIMD (BALANCED): a lone
+      // wave issues one instruction per slot, so everything it does besides
+      // VALU comes straight off its chain.  Per 128-B stage: the next stage's
+      // DMA goes into the other image BEFORE this stage's rows are read (so
+      // the ds_read latency is spent issuing it, not waiting), block 0 starts
+      // as soon as its four rows are in (lgkmcnt(4)), and the DMA's LDS base
+      // is set twice per stage, not eight times: rows 0-3 / 4-7 take M0 =
+      // image / image + 4 KiB and their 1 KiB row offset in the instruction
+      // (which adds it to the global address too, so the row pointers are
+      // pre-biased by it).  The DMA lead stays one stage, as with one image.
+      static_assert(D == 1 && !kHalf, "LDS-DMA images: full 8 KiB stages");
+      const bool lined = __ballot(((uint32_t)(uintptr_t)chunk & 127u) != 0 && live && nst != 0) == 0;
+      const uint32_t rmin = wave_min(nst ? nst : smax) - 1u;
+      auto* limg = (__attribute__((address_space(3))) uint8_t*)img;
+      const uint8_t* bptr[8];
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        bptr[r] = rptr[r] - (r & 3) * 1024;
+        asm volatile("" : "+v"(bptr[r]));      // keep the bias in the pointer (not re-added per stage)
+      }
+      auto run2 = [&](auto pol) __attribute__((always_inline)) {
+        constexpr int P = decltype(pol)::value;
+        // row R's DMA (the offset must be an immediate: R is a template constant)
+        auto dma = [&](auto R, const uint8_t* g, __attribute__((address_space(3))) uint8_t* im)
+            __attribute__((always_inline)) {
+          constexpr int r = decltype(R)::value;
+          __builtin_amdgcn_global_load_lds(g, im + (r >> 2) * 4096, 16, (r & 3) * 1024, P);
+        };
+        // stage stg into image B (a template constant: the image bases fold
+        // into M0 values and ds_read offsets, no address arithmetic per stage)
+        auto issue = [&](uint32_t stg, auto B) __attribute__((always_inline)) {
+          auto* im = limg + decltype(B)::value * 8192u;
+          auto rows = [&](auto... R) __attribute__((always_inline)) {
+            if (stg <= rmin) {                                 // wave-uniform, no row clamped
+              const uint64_t so = (uint64_t)stg << 7;
+              (dma(R, bptr[decltype(R)::value] + so, im), ...);
+            } else {
+              (dma(R, bptr[decltype(R)::value] + (min(stg, rlast[decltype(R)::value]) << 7), im), ...);
+            }
+          };
+          rows(std::integral_constant<int, 0>{}, std::integral_constant<int, 1>{},
+               std::integral_constant<int, 2>{}, std::integral_constant<int, 3>{},
+               std::integral_constant<int, 4>{}, std::integral_constant<int, 5>{},
+               std::integral_constant<int, 6>{}, std::integral_constant<int, 7>{});
+        };
+        using I0 = std::integral_constant<int, 0>;
+        using I1 = std::integral_constant<int, 1>;
+        // this lane's 8 row-piece addresses in image 0, kept in VGPRs: image
+        // 1's are the same + 8192, an immediate of the ds_read
+        using lds_u4 = const __attribute__((address_space(3))) u32x4;
+        uint32_t raddr[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          raddr[q] = (uint32_t)(uintptr_t)(limg + (myrow - img) + ((q ^ g) * 16));
+          asm volatile("" : "+v"(raddr[q]));
+        }
+        // one stage held in image B; the next goes into the other one
+        auto stage = [&](uint32_t stg, auto B) __attribute__((always_inline)) {
+          constexpr int b = decltype(B)::value;
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");      // stage stg landed (the only one out)
+          uint4 w[2][4];
+#pragma unroll
+          for (int q = 0; q < 8; ++q) {
+            const u32x4 v = *reinterpret_cast<lds_u4*>(raddr[q] + b * 8192u);
+            w[q >> 2][q & 3] = make_uint4(v.x, v.y, v.z, v.w);
+          }
+          if (stg + 1 < smax) {                                  // issued under the reads' latency
+            if constexpr (b == 0) issue(stg + 1, I1{});
+            else issue(stg + 1, I0{});
+          }
+          asm volatile("s_waitcnt lgkmcnt(4)" ::: "memory");   // block 0's rows
+          __builtin_amdgcn_sched_barrier(0);
+          if (stg < nst) h.block(st, w[0]);
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          __builtin_amdgcn_sched_barrier(0);
+          if (stg < nst) h.block(st, w[1]);
+        };
+        issue(0, I0{});
+        for (uint32_t stg = 0; stg < smax; stg += 2) {
+          stage(stg, I0{});
+          if (stg + 1 < smax) stage(stg + 1, I1{});
+        }
+      };
+      if (CP == 0 || !lined) run2(std::integral_constant<int, 0>{});
+      else run2(std::integral_constant<int, CP>{});
     } else if constexpr (kDma && (NB == 2 || W > 1)) {
       static_assert(D == 1 && !kHalf && (NB == 1 || NB == 2), "LDS-DMA images: full 8 KiB stages");
       const uint32_t nws = (smax + W - 1) / W;              // wide stages
@@ -1254,13 +1340,16 @@ __device__ __forceinline__ uint32_t balanced_body(const uint8_t* __restrict__ ba
 // five coalesced batches.  Wider stages (W x 128 B per visit), two buffers,
 // 8 waves per CU and split long/short queues measured no better.
 constexpr int kBalancedWaves = 4;
-constexpr int kBalancedImages = 1;
+#ifndef MD5HIP_BALANCED_IMAGES          // A/B builds only (scripts/lib_ab.py); the product sets it here
+#define MD5HIP_BALANCED_IMAGES 1
+#endif
+constexpr int kBalancedImages = MD5HIP_BALANCED_IMAGES;
 constexpr int kBalancedWide = 1;
 constexpr bool kBalancedSplit = false;
 constexpr int kBalancedPolicy = 2;   // nt for line-aligned groups only (desc_xpose_group)
 
 template <int WPB, int NB, bool kSplit, int W, int CP>
-__global__ void __launch_bounds__(64 * WPB)
+__global__ void __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(1, WPB / 4)))
 md5_desc_balanced_t(const uint8_t* __restrict__ base, const uint64_t* __restrict__ offs,
                     const uint32_t* __restrict__ lens, const uint32_t* __restrict__ order, uint64_t n,
                     uint4* __restrict__ out, uint32_t* __restrict__ ctr) {
