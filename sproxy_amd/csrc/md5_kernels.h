@@ -1328,8 +1328,8 @@ __device__ __forceinline__ uint32_t balanced_body(const uint8_t* __restrict__ ba
 }
 
 // the product's shape (profiles/r02_c3_balanced_ab.json,
-// r02_c3_wide_ab.json, r02_c3_cache_policy_ab.json): one wave per SIMD, one
-// 8 KiB image of 128-B stages, one queue, the DEFAULT cache policy for any
+// r02_c3_wide_ab.json, r02_c3_cache_policy_ab.json): one wave per SIMD, two
+// 8 KiB images of 128-B stages (round 4, below), one queue, the DEFAULT cache policy for any
 // group with a chunk off the 128-B line (nt only for line-aligned groups,
 // as every LDS-DMA loader here).  A C3 chunk
 // starts 16-B aligned, so each 128-B stage straddles two lines and shares one
@@ -1337,13 +1337,14 @@ __device__ __forceinline__ uint32_t balanced_body(const uint8_t* __restrict__ ba
 // are line-aligned) that line left L2 before the next stage came, and HBM
 // bytes ran 1.21-1.7x the payload, capping the loads alone at 3.9 TB/s.  The
 // default policy keeps it: 1.005x, the same kernel 22.1 -> 16.1-16.7 ms on
-// five coalesced batches.  Wider stages (W x 128 B per visit), two buffers,
-// 8 waves per CU and split long/short queues measured no better.
+// five coalesced batches.  Wider stages (W x 128 B per visit), two buffers
+// filled the round-2 way (DMA after the reads), 8 waves per CU and split
+// long/short queues measured no better.
 constexpr int kBalancedWaves = 4;
-#ifndef MD5HIP_BALANCED_IMAGES          // A/B builds only (scripts/lib_ab.py); the product sets it here
-#define MD5HIP_BALANCED_IMAGES 1
-#endif
-constexpr int kBalancedImages = MD5HIP_BALANCED_IMAGES;
+// two images: the lone wave's next DMA issued under its row reads, the LDS
+// base set twice per stage (round 4: 0.8-1.7 % faster on 3 and 6 coalesced
+// C3 batches, profiles/r04c/balanced_ab.json)
+constexpr int kBalancedImages = 2;
 constexpr int kBalancedWide = 1;
 constexpr bool kBalancedSplit = false;
 constexpr int kBalancedPolicy = 2;   // nt for line-aligned groups only (desc_xpose_group)

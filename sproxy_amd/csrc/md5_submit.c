@@ -177,6 +177,8 @@ struct seg {
 struct slot {
     hipStream_t stream;
     hipEvent_t done;
+    hipEvent_t kdone;                 /* right after the hash kernel: what a chained launch waits on
+                                         (the digest scatter / D2H behind it need not) */
     unsigned char *h_data, *d_data;   /* staging, `cap` bytes */
     uint64_t *h_off, *d_off;          /* descriptors, `maxn` entries */
     uint32_t *h_len, *d_len;
@@ -401,6 +403,7 @@ static int slot_enqueue(md5hip_batcher *b, struct slot *sl)
                                   (uint32_t *)sl->d_dig, sl->stream)
                  : md5hip_digest_fixed(sl->d_data, n, sl->fx_len, sl->fx_stride, sl->d_dig, sl->stream);
         if (rc) return rc;
+        if (hipEventRecord(sl->kdone, sl->stream)) return -EIO;
     } else {
         if ((rc = slot_prepare(b, sl))) return rc;
         const int dvar = sl->plan_var;
@@ -451,6 +454,7 @@ static int slot_enqueue(md5hip_batcher *b, struct slot *sl)
                  : md5hip_digest_desc_variant(sl->d_data, doff, dlen, ord, n,
                                               dst, sl->stream, dvar);
         if (rc) return rc;
+        if (hipEventRecord(sl->kdone, sl->stream)) return -EIO;
     }
     /* digests out: one D2H for the host segments, one scatter for the device ones */
     int any_host = 0;
@@ -689,7 +693,7 @@ static void *progress_main(void *arg)
                     const uint64_t end = last ? last->launched_us + (uint64_t)b->launch_ema_us : 0;
                     const uint64_t now = now_us();
                     if (last && (double)now + lead >= (double)end && (double)now <= (double)end + lead) {
-                        o->chain_ev = last->done;
+                        o->chain_ev = last->kdone;
                         o->chain_at = end > now ? end : now;
                         slot_try_launch(b, o);
                     }
@@ -825,6 +829,7 @@ static void batcher_free(md5hip_batcher *b)
         if (sl->state == SLOT_INFLIGHT) hipEventSynchronize(sl->done);
         if (sl->stream) hipStreamDestroy(sl->stream);
         if (sl->done) hipEventDestroy(sl->done);
+        if (sl->kdone) hipEventDestroy(sl->kdone);
         hipHostFree(sl->h_data); hipHostFree(sl->h_off); hipHostFree(sl->h_len);
         hipHostFree(sl->h_ord); hipHostFree(sl->h_dig);
         hipFree(sl->d_data); hipFree(sl->d_off); hipFree(sl->d_len);
@@ -907,6 +912,7 @@ static int batcher_new(int device, uint64_t slice_bytes, uint32_t nslots, uint64
         struct slot *sl = &b->s[k];
         CK(hipStreamCreateWithFlags(&sl->stream, hipStreamNonBlocking));
         CK(hipEventCreateWithFlags(&sl->done, hipEventDisableTiming));
+        CK(hipEventCreateWithFlags(&sl->kdone, hipEventDisableTiming));
         CK(hipHostMalloc((void **)&sl->h_data, b->cap, hipHostMallocDefault));
         /* fine-grained: a small slot's kernel reads them in place (slot_prepare) */
         CK(hipHostMalloc((void **)&sl->h_off, 8 * b->maxn, hipHostMallocCoherent));

@@ -193,6 +193,7 @@ int md5hip_digest_desc_variant(const void *d_base, const uint64_t *d_offsets, co
     if (((uintptr_t)d_digests & 15u) != 0) return -EINVAL;
     for (uint64_t k = 0; k < n; k++)
         if (d_lens[k] == fake_hip_fail_len) return -EIO;
+    if (getenv("FAKE_HIP_NOHASH")) return 0;         /* host-side cost probes: no digests */
     for (uint64_t k = 0; k < n; k++) {               /* lanes in `order`, digests by chunk */
         const uint64_t c = d_order ? d_order[k] : k;
         if (c >= n) return -EINVAL;
