@@ -9,7 +9,7 @@ One caller per in-flight launch polls its event; every other blocked caller
 sleeps on its slot and is woken by the retire (md5_submit.c wait_ticket /
 watch_launch), so the CPU a call costs must not grow with the number of
 callers: at 256 threads it stays within 1.5x of the 8-thread figure (the
-VERDICT r03 bound; measured figures in profiles/r04/asio_scale_threads.json).
+VERDICT r03 bound; measured figures in profiles/r04c/asio_threads.json).
 The CPU-only test checks that the probe fails loudly without a device."""
 import json
 import os
