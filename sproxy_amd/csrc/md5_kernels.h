@@ -1861,7 +1861,13 @@ md5_init_ctx(uint32_t* __restrict__ ctxs, uint64_t n) {  // md5.c:153-163 (in[] 
 // The longest-first order of a descriptor batch on the device (the batcher's
 // planner, md5_submit.c): a counting sort whose bucket starts the host took
 // from the histogram it keeps while chunks are reserved.  One atomic per
-// distinct key per wave: the lanes of one key take consecutive positions.
+// distinct key per wave (the lanes of one key take consecutive positions),
+// and all of a wave's atomics in ONE instruction: the key loop only finds
+// each lane's leader and rank (scalar reads and ballots), then the leaders
+// add at once and every lane reads its leader's base.  Waiting out one
+// returning atomic per distinct key instead took 138 us for a 472 K-chunk
+// burst of random lengths (~64 round trips per wave, profiles/r04b/
+// c3q_breakdown.json).
 // ---------------------------------------------------------------------------
 __global__ void __launch_bounds__(256)
 order_scatter(const uint32_t* __restrict__ lens, uint64_t n, uint32_t kmax,
@@ -1873,19 +1879,26 @@ order_scatter(const uint32_t* __restrict__ lens, uint64_t n, uint32_t kmax,
   // index before next[0]: such a chunk is left out of the order instead
   const bool live = i < n && k0 <= kmax;
   const uint32_t key = live ? k0 : 0u;
+  const uint64_t below = (1ull << lane) - 1ull;
+  uint32_t leader = 0, rank = 0, count = 0;
   uint64_t todo = __ballot(live);
   while (todo) {                                       // wave-uniform
-    const uint32_t leader = (uint32_t)__builtin_ctzll(todo);
-    const uint32_t lk = (uint32_t)__shfl((int)key, (int)leader, 64);
+    const uint32_t ld = (uint32_t)__builtin_ctzll(todo);
+    const uint32_t lk = (uint32_t)__builtin_amdgcn_readlane((int)key, (int)ld);
     const uint64_t same = __ballot(live && key == lk);
-    uint32_t base = 0;
-    if (lane == leader) base = atomicAdd(&next[kmax - lk], (uint32_t)__popcll(same));
-    base = (uint32_t)__shfl((int)base, (int)leader, 64);
     if (live && key == lk) {
-      const uint32_t pos = base + (uint32_t)__popcll(same & ((1ull << lane) - 1ull));
-      if (pos < n) order[pos] = (uint32_t)i;           // bound: a torn bucket table stays in range
+      leader = ld;
+      rank = (uint32_t)__popcll(same & below);
+      if (lane == ld) count = (uint32_t)__popcll(same);
     }
     todo &= ~same;
+  }
+  uint32_t base = 0;
+  if (count) base = atomicAdd(&next[kmax - key], count);   // leaders only
+  base = (uint32_t)__shfl((int)base, (int)leader, 64);
+  if (live) {
+    const uint32_t pos = base + rank;
+    if (pos < n) order[pos] = (uint32_t)i;             // bound: a torn bucket table stays in range
   }
 }
 

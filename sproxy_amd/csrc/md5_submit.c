@@ -456,16 +456,31 @@ static int slot_enqueue(md5hip_batcher *b, struct slot *sl)
         if (rc) return rc;
         if (hipEventRecord(sl->kdone, sl->stream)) return -EIO;
     }
-    /* digests out: one D2H for the host segments, one scatter for the device ones */
+    /* digests out: one D2H for the host segments, one scatter for the device
+     * ones.  The scatter kernel runs one workgroup per entry, so a long
+     * segment is cut into pieces of DSC_PIECE bytes as the table has room
+     * (6 tickets of 79 K digests as 6 entries took 145 us) */
+    enum { DSC_PIECE = 64 << 10 };
     int any_host = 0;
     sl->ndsc = 0;
+    uint64_t ndev = 0;
+    for (uint32_t k = 0; k < sl->nsegs && !sl->direct; k++) ndev += sl->segs[k].on_device;
+    uint64_t spare = b->segcap - ndev;                   /* nsegs < segcap (slot_open) */
     for (uint32_t k = 0; k < sl->nsegs && !sl->direct; k++) {
         const struct seg *g = &sl->segs[k];
         if (!g->on_device) { any_host = 1; continue; }
-        sl->h_dsc[sl->ndsc++] = (struct md5hip_seg){
-            (uint64_t)(uintptr_t)(sl->d_dig + (size_t)sl->dsz * g->first),
-            (uint64_t)((uintptr_t)g->user - (uintptr_t)sl->d_dig),     /* relative to d_dig (mod 2^64) */
-            (uint32_t)(sl->dsz * g->count), 0};
+        const uint64_t len = (uint64_t)sl->dsz * g->count;
+        uint64_t extra = (len + DSC_PIECE - 1) / DSC_PIECE - 1;
+        if (extra > spare) extra = spare;
+        spare -= extra;
+        const uint64_t piece = ((len + extra) / (extra + 1) + 15) & ~15ull;   /* 16-B multiples */
+        for (uint64_t at = 0; at < len; at += piece) {
+            const uint64_t l = len - at < piece ? len - at : piece;
+            sl->h_dsc[sl->ndsc++] = (struct md5hip_seg){
+                (uint64_t)(uintptr_t)(sl->d_dig + (size_t)sl->dsz * g->first + at),
+                (uint64_t)((uintptr_t)g->user + at - (uintptr_t)sl->d_dig),   /* relative to d_dig (mod 2^64) */
+                (uint32_t)l, 0};
+        }
     }
     if (sl->ndsc) {
         if (hipMemcpyAsync(sl->d_dsc, sl->h_dsc, sizeof(struct md5hip_seg) * sl->ndsc,
@@ -1204,9 +1219,11 @@ static void gather_range(const struct chunk_src *src, uint64_t first, uint64_t m
  * ------------------------------------------------------------------------ */
 /* Device-resident chunks [i, i + m) into slot `sl` (mu held, m fits): the
  * descriptors, payload and key histogram in one pass with the running
- * values in registers -- no bytes to stage, so a burst of C3 vectors
- * (~80 K chunks each) costs the device no idle time beyond this loop
- * (bench.py --config c3q `drained`). */
+ * values in registers -- no bytes to stage.  On the box's host this pass
+ * costs ~0.75 ns per chunk (0.36 ms for the 472 K chunks of a 6-vector c3q
+ * burst); cutting it over threads made it slower at every thread count,
+ * created per call or persistent-but-woken (scripts/probes/reserve_probe.c,
+ * profiles/r04f/reserve_probe_t*.json), so it stays on the calling thread. */
 static void reserve_device(md5hip_batcher *b, struct slot *sl, const struct chunk_src *src, uint64_t i,
                            uint64_t m)
 {

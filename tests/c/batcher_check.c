@@ -22,7 +22,9 @@
  * watcher's spin ends on NotReady just as the kernel finishes and the
  * progress thread retires the launch (fake_hip_slow_query) -- every waiter
  * must return with correct digests within the round's deadline (the lost
- * wake-up of round 3 hung here).  Exits 0 when every check holds.
+ * wake-up of round 3 hung here).  Then large_device(): large
+ * device-resident vectors, coalesced, with their device digests scattered
+ * in pieces.  Exits 0 when every check holds.
  */
 #include <errno.h>
 #include <pthread.h>
@@ -420,6 +422,65 @@ static int blocked_callers(int rounds)
     return 0;
 }
 
+/* ------------------------------------------------- large device submissions */
+/* Large device-resident vectors (reserve_device's one-pass descriptors and
+ * key histogram) and slots whose device digests go out through a scatter
+ * table cut into pieces: 3 coalesced asynchronous
+ * vectors of 40,000 chunks (random lengths, unsorted) plus one synchronous
+ * vector of 70,000, digests on the host and on the device (16-B aligned and
+ * not), every one checked.  The fake planner checks that the histogram
+ * counts every chunk. */
+static int large_device(void)
+{
+    enum { NV = 3, NA = 40000, NS = 70000 };
+    md5hip_batcher *q;
+    int rc = md5hip_queue_create(0, 4 * NA, 2, &q);
+    if (rc) { printf("FAIL large queue %d\n", rc); return 1; }
+    md5hip_batcher_set_chain(q, 0);
+    uint64_t s = 99;
+    uint64_t *dp = malloc(sizeof(uint64_t) * NS);
+    uint32_t *ln = malloc(sizeof(uint32_t) * NS);
+    int *idx = malloc(sizeof(int) * NS);
+    unsigned char *raw = malloc(16 * (size_t)NS * (NV + 1) + 32);
+    for (int round = 0; round < 2 && !rc; round++) {
+        for (int i = 0; i < NS; i++) {
+            idx[i] = (int)(rnd(&s) % NCH);
+            dp[i] = (uint64_t)(uintptr_t)(g_heap + g_offs[idx[i]]);
+            ln[i] = g_lens[idx[i]];
+        }
+        unsigned char *d = raw + (round ? 4 : 0);       /* device digests: scattered when odd */
+        uint64_t tk[NV], bt;
+        /* a held launch in flight, so the three vectors coalesce in the open slot */
+        __atomic_store_n(&fake_hip_hold, 1, __ATOMIC_RELAXED);
+        unsigned char bd[16];
+        rc = md5_batch_submit_device_async(q, dp, ln, 1, bd, 0, &bt);
+        if (!rc) rc = md5_batch_flush(q);
+        for (int v = 0; v < NV && !rc; v++)
+            rc = md5_batch_submit_device_async(q, dp + v * 1000, ln + v * 1000, NA, d + (size_t)16 * NA * v,
+                                               round, &tk[v]);
+        __atomic_store_n(&fake_hip_hold, 0, __ATOMIC_RELAXED);
+        if (!rc) rc = md5_batch_wait(q, bt);
+        for (int v = 0; v < NV && !rc; v++) rc = md5_batch_wait(q, tk[v]);
+        for (int v = 0; v < NV && !rc; v++)
+            if (!check_md5((unsigned char (*)[16])(d + (size_t)16 * NA * v), idx + v * 1000, NA)) rc = -4000 - v;
+        if (!rc) rc = md5_batch_submit_device(q, dp, ln, NS, d, round);
+        if (!rc && !check_md5((unsigned char (*)[16])d, idx, NS)) rc = -4100;
+    }
+    struct md5hip_batcher_stats st;
+    md5hip_batcher_get_stats(q, &st);
+    md5hip_batcher_destroy(q);
+    free(dp), free(ln), free(idx), free(raw);
+    if (rc) { printf("FAIL large device submissions %d\n", rc); return 1; }
+    if (st.max_tickets_per_launch < NV) {
+        printf("FAIL large device submissions: max %llu tickets per launch\n",
+               (unsigned long long)st.max_tickets_per_launch);
+        return 1;
+    }
+    printf("large device submissions ok: %llu launches, max %llu tickets per launch\n",
+           (unsigned long long)st.launches, (unsigned long long)st.max_tickets_per_launch);
+    return 0;
+}
+
 /* a hang is a failure, not a stuck test */
 static void *watchdog(void *arg)
 {
@@ -472,6 +533,7 @@ int main(int argc, char **argv)
     pthread_create(&wd, NULL, watchdog, &wd_secs);
     pthread_detach(wd);
     if (blocked_callers(12)) return 1;
+    if (large_device()) return 1;
     /* error paths, one thread: a chunk over the slice, a never-issued
      * ticket, a launch that fails (sync and async; the failure is kept for
      * a second wait and does not touch later submissions) */

@@ -256,6 +256,9 @@ int md5hip_plan_desc(const uint32_t *lens, uint64_t n, uint32_t *order)
 int md5hip_plan_hist(const uint32_t *hist, uint32_t kmax, uint64_t n, uint32_t *bucket_start)
 {
     if (!hist) return -EINVAL;
+    uint64_t sum = 0;                                 /* the batcher's histogram counts every chunk */
+    for (uint32_t k = 1; k <= kmax; k++) sum += hist[k];
+    if (sum != n) return -EBADMSG;
     if (bucket_start) {
         uint64_t at = 0;
         for (int64_t k = kmax; k >= 1; k--) {

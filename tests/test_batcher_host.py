@@ -13,7 +13,10 @@ and every copy or kernel must be enqueued from its stream's device (waits
 and polls on another device's ticket included).  First, 64 blocked callers
 wait on one slot for 12 rounds, every other round with the watcher's spin
 ending on NotReady just as the launch completes (the round-3 lost wake-up,
-which hangs that phase).  Runs under ASan+UBSan and under ThreadSanitizer
+which hangs that phase).  Then large device-resident vectors (md5_submit.c
+reserve_device), three coalesced in one slot with their device digests
+scattered in pieces; the fake planner rejects a histogram that misses a
+chunk.  Runs under ASan+UBSan and under ThreadSanitizer
 (which found the unlocked gather-mode read in submit(), now atomic)."""
 import os
 import shutil
@@ -43,6 +46,7 @@ def _build_and_run(name, san, env_extra, secs):
     assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-3000:]
     assert out.stdout.strip().endswith("batcher ok")
     assert "blocked callers: 12 rounds x 64 waiters on one slot ok" in out.stdout
+    assert "large device submissions ok" in out.stdout
 
 
 def test_batcher_under_asan():

@@ -721,9 +721,11 @@ def test_order_device_is_a_longest_first_permutation(cuda):
     from sproxy_amd import _lib
     L = _lib.lib()
     rng = np.random.default_rng(2024)
-    for n in (1, 63, 64, 1000, 200003):
+    for n in (1, 63, 64, 1000, 200003, 100001):
         lens = rng.integers(0, 300000, n).astype(np.uint32)
         lens[rng.integers(0, n, max(1, n // 10))] = 16384          # a popular key
+        if n == 100001:                                             # two keys, interleaved:
+            lens = np.where(rng.integers(0, 2, n) == 1, 4096, 65536).astype(np.uint32)   # one add per key per wave
         keys = (lens >> 6) + 1
         kmax = int(keys.max())
         hist = np.bincount(keys, minlength=kmax + 1).astype(np.uint32)
