@@ -5,9 +5,13 @@
  * preallocated histograms; parts handed to persistent helper threads.  The
  * destination is pinned coherent host memory (hipHostMallocCoherent) as in
  * the batcher, or plain malloc.  6 vectors of 79 K chunks of random C3-like
- * lengths (the c3q drained burst), median of 15 bursts.
+ * lengths (the c3q drained burst), median of 15 bursts.  Then one thread
+ * writing into 4 slot-sized pinned regions in turn, as the batcher's slots
+ * cycle (so the descriptor writes miss the caches), with ordinary and with
+ * non-temporal stores.
  * usage: reserve_probe [threads]   (prints one JSON line) */
 #include <hip/hip_runtime_api.h>
+#include <immintrin.h>
 #include <pthread.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -54,6 +58,32 @@ static void *run(void *arg)
             if (key > kmax) kmax = key;
         }
     }
+    p->pay = pay + (uint64_t)uns;
+    p->kmax = kmax;
+    return NULL;
+}
+
+static void *run_nt(void *arg)
+{
+    struct part *p = arg;
+    uint64_t pay = 0;
+    uint32_t kmax = 0, last = UINT32_MAX;
+    int uns = 0;
+    for (uint64_t k = 0; k < p->m; k++) {
+        const uint64_t q = p->dp[k];
+        const uint32_t L = p->ln[k];
+        _mm_stream_si64((long long *)&p->ho[k], (long long)(q - 4096));
+        _mm_stream_si32((int *)&p->hl[k], (int)L);
+        pay += L;
+        const uint32_t key = (L >> 6) + 1;
+        uns |= key > last;
+        last = key;
+        if (key <= KMAX) {
+            p->hh[key]++;
+            if (key > kmax) kmax = key;
+        }
+    }
+    _mm_sfence();
     p->pay = pay + (uint64_t)uns;
     p->kmax = kmax;
     return NULL;
@@ -161,6 +191,32 @@ int main(int argc, char **argv)
             qsort(ms, REPS, sizeof(double), cmp);
             printf("%s\"%s_%s\": %.3f", mem || how ? ", " : "", mem ? "malloc" : "pinned", names[how], ms[REPS / 2]);
         }
+    }
+    /* 4 slot regions of NV * M descriptors, cycled per burst */
+    uint64_t *cyc_o;
+    uint32_t *cyc_l;
+    if (hipHostMalloc((void **)&cyc_o, 8 * (size_t)M * NV * 4, hipHostMallocCoherent) ||
+        hipHostMalloc((void **)&cyc_l, 4 * (size_t)M * NV * 4, hipHostMallocCoherent)) {
+        printf("}}\n");
+        return 77;
+    }
+    memset(cyc_o, 0, 8 * (size_t)M * NV * 4);
+    memset(cyc_l, 0, 4 * (size_t)M * NV * 4);
+    for (int nt = 0; nt < 2; nt++) {
+        double ms[REPS];
+        for (int r = 0; r < REPS; r++) {
+            const size_t slot = (size_t)(r & 3) * M * NV;
+            const double t0 = now_ms();
+            for (int v = 0; v < NV; v++) {
+                struct part p = {dp, ln, cyc_o + slot + (size_t)v * M, cyc_l + slot + (size_t)v * M, hh, M, 0, 0};
+                if (nt) run_nt(&p);
+                else run(&p);
+            }
+            ms[r] = now_ms() - t0;
+            memset(hh, 0, 4 * (KMAX + 2));
+        }
+        qsort(ms, REPS, sizeof(double), cmp);
+        printf(", \"pinned_4slots_%s\": %.3f", nt ? "nt" : "wb", ms[REPS / 2]);
     }
     printf("}}\n");
     pthread_mutex_lock(&mu);

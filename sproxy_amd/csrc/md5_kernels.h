@@ -552,64 +552,7 @@ __device__ __forceinline__ void desc_xpose_group(H& h, const uint8_t* __restrict
         h.block(st, w[1]);
       }
     };
-    if constexpr (kDma && NB == 3) {
-      // Register-pipelined stages for a lone wave on its SIMD (BALANCED):
-      // three 8 KiB images; while stage s is compressed from registers, the
-      // rows of stage s+1 (landed) are already being read into the other
-      // register set and the DMA of stage s+3 goes into the image stage s
-      // left.  Neither the ds_read round trip nor a DMA shorter than two
-      // compressions is exposed.  Per wave: nt only for line-aligned groups,
-      // as the one-image path below.
-      static_assert(D == 1 && !kHalf && W == 1, "three full 8 KiB images");
-      const bool lined = __ballot(((uint32_t)off & 127u) != 0 && live && nst != 0) == 0;
-      auto run = [&](auto pol) __attribute__((always_inline)) {
-        constexpr int P = decltype(pol)::value;
-        auto issue = [&](uint32_t stg) __attribute__((always_inline)) {
-          uint8_t* im = img + (stg % 3u) * 8192u;
-#pragma unroll
-          for (int r = 0; r < 8; ++r)
-            __builtin_amdgcn_global_load_lds(rptr[r] + (min(stg, rlast[r]) << 7), im + r * 1024, 16, 0,
-                                             P);
-        };
-        auto rd = [&](uint32_t stg, uint4 (&w)[2][4]) __attribute__((always_inline)) {
-          const uint8_t* row = myrow + (stg % 3u) * 8192u;
-#pragma unroll
-          for (int q = 0; q < 8; ++q) {
-            const u32x4 v = *reinterpret_cast<const u32x4*>(row + ((q ^ g) * 16));
-            w[q >> 2][q & 3] = make_uint4(v.x, v.y, v.z, v.w);
-          }
-        };
-        uint4 wa[2][4], wb[2][4];
-        issue(0);
-        if (smax > 1) { issue(1); wait_vmcnt<8>(); } else { wait_vmcnt<0>(); }
-        rd(0, wa);
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        if (smax > 2) issue(2);
-        // one stage: `cur` holds stage stg; reads stage stg+1 into `nxt`
-        auto step = [&](uint32_t stg, uint4 (&cur)[2][4], uint4 (&nxt)[2][4])
-            __attribute__((always_inline)) {
-          if (stg + 1 < smax) {                              // wave-uniform
-            if (stg + 2 < smax) wait_vmcnt<8>();             // stage stg+1 in, stg+2 may fly
-            else wait_vmcnt<0>();
-            rd(stg + 1, nxt);
-            // stage stg's reads (one compression ago) are done; stg+1's may fly
-            asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory");
-            if (stg + 3 < smax) issue(stg + 3);              // into the image stg left
-          }
-          __builtin_amdgcn_sched_barrier(0);
-          if (stg < nst) {
-            h.block(st, cur[0]);
-            h.block(st, cur[1]);
-          }
-        };
-        for (uint32_t stg = 0; stg < smax; stg += 2) {
-          step(stg, wa, wb);
-          if (stg + 1 < smax) step(stg + 1, wb, wa);
-        }
-      };
-      if (CP == 0 || !lined) run(std::integral_constant<int, 0>{});
-      else run(std::integral_constant<int, CP>{});
-    } else if constexpr (kDma && NB == 2 && W == 1) {
+    if constexpr (kDma && NB == 2 && W == 1) {
       // Two 8 KiB images for a LONE wave on its SIMD (BALANCED): a lone
       // wave issues one instruction per slot, so everything it does besides
       // VALU comes straight off its chain.  Per 128-B stage: the next stage's
@@ -619,7 +562,10 @@ __device__ __forceinline__ void desc_xpose_group(H& h, const uint8_t* __restrict
       // is set twice per stage, not eight times: rows 0-3 / 4-7 take M0 =
       // image / image + 4 KiB and their 1 KiB row offset in the instruction
       // (which adds it to the global address too, so the row pointers are
-      // pre-biased by it).  The DMA lead stays one stage, as with one image.
+      // pre-biased by it).  The DMA lead stays one stage, as with one image:
+      // a third image for a two-stage lead (the 96 KiB a CU already reserves
+      // for BALANCED) measured 1.0-1.4 % slower on 3 and 6 coalesced C3
+      // batches (profiles/r04h/balanced3_ab.json).
       static_assert(D == 1 && !kHalf, "LDS-DMA images: full 8 KiB stages");
       const bool lined = __ballot(((uint32_t)(uintptr_t)chunk & 127u) != 0 && live && nst != 0) == 0;
       const uint32_t rmin = wave_min(nst ? nst : smax) - 1u;

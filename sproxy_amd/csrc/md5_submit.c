@@ -1219,11 +1219,14 @@ static void gather_range(const struct chunk_src *src, uint64_t first, uint64_t m
  * ------------------------------------------------------------------------ */
 /* Device-resident chunks [i, i + m) into slot `sl` (mu held, m fits): the
  * descriptors, payload and key histogram in one pass with the running
- * values in registers -- no bytes to stage.  On the box's host this pass
- * costs ~0.75 ns per chunk (0.36 ms for the 472 K chunks of a 6-vector c3q
- * burst); cutting it over threads made it slower at every thread count,
- * created per call or persistent-but-woken (scripts/probes/reserve_probe.c,
- * profiles/r04f/reserve_probe_t*.json), so it stays on the calling thread. */
+ * values in registers -- no bytes to stage.  While a burst of C3 vectors is
+ * submitted to an idle queue this pass is the device's idle time (bench.py
+ * --config c3q `drained`): ~97 us of a 79 K-chunk vector's submission on
+ * the box's host, the rest of the call ~3 us of HIP calls (rocprofv3
+ * --hip-trace, profiles/r04k/).  Neither threads (slower at every count,
+ * profiles/r04f/) nor non-temporal stores (2.4x in isolation,
+ * profiles/r04i/, no change in the submission, profiles/r04j/) shortened
+ * it, so it stays one plain pass on the calling thread. */
 static void reserve_device(md5hip_batcher *b, struct slot *sl, const struct chunk_src *src, uint64_t i,
                            uint64_t m)
 {
