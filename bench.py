@@ -91,8 +91,8 @@ def parse_args(argv):
     p.add_argument("--c3q-inflight", type=int, default=1,
                    help="--config c3q: launches in flight before the queue coalesces")
     p.add_argument("--c3q-slots", type=int, default=4, help="--config c3q: queue slots")
-    p.add_argument("--c3q-chain", type=int, default=1,
-                   help="--config c3q: chained launches (md5hip_batcher_set_chain; 0 = off, for A/B)")
+    p.add_argument("--c3q-chain", type=int, default=2,
+                   help="--config c3q: chained launches (md5hip_batcher_set_chain: 0 off, 1 on, 2 = on + BALANCED tails overlap, the default)")
     p.add_argument("--c5-chunks", type=int, default=1 << 18)
     p.add_argument("--c5-slice", type=int, default=64 << 20)
     return p.parse_args(argv)
@@ -795,8 +795,8 @@ def run_c3q(a, rank, world, local, device, backend):
         subs.append((ptrs, lk[j].astype(np.uint32), None))
     outs = [[torch.empty((x.size, 16), dtype=torch.uint8, device="cuda") for x in lk] for _ in range(2)]
     q = m.Queue(device=torch.cuda.current_device(), nslots=a.c3q_slots, inflight=a.c3q_inflight)
-    if not a.c3q_chain:
-        q.set_chain(False)
+    if a.c3q_chain != 2:
+        q.set_chain(a.c3q_chain)
 
     def submit(k):
         return [q.submit_device_async(p, L_, o) for (p, L_, _), o in zip(subs, outs[k & 1])]

@@ -289,13 +289,17 @@ int md5hip_batcher_set_inflight(md5hip_batcher *b, uint32_t target);
  * flush on one of its tickets, a full slot or a synchronous submission still
  * launches at once.  Default max_us 5000; 0 = launch at once. */
 int md5hip_batcher_set_linger(md5hip_batcher *b, uint32_t max_us);
-/* ABI 3: chained launches (default on).  With the pipeline at its target and
- * the running launch due to end within min(2 ms, a quarter of a launch), the
- * open slot -- planned, no chunk arrived since the last poll -- is launched
- * at once with its hash kernel waiting on the running launch's event, so it
- * starts when that one ends instead of after the host has seen it end (a C3
- * stream step lost ~1.3 ms to that).  0 turns it off. */
-int md5hip_batcher_set_chain(md5hip_batcher *b, int on);
+/* ABI 3: chained launches.  With the pipeline at its target and the running
+ * launch due to end within min(2 ms, a quarter of a launch), the open slot --
+ * planned, no chunk arrived since the last poll -- is launched at once with
+ * its hash kernel waiting on the running launch's event, so it starts when
+ * that one ends instead of after the host has seen it end (a C3 stream step
+ * lost ~1.3 ms to that).  mode 1: that; mode 2 (the
+ * default): the same, except that when both launches are BALANCED the hash
+ * kernel does not wait -- its workgroups take CUs as the running launch's
+ * finish (one BALANCED workgroup fills a CU's LDS, so the two never share a
+ * CU); 0: off. */
+int md5hip_batcher_set_chain(md5hip_batcher *b, int mode);
 
 struct md5hip_batcher_stats {
     uint64_t submissions;             /* tickets issued */

@@ -237,6 +237,10 @@ struct slot {
      * profiles/r04b/c3q_gaps.json); chain_at = when it should start */
     hipEvent_t chain_ev;
     uint64_t chain_at;
+    /* chain mode 2, both launches BALANCED: no device-side wait -- this
+     * launch's workgroups take CUs as the running one's finish (a BALANCED
+     * workgroup holds 96 KiB of LDS, so two never share a CU) */
+    int chain_overlap;
 };
 enum { WATCH_NONE = 0, WATCH_ACTIVE, WATCH_GAVE_UP };
 
@@ -266,7 +270,7 @@ struct md5hip_batcher {
     pthread_t progress;
     int progress_started, stop;
     int poll_fast;            /* the progress thread polls launches every 10 us now */
-    int chain;                /* chain the open slot behind the running launch (default 1) */
+    int chain;                /* chain the open slot behind the running launch: 0 off, 1 on, 2 (default) on + BALANCED tails overlap */
     hipEvent_t after_ev;     /* recorded on a producer's stream (md5_batch_submit_device_on) */
 };
 
@@ -441,7 +445,8 @@ static int slot_enqueue(md5hip_batcher *b, struct slot *sl)
         }
         /* a chained launch: bytes in and plan made beside the running
          * launch, the hash kernel after it */
-        if (sl->chain_ev && hipStreamWaitEvent(sl->stream, sl->chain_ev, 0) != hipSuccess) return -EIO;
+        if (sl->chain_ev && !sl->chain_overlap && hipStreamWaitEvent(sl->stream, sl->chain_ev, 0) != hipSuccess)
+            return -EIO;
         const uint32_t *ord = sl->use_order ? sl->d_ord : NULL;
         const uint64_t *doff = sl->desc_direct ? sl->dh_off : sl->d_off;
         const uint32_t *dlen = sl->desc_direct ? sl->dh_len : sl->d_len;
@@ -501,6 +506,7 @@ static void slot_reset(struct slot *sl)
     sl->watch = WATCH_NONE;
     sl->chain_ev = NULL;
     sl->chain_at = 0;
+    sl->chain_overlap = 0;
     sl->mode = MODE_NONE;
     sl->writers = sl->full = sl->flush = sl->err = sl->direct = 0;
     sl->n = sl->used = sl->nseg = sl->ndma = sl->ndsc = 0;
@@ -710,6 +716,9 @@ static void *progress_main(void *arg)
                     if (last && (double)now + lead >= (double)end && (double)now <= (double)end + lead) {
                         o->chain_ev = last->kdone;
                         o->chain_at = end > now ? end : now;
+                        o->chain_overlap = b->chain == 2 && last->mode != MODE_FIXED &&
+                                           last->plan_var == MD5HIP_DESC_BALANCED &&
+                                           o->plan_var == MD5HIP_DESC_BALANCED;
                         slot_try_launch(b, o);
                     }
                 }
@@ -916,7 +925,7 @@ static int batcher_new(int device, uint64_t slice_bytes, uint32_t nslots, uint64
     b->gather = MD5HIP_GATHER_AUTO;
     b->target = nslots > 2 ? 2 : 1;
     b->linger_max_us = 5000;
-    b->chain = 1;
+    b->chain = 2;
     b->open = -1;
     b->s = calloc(nslots, sizeof *b->s);
     /* ticket 0 = "nothing": complete at once */
@@ -1069,11 +1078,11 @@ int md5hip_batcher_set_linger(md5hip_batcher *b, uint32_t max_us)
     return 0;
 }
 
-int md5hip_batcher_set_chain(md5hip_batcher *b, int on)
+int md5hip_batcher_set_chain(md5hip_batcher *b, int mode)
 {
     if (!b) return -EINVAL;
     pthread_mutex_lock(&b->mu);
-    b->chain = on != 0;
+    b->chain = mode >= 2 ? 2 : mode != 0;
     pthread_mutex_unlock(&b->mu);
     return 0;
 }

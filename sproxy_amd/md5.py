@@ -563,10 +563,13 @@ class Batcher:
         min(max_us, 1/8 of recent launch time) for more work (0 = never)."""
         check(*self._call("set_linger", max_us))
 
-    def set_chain(self, on: bool):
-        """Chained launches (default on): the next slot's kernel queued behind
-        the running launch's event just before it ends."""
-        check(*self._call("set_chain", 1 if on else 0))
+    def set_chain(self, on):
+        """Chained launches: 1 = the next slot's kernel queued behind the
+        running launch's event just before it ends; 2 (the default) = the
+        same without the device-side wait when both launches are BALANCED
+        (the next one's workgroups take CUs as the running one's finish);
+        0/False = off."""
+        check(*self._call("set_chain", int(on)))
 
     def stats(self) -> dict:
         st = MD5HipBatcherStats()

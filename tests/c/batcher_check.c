@@ -292,7 +292,7 @@ static void *knobs(void *arg)
     while (!STOPPED()) {
         md5hip_batcher_set_inflight(g_b, 1 + (uint32_t)(rnd(&s) % 3));
         md5hip_batcher_set_linger(g_q, (uint32_t)(rnd(&s) % 400));
-        md5hip_batcher_set_chain(g_b, (int)(rnd(&s) & 1));
+        md5hip_batcher_set_chain(g_b, (int)(rnd(&s) % 3));
         md5hip_batcher_set_gather(g_b, (int)(rnd(&s) % 4));
         md5hip_pool_set_gather(g_pool, (int)(rnd(&s) % 4));
         md5hip_pool_set_split(g_pool, (rnd(&s) % 2) ? 0 : 256u << 10);
