@@ -633,8 +633,46 @@ __device__ __forceinline__ void desc_xpose_group(H& h, const uint8_t* __restrict
           __builtin_amdgcn_sched_barrier(0);
           if (stg < nst) h.block(st, w[1]);
         };
+        // The pairs of stages every live lane holds whole, whose next DMAs
+        // clamp no row: no per-lane guard, no clamp test, the stage offset
+        // in SGPRs (the common case: LPT groups are near-uniform).
+        auto stage_all = [&](uint32_t stg, auto B) __attribute__((always_inline)) {
+          constexpr int b = decltype(B)::value;
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          uint4 w[2][4];
+#pragma unroll
+          for (int q = 0; q < 8; ++q) {
+            const u32x4 v = *reinterpret_cast<lds_u4*>(raddr[q] + b * 8192u);
+            w[q >> 2][q & 3] = make_uint4(v.x, v.y, v.z, v.w);
+          }
+          {
+            auto* im = limg + (b ^ 1) * 8192u;
+            const uint64_t so = (uint64_t)(stg + 1) << 7;
+            auto rows = [&](auto... R) __attribute__((always_inline)) {
+              (dma(R, bptr[decltype(R)::value] + so, im), ...);
+            };
+            rows(std::integral_constant<int, 0>{}, std::integral_constant<int, 1>{},
+                 std::integral_constant<int, 2>{}, std::integral_constant<int, 3>{},
+                 std::integral_constant<int, 4>{}, std::integral_constant<int, 5>{},
+                 std::integral_constant<int, 6>{}, std::integral_constant<int, 7>{});
+          }
+          asm volatile("s_waitcnt lgkmcnt(4)" ::: "memory");
+          __builtin_amdgcn_sched_barrier(0);
+          h.block(st, w[0]);
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          __builtin_amdgcn_sched_barrier(0);
+          h.block(st, w[1]);
+        };
+        const uint32_t fmin = wave_min(live ? nst : 0xFFFFFFFFu);   // stages every live lane holds
+        const uint32_t lim = min(rmin, fmin - 1u);                 // fmin 0: wraps, guarded below
         issue(0, I0{});
-        for (uint32_t stg = 0; stg < smax; stg += 2) {
+        uint32_t stg = 0;
+        if (fmin > 0)
+          for (; stg + 2 <= lim; stg += 2) {
+            stage_all(stg, I0{});
+            stage_all(stg + 1, I1{});
+          }
+        for (; stg < smax; stg += 2) {
           stage(stg, I0{});
           if (stg + 1 < smax) stage(stg + 1, I1{});
         }
