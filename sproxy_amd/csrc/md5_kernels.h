@@ -634,9 +634,19 @@ __device__ __forceinline__ void desc_xpose_group(H& h, const uint8_t* __restrict
           if (stg < nst) h.block(st, w[1]);
         };
         // The pairs of stages every live lane holds whole, whose next DMAs
-        // clamp no row: no per-lane guard, no clamp test, the stage offset
-        // in SGPRs (the common case: LPT groups are near-uniform).
-        auto stage_all = [&](uint32_t stg, auto B) __attribute__((always_inline)) {
+        // clamp no row: no per-lane guard, no clamp test (the common case:
+        // LPT groups are near-uniform).  The pair's row pointers are formed
+        // once (pb = bptr + pair offset); the two stages' DMAs reach +128 /
+        // +256 through the instruction offset, which the LDS address takes
+        // too, so their M0 is the image base less that much (the images sit
+        // kImgPad bytes into the workgroup's LDS, balanced_body).
+        auto dma_at = [&](auto R, auto OFF, const uint8_t* g, __attribute__((address_space(3))) uint8_t* im)
+            __attribute__((always_inline)) {
+          constexpr int r = decltype(R)::value;
+          constexpr int o = decltype(OFF)::value;
+          __builtin_amdgcn_global_load_lds(g, im + (r >> 2) * 4096 - o, 16, (r & 3) * 1024 + o, P);
+        };
+        auto stage_all = [&](const uint8_t* const (&pb)[8], auto B) __attribute__((always_inline)) {
           constexpr int b = decltype(B)::value;
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
           uint4 w[2][4];
@@ -647,9 +657,9 @@ __device__ __forceinline__ void desc_xpose_group(H& h, const uint8_t* __restrict
           }
           {
             auto* im = limg + (b ^ 1) * 8192u;
-            const uint64_t so = (uint64_t)(stg + 1) << 7;
+            using O = std::integral_constant<int, 128 * (b + 1)>;   // the next stage: pair + 1 or + 2
             auto rows = [&](auto... R) __attribute__((always_inline)) {
-              (dma(R, bptr[decltype(R)::value] + so, im), ...);
+              (dma_at(R, O{}, pb[decltype(R)::value], im), ...);
             };
             rows(std::integral_constant<int, 0>{}, std::integral_constant<int, 1>{},
                  std::integral_constant<int, 2>{}, std::integral_constant<int, 3>{},
@@ -669,8 +679,12 @@ __device__ __forceinline__ void desc_xpose_group(H& h, const uint8_t* __restrict
         uint32_t stg = 0;
         if (fmin > 0)
           for (; stg + 2 <= lim; stg += 2) {
-            stage_all(stg, I0{});
-            stage_all(stg + 1, I1{});
+            const uint8_t* pb[8];
+            const uint64_t so = (uint64_t)stg << 7;
+#pragma unroll
+            for (int r = 0; r < 8; ++r) pb[r] = bptr[r] + so;
+            stage_all(pb, I0{});
+            stage_all(pb, I1{});
           }
         for (; stg < smax; stg += 2) {
           stage(stg, I0{});
@@ -1234,8 +1248,12 @@ md5_desc_fed(const uint8_t* __restrict__ base, const uint64_t* __restrict__ offs
 template <int WPB, int NB = 1, int W = 1>
 struct BalancedCfg {
   static constexpr uint32_t kWave = NB * W * 8192u;
-  static constexpr uint32_t kLds = WPB * kWave > 81920u ? WPB * kWave : 81920u + 16384u;
-  static_assert(WPB * kWave <= 160u * 1024u, "LDS per CU");
+  // the images start kImgPad bytes in: a DMA whose instruction offset
+  // carries the stage step (desc_xpose_group, NB = 2) takes M0 = image -
+  // up to 256 B
+  static constexpr uint32_t kImgPad = 256u;
+  static constexpr uint32_t kLds = WPB * kWave + kImgPad > 81920u ? WPB * kWave + kImgPad : 81920u + 16384u;
+  static_assert(WPB * kWave + kImgPad <= 160u * 1024u, "LDS per CU");
 };
 
 // The persistent body.  kSplit (WPB = 8, two waves per SIMD): groups whose
@@ -1261,7 +1279,7 @@ __device__ __forceinline__ uint32_t balanced_body(const uint8_t* __restrict__ ba
   Md5Hasher<true> h;
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  uint8_t* img = lds + wave * BalancedCfg<WPB, NB, W>::kWave;
+  uint8_t* img = lds + BalancedCfg<WPB, NB, W>::kImgPad + wave * BalancedCfg<WPB, NB, W>::kWave;
   const uint64_t ngroups = (n + 63) / 64;
   const DescArrays src{offs, lens, order};
   uint64_t nlong = ngroups;
