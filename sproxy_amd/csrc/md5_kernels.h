@@ -633,21 +633,23 @@ __device__ __forceinline__ void desc_xpose_group(H& h, const uint8_t* __restrict
           __builtin_amdgcn_sched_barrier(0);
           if (stg < nst) h.block(st, w[1]);
         };
-        // The pairs of stages every live lane holds whole, whose next DMAs
+        // The stages every live lane holds whole, whose next DMAs
         // clamp no row: no per-lane guard, no clamp test (the common case:
-        // LPT groups are near-uniform).  The pair's row pointers are formed
-        // once (pb = bptr + pair offset); the two stages' DMAs reach +128 /
-        // +256 through the instruction offset, which the LDS address takes
-        // too, so their M0 is the image base less that much (the images sit
-        // kImgPad bytes into the workgroup's LDS, balanced_body).
+        // LPT groups are near-uniform), four stages per loop test.  The row
+        // pointers are formed once per four stages (pb = bptr + offset); the
+        // stages' DMAs reach +128 .. +512 through the instruction offset,
+        // which the LDS address takes too, so their M0 is the image base less
+        // that much (the images sit kImgPad bytes into the workgroup's LDS,
+        // balanced_body).
         auto dma_at = [&](auto R, auto OFF, const uint8_t* g, __attribute__((address_space(3))) uint8_t* im)
             __attribute__((always_inline)) {
           constexpr int r = decltype(R)::value;
           constexpr int o = decltype(OFF)::value;
           __builtin_amdgcn_global_load_lds(g, im + (r >> 2) * 4096 - o, 16, (r & 3) * 1024 + o, P);
         };
-        auto stage_all = [&](const uint8_t* const (&pb)[8], auto B) __attribute__((always_inline)) {
-          constexpr int b = decltype(B)::value;
+        auto stage_all = [&](const uint8_t* const (&pb)[8], auto J) __attribute__((always_inline)) {
+          constexpr int j = decltype(J)::value;                 // stage j of the quad
+          constexpr int b = j & 1;
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
           uint4 w[2][4];
 #pragma unroll
@@ -657,7 +659,7 @@ __device__ __forceinline__ void desc_xpose_group(H& h, const uint8_t* __restrict
           }
           {
             auto* im = limg + (b ^ 1) * 8192u;
-            using O = std::integral_constant<int, 128 * (b + 1)>;   // the next stage: pair + 1 or + 2
+            using O = std::integral_constant<int, 128 * (j + 1)>;   // the next stage: quad + j + 1
             auto rows = [&](auto... R) __attribute__((always_inline)) {
               (dma_at(R, O{}, pb[decltype(R)::value], im), ...);
             };
@@ -678,13 +680,15 @@ __device__ __forceinline__ void desc_xpose_group(H& h, const uint8_t* __restrict
         issue(0, I0{});
         uint32_t stg = 0;
         if (fmin > 0)
-          for (; stg + 2 <= lim; stg += 2) {
+          for (; stg + 4 <= lim; stg += 4) {
             const uint8_t* pb[8];
             const uint64_t so = (uint64_t)stg << 7;
 #pragma unroll
             for (int r = 0; r < 8; ++r) pb[r] = bptr[r] + so;
-            stage_all(pb, I0{});
-            stage_all(pb, I1{});
+            stage_all(pb, std::integral_constant<int, 0>{});
+            stage_all(pb, std::integral_constant<int, 1>{});
+            stage_all(pb, std::integral_constant<int, 2>{});
+            stage_all(pb, std::integral_constant<int, 3>{});
           }
         for (; stg < smax; stg += 2) {
           stage(stg, I0{});
@@ -1250,8 +1254,8 @@ struct BalancedCfg {
   static constexpr uint32_t kWave = NB * W * 8192u;
   // the images start kImgPad bytes in: a DMA whose instruction offset
   // carries the stage step (desc_xpose_group, NB = 2) takes M0 = image -
-  // up to 256 B
-  static constexpr uint32_t kImgPad = 256u;
+  // up to 512 B
+  static constexpr uint32_t kImgPad = 512u;
   static constexpr uint32_t kLds = WPB * kWave + kImgPad > 81920u ? WPB * kWave + kImgPad : 81920u + 16384u;
   static_assert(WPB * kWave + kImgPad <= 160u * 1024u, "LDS per CU");
 };
