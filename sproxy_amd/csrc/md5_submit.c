@@ -350,7 +350,7 @@ static int seg_has(const struct slot *sl, uint64_t t)
 /* Small slots (a netcache vector) skip the two descriptor copies: the kernel
  * reads the fine-grained pinned arrays in place, one PCIe round trip per wave
  * instead of two copy operations ahead of the launch on the slot's stream. */
-enum { DESC_DIRECT_MAX = 4096 };
+enum { DESC_DIRECT_MAX = 4096, EARLY_COPY_MIN = 8192 };
 
 static int slot_prepare(md5hip_batcher *b, struct slot *sl)
 {
@@ -1437,6 +1437,20 @@ static int submit(md5hip_batcher *b, const struct chunk_src *src, uint64_t n, un
         }
         const uint64_t m = (uint64_t)got;
         const uint64_t hi = sl->used;
+        /* a large device-resident range: its descriptors go over now, on the
+         * slot's idle stream, instead of after the burst's last submission
+         * (a drained c3q step's 6 vectors: ~0.12 ms of copies that no longer
+         * sit between the burst and its kernel); appended descriptors are
+         * final, slot_prepare copies only what follows */
+        if (src->dptrs && m >= EARLY_COPY_MIN && sl->n > DESC_DIRECT_MAX && sl->n > sl->copied_n) {
+            const uint64_t c0 = sl->copied_n, cn = sl->n - c0;
+            if (hipMemcpyAsync(sl->d_off + c0, sl->h_off + c0, 8 * cn, hipMemcpyHostToDevice, sl->stream) ||
+                hipMemcpyAsync(sl->d_len + c0, sl->h_len + c0, 4 * cn, hipMemcpyHostToDevice, sl->stream)) {
+                if (!sl->err) sl->err = -EIO;
+            } else {
+                sl->copied_n = sl->n;
+            }
+        }
         /* recorded and waited on under one hold of b->mu (slot_take may have
          * let another producer record the event meanwhile), before this
          * slot's kernel can be enqueued: the kernel runs after the producer's
