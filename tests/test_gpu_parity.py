@@ -152,6 +152,41 @@ def test_desc_long_and_short_waves(cuda, dv):
         assert np.array_equal(got, want), order is None
 
 
+def test_balanced_guard_free_stage_edges(cuda):
+    """BALANCED's guard-free stages (md5_kernels.h, desc_xpose_group NB = 2:
+    stages every live lane holds whole and no row clamps, four per loop test)
+    hand over to the guarded stage at every boundary: 64-chunk groups of one
+    length with 1..21 whole 128-B stages and each of 0 / 64 / 100 B more; the
+    same groups with one lane of no stage, one lane a stage short, one lane
+    much longer; 16-B-aligned (off-line) and line-aligned packing; a ragged
+    last group.  Longest-first and unordered, against the oracle."""
+    rng = np.random.default_rng(5150)
+    lens = []
+    for k in range(1, 22):
+        for extra in (0, 64, 100):
+            g = [128 * k + extra] * 64
+            lens += g
+            h = list(g)
+            h[int(rng.integers(0, 64))] = int(rng.integers(0, 128))        # a lane with no stage
+            lens += h
+            h = list(g)
+            h[int(rng.integers(0, 64))] = max(0, 128 * (k - 1) + extra)   # a stage short
+            lens += h
+            h = list(g)
+            h[int(rng.integers(0, 64))] = 128 * (k + 9) + 17               # one much longer
+            lens += h
+    lens += [128 * 7 + 3] * 37                                            # ragged last group
+    for align in (16, 128):
+        offs, total = gen.pack_offsets(lens, align=align)
+        buf = gen.xorshift_array(total + 64, seed=align + 5150)
+        want = gen.oracle_digests(buf, offs, lens)
+        for order in (None, m.plan_order(lens).astype(np.int32)):
+            got = m.digest_desc(_dev(buf, cuda), torch.tensor(offs, dtype=torch.int64, device=cuda),
+                                torch.tensor(lens, dtype=torch.int32, device=cuda),
+                                None if order is None else _dev(order, cuda), variant="balanced").cpu().numpy()
+            assert np.array_equal(got, want), (align, order is None)
+
+
 def test_hybrid_long_group_edges(cuda):
     """HYBRID's long groups (longest chunk >= 256 KiB, one per CU, run
     lane-direct): long chunks at every residue mod 64 and 128 beside lanes
