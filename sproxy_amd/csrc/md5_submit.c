@@ -717,6 +717,7 @@ static void *progress_main(void *arg)
                         o->chain_ev = last->kdone;
                         o->chain_at = end > now ? end : now;
                         o->chain_overlap = b->chain == 2 && last->mode != MODE_FIXED &&
+                                           last->kind == MD5HIP_DIGEST_MD5 && o->kind == MD5HIP_DIGEST_MD5 &&
                                            last->plan_var == MD5HIP_DESC_BALANCED &&
                                            o->plan_var == MD5HIP_DESC_BALANCED;
                         slot_try_launch(b, o);
