@@ -427,22 +427,9 @@ __device__ __forceinline__ void emit(H& h, typename H::Out* __restrict__ out, ui
 // kLongPair: HYBRID's lane-direct long waves refill their 8-block ring two
 // blocks (one whole 128-B line) at a time, so no lane leaves half a line
 // behind to be fetched again after eviction (ring_steps).
-// NB (kDma): LDS-DMA buffers per wave.  2: the DMA of wide stage s+2 is
-// issued as soon as wide stage s is read, so a lone wave on its SIMD
-// (BALANCED) keeps a stage in flight under each compression.
-// W (kDma): 128-B stages per wide stage; a buffer is W 8 KiB images, and the
-// W loads of one row (8 chunks) go out back to back, so each chunk is read
-// W x 128 B contiguous per visit instead of 128 B.
-// kHashOff: loads only, no compression (diagnostic memory-side ceiling).
-template <int N>
-__device__ __forceinline__ void wait_vmcnt() {
-  static_assert(N == 0 || N == 8 || N == 16 || N == 32, "vmcnt immediates in use");
-  if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-  else if constexpr (N == 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-  else asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
-}
-
+// NB (kDma): LDS-DMA images per wave, 1 or 2.  2 is BALANCED's lone wave per
+// SIMD: the next stage's DMA goes into the other image under this stage's
+// row reads (below).
 // kShift (kDma, one image): a wave holding a chunk that does not start on a
 // 128-B line loads whole LINES instead of chunk-relative 128-B stages, each
 // line once; a lane rotates its line reads by its chunk's 16-B offset s and
@@ -452,8 +439,8 @@ __device__ __forceinline__ void wait_vmcnt() {
 // between the two visits under 16 waves per CU (16-B-packed ragged blocks:
 // 1.29x the payload read from HBM).
 template <int CP, class H, uint32_t kLong = 0, int D = 1, bool kHalf = false, bool kPeel = true,
-          bool kDma = false, class Src = DescArrays, bool kLongPair = true, int NB = 1, int W = 1,
-          bool kHashOff = false, bool kShift = false>
+          bool kDma = false, class Src = DescArrays, bool kLongPair = true, int NB = 1,
+          bool kShift = false>
 __device__ __forceinline__ void desc_xpose_group(H& h, const uint8_t* __restrict__ base,
                                                  const Src& src, uint64_t n,
                                                  uint64_t first, typename H::Out* __restrict__ out,
@@ -552,7 +539,8 @@ __device__ __forceinline__ void desc_xpose_group(H& h, const uint8_t* __restrict
         h.block(st, w[1]);
       }
     };
-    if constexpr (kDma && NB == 2 && W == 1) {
+    static_assert(NB == 1 || (NB == 2 && kDma), "LDS-DMA images per wave: 1 or 2");
+    if constexpr (kDma && NB == 2) {
       // Two 8 KiB images for a LONE wave on its SIMD (BALANCED): a lone
       // wave issues one instruction per slot, so everything it does besides
       // VALU comes straight off its chain.  Per 128-B stage: the next stage's
@@ -697,57 +685,6 @@ __device__ __forceinline__ void desc_xpose_group(H& h, const uint8_t* __restrict
       };
       if (CP == 0 || !lined) run2(std::integral_constant<int, 0>{});
       else run2(std::integral_constant<int, CP>{});
-    } else if constexpr (kDma && (NB == 2 || W > 1)) {
-      static_assert(D == 1 && !kHalf && (NB == 1 || NB == 2), "LDS-DMA images: full 8 KiB stages");
-      const uint32_t nws = (smax + W - 1) / W;              // wide stages
-      auto issue = [&](uint32_t ws) __attribute__((always_inline)) {
-        uint8_t* im = img + (ws % NB) * (W * 8192u);
-#pragma unroll
-        for (int r = 0; r < 8; ++r) {
-#pragma unroll
-          for (int j = 0; j < W; ++j) {
-            const uint32_t stg = ws * W + j;
-            if (W == 1 || stg < smax)                       // wave-uniform
-              __builtin_amdgcn_global_load_lds(rptr[r] + (min(stg, rlast[r]) << 7),
-                                               im + j * 8192 + r * 1024, 16, 0, CP);
-          }
-        }
-      };
-      issue(0);
-      if (NB == 2 && nws > 1) issue(1);
-      for (uint32_t ws = 0; ws < nws; ++ws) {
-        // wide stage ws is in once at most the next one's loads are
-        // outstanding (loads complete in issue order); a partial next one
-        // (the group's last) falls back to a full drain
-        if constexpr (NB == 2) {
-          if ((ws + 2) * W <= smax) wait_vmcnt<8 * W>();
-          else wait_vmcnt<0>();
-        } else {
-          wait_vmcnt<0>();
-        }
-        uint4 w[W][2][4];
-        const uint8_t* row = myrow + (ws % NB) * (W * 8192u);
-#pragma unroll
-        for (int j = 0; j < W; ++j) {
-#pragma unroll
-          for (int q = 0; q < 8; ++q) {
-            const u32x4 v = *reinterpret_cast<const u32x4*>(row + j * 8192 + ((q ^ g) * 16));
-            w[j][q >> 2][q & 3] = make_uint4(v.x, v.y, v.z, v.w);
-          }
-        }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // reads done before the refill
-        if (ws + NB < nws) issue(ws + NB);
-        __builtin_amdgcn_sched_barrier(0);
-        if constexpr (!kHashOff) {
-#pragma unroll
-          for (int j = 0; j < W; ++j) {
-            if (ws * W + j < nst) {
-              h.block(st, w[j][0]);
-              h.block(st, w[j][1]);
-            }
-          }
-        }
-      }
     } else if constexpr (kDma) {
       static_assert(D == 1 && !kHalf, "LDS-DMA image: one full 8 KiB stage");
       // Cache policy per wave: CP (nt for the product kernels) when every
@@ -912,7 +849,7 @@ __device__ __forceinline__ void desc_xpose_body(const uint8_t* __restrict__ base
   H h;
   const uint64_t first = ((uint64_t)blockIdx.x * blockDim.x) + (threadIdx.x & ~63u);
   if (first >= n) return;
-  desc_xpose_group<CP, H, kLong, D, false, true, kDma, DescArrays, true, 1, 1, false, kShift>(
+  desc_xpose_group<CP, H, kLong, D, false, true, kDma, DescArrays, true, 1, kShift>(
       h, base, DescArrays{offs, lens, order}, n, first, out, img, nlong);
 }
 
@@ -1246,12 +1183,12 @@ md5_desc_fed(const uint8_t* __restrict__ base, const uint64_t* __restrict__ offs
 // done; the last wave out resets both, so a counter serves the next launch
 // on its stream (md5_kernels.hip keeps one per device and stream).
 // ---------------------------------------------------------------------------
-// WPB waves per workgroup (one per SIMD at 4, two at 8), each with NB x W
-// 8 KiB LDS-DMA images; the workgroup asks for more than half the CU's LDS,
-// so a CU runs exactly one.
-template <int WPB, int NB = 1, int W = 1>
+// WPB waves per workgroup (one per SIMD at 4, two at 8), each with NB 8 KiB
+// LDS-DMA images; the workgroup asks for more than half the CU's LDS, so a
+// CU runs exactly one.
+template <int WPB, int NB = 1>
 struct BalancedCfg {
-  static constexpr uint32_t kWave = NB * W * 8192u;
+  static constexpr uint32_t kWave = NB * 8192u;
   // the images start kImgPad bytes in: a DMA whose instruction offset
   // carries the stage step (desc_xpose_group, NB = 2) takes M0 = image -
   // up to 512 B
@@ -1260,67 +1197,35 @@ struct BalancedCfg {
   static_assert(WPB * kWave + kImgPad <= 160u * 1024u, "LDS per CU");
 };
 
-// The persistent body.  kSplit (WPB = 8, two waves per SIMD): groups whose
-// first (longest) chunk is >= 256 KiB form the LONG queue, the rest the SHORT
-// queue; waves 0-3 of the workgroup (one per SIMD) take LONG groups, waves
-// 4-7 SHORT ones, each falling back to the other queue when its own is empty.
-// So every SIMD runs one serial chain at a time at s_setprio 3, and the short
-// groups fill the chain's issue gaps at a lower priority instead of slowing it
-// (measured slower: a lone wave already issues VALU at the SIMD's full rate,
-// profiles/r02_chain_ilp_probe.json; two long chains on one SIMD halve each
-// other's speed).
-// ctr[0] long (all groups, unsplit), ctr[1] short, ctr[2] waves done.
-// Returns the number of groups this wave took (diagnostics).
-template <int WPB, int NB, bool kSplit, int W = 1, bool kHashOff = false, int CP = 2,
-          uint32_t kLong = 0>
+// The persistent body: each wave takes the next 64-chunk group (longest
+// first) from ctr[0] until none is left; ctr[2] counts waves done, and the
+// last one out resets the counters for the next launch on the stream.  (Two
+// waves per SIMD, with or without split long / short queues at different
+// s_setprio, measured slower: a 1 MiB chain sharing its SIMD runs at half
+// speed, profiles/r02_c3_balanced_ab.json, r04v/balanced_2wps_ab.json.)
+// Returns the number of groups this wave took.
+template <int WPB, int NB, int CP = 2, uint32_t kLong = 0>
 __device__ __forceinline__ uint32_t balanced_body(const uint8_t* __restrict__ base,
                                                   const uint64_t* __restrict__ offs,
                                                   const uint32_t* __restrict__ lens,
                                                   const uint32_t* __restrict__ order, uint64_t n,
                                                   uint4* __restrict__ out, uint32_t* __restrict__ ctr,
                                                   uint8_t* lds) {
-  static_assert(!kSplit || WPB == 8, "split queues: one long and one short wave per SIMD");
   Md5Hasher<true> h;
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  uint8_t* img = lds + BalancedCfg<WPB, NB, W>::kImgPad + wave * BalancedCfg<WPB, NB, W>::kWave;
+  uint8_t* img = lds + BalancedCfg<WPB, NB>::kImgPad + wave * BalancedCfg<WPB, NB>::kWave;
   const uint64_t ngroups = (n + 63) / 64;
   const DescArrays src{offs, lens, order};
-  uint64_t nlong = ngroups;
-  if constexpr (kSplit) {          // first group whose first chunk is < 256 KiB (longest-first)
-    uint64_t lo = 0, hi = ngroups;
-    while (lo < hi) {
-      const uint64_t mid = (lo + hi) >> 1;
-      const uint32_t L = lens[src.index(mid * 64u)];
-      if ((L >> 6) >= kHybridLongBlocks) lo = mid + 1;
-      else hi = mid;
-    }
-    nlong = __builtin_amdgcn_readfirstlane((uint32_t)lo);
-  }
-  const bool pref_long = !kSplit || wave < 4;
-  auto take = [&](bool lng) __attribute__((always_inline)) -> uint64_t {
-    uint32_t t = 0;
-    if (lane == 0) t = atomicAdd(&ctr[lng ? 0 : 1], 1u);
-    t = __builtin_amdgcn_readfirstlane((uint32_t)__shfl((int)t, 0, 64));
-    const uint64_t g = lng ? (uint64_t)t : nlong + t;
-    return (lng ? g < nlong : g < ngroups) ? g : ~0ull;
-  };
   uint32_t taken = 0;
-  bool mine = true;                // still drawing from the preferred queue
   for (;;) {
-    uint64_t g = ~0ull;
-    if (mine) {
-      g = take(pref_long);
-      if (g == ~0ull) mine = false;
-    }
-    if (g == ~0ull) {
-      if (!kSplit) break;
-      g = take(!pref_long);
-      if (g == ~0ull) break;
-    }
+    uint32_t t = 0;
+    if (lane == 0) t = atomicAdd(&ctr[0], 1u);
+    t = __builtin_amdgcn_readfirstlane((uint32_t)__shfl((int)t, 0, 64));
+    if ((uint64_t)t >= ngroups) break;
     ++taken;
-    desc_xpose_group<CP, Md5Hasher<true>, kLong, 1, false, true, true, DescArrays, true, NB, W, kHashOff>(
-        h, base, src, n, g * 64u, out, img, 0xFFFFFFFFu);   // kLong: every long group lane-direct
+    desc_xpose_group<CP, Md5Hasher<true>, kLong, 1, false, true, true, DescArrays, true, NB>(
+        h, base, src, n, (uint64_t)t * 64u, out, img, 0xFFFFFFFFu);   // kLong: every long group lane-direct
   }
   if (lane == 0) {
     const uint32_t total = gridDim.x * (blockDim.x >> 6);
@@ -1345,23 +1250,22 @@ __device__ __forceinline__ uint32_t balanced_body(const uint8_t* __restrict__ ba
 // default policy keeps it: 1.005x, the same kernel 22.1 -> 16.1-16.7 ms on
 // five coalesced batches.  Wider stages (W x 128 B per visit), two buffers
 // filled the round-2 way (DMA after the reads), 8 waves per CU and split
-// long/short queues measured no better.
+// long/short queues measured no better (their code is in git history,
+// profiles/r02_c3_wide_ab.json, r02_c3_balanced_ab.json).
 constexpr int kBalancedWaves = 4;
 // two images: the lone wave's next DMA issued under its row reads, the LDS
 // base set twice per stage (round 4: 0.8-1.7 % faster on 3 and 6 coalesced
 // C3 batches, profiles/r04c/balanced_ab.json)
 constexpr int kBalancedImages = 2;
-constexpr int kBalancedWide = 1;
-constexpr bool kBalancedSplit = false;
 constexpr int kBalancedPolicy = 2;   // nt for line-aligned groups only (desc_xpose_group)
 
-template <int WPB, int NB, bool kSplit, int W, int CP>
+template <int WPB, int NB, int CP>
 __global__ void __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(1, WPB / 4)))
 md5_desc_balanced_t(const uint8_t* __restrict__ base, const uint64_t* __restrict__ offs,
                     const uint32_t* __restrict__ lens, const uint32_t* __restrict__ order, uint64_t n,
                     uint4* __restrict__ out, uint32_t* __restrict__ ctr) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t lds_dyn[];   // BalancedCfg<WPB, NB, W>::kLds
-  (void)balanced_body<WPB, NB, kSplit, W, false, CP>(base, offs, lens, order, n, out, ctr, lds_dyn);
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds_dyn[];   // BalancedCfg<WPB, NB>::kLds
+  (void)balanced_body<WPB, NB, CP>(base, offs, lens, order, n, out, ctr, lds_dyn);
 }
 
 // ---------------------------------------------------------------------------

@@ -222,8 +222,8 @@ int md5hip_digest_desc_variant(const void* d_base, const uint64_t* d_offsets,
     uint32_t* ctr = balanced_counter(s);
     if (!ctr) return -ENOMEM;
     constexpr int WPB = kBalancedWaves;
-    constexpr uint32_t lds = BalancedCfg<WPB, kBalancedImages, kBalancedWide>::kLds;
-    auto kern = md5_desc_balanced_t<WPB, kBalancedImages, kBalancedSplit, kBalancedWide, kBalancedPolicy>;
+    constexpr uint32_t lds = BalancedCfg<WPB, kBalancedImages>::kLds;
+    auto kern = md5_desc_balanced_t<WPB, kBalancedImages, kBalancedPolicy>;
     if (!dyn_lds_ready(reinterpret_cast<const void*>(kern), lds)) return -ENODEV;
     // the kernel resets its counter on exit; zero it on the stream anyway, so
     // a launch that never finished (a fault) cannot poison the next one
