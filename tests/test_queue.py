@@ -360,3 +360,58 @@ def test_queue_concurrency_stress(cuda):
         st = q.stats()
     assert not errs, errs[:3]
     assert len(done) > 50 and st["submissions"] >= len(done), (len(done), st)
+
+
+@pytest.mark.parametrize("chain", [0, 1, 2])
+def test_queue_pipelined_stream_every_chain_mode(cuda, chain):
+    """The c3q stream in miniature under each chain mode
+    (md5hip_batcher_set_chain: 0 off, 1 kernel queued behind the running
+    launch's event, 2 the same but BALANCED launches overlapping their
+    tails): 4 C3-shaped vectors of 8 GiB per step -- coalesced, BALANCED's
+    size -- 5 steps, step k submitted before step k-1 is waited for, digests
+    into two alternating sets of device tensors.  Every digest of every step
+    equals a separate XDMA launch over the same vector, and a sample of the
+    oracle's."""
+    import sys
+    sys.path.insert(0, gen.REPO)
+    import bench
+    K = 4
+    lk = [bench.c3_lens(8 << 30, 90 + j) for j in range(K)]
+    _, var = m.plan_desc(np.concatenate(lk).astype(np.uint32))
+    assert var == "balanced", var                  # the launches chain mode 2 overlaps
+    spans = [int(((L + 15) // 16 * 16).sum()) for L in lk]
+    starts = np.concatenate([[0], np.cumsum(spans)[:-1]]).astype(np.int64)
+    data = m.arena_empty(int(sum(spans)) + 64)
+    m.fill_synthetic(data, seed=0xC4A1)
+    torch.cuda.synchronize()
+    ref, subs = [], []
+    for j, L in enumerate(lk):
+        offs = starts[j] + np.concatenate([[0], np.cumsum((L + 15) // 16 * 16)[:-1]])
+        ref.append(m.digest_desc(data, torch.from_numpy(offs).to(cuda),
+                                 torch.from_numpy(L.astype(np.int32)).to(cuda), variant="xdma"))
+        subs.append(((np.uint64(data.data_ptr()) + offs.astype(np.uint64)), L.astype(np.uint32)))
+    # the oracle on the chunks of vector 0's first 256 MiB
+    offs0 = np.concatenate([[0], np.cumsum((lk[0] + 15) // 16 * 16)[:-1]])
+    near = np.nonzero(offs0 + lk[0] <= (256 << 20))[0]
+    idx = np.unique(np.concatenate([near[:64], np.random.default_rng(9).choice(near, 200)]))
+    host = data[: 256 << 20].cpu().numpy()
+    want = gen.oracle_digests(host, offs0[idx], lk[0][idx])
+    assert np.array_equal(ref[0].cpu().numpy()[idx], want)
+    q = m.Queue(device=0, nslots=4, inflight=1)
+    q.set_chain(chain)
+    outs = [[torch.empty((L.size, 16), dtype=torch.uint8, device=cuda) for L in lk] for _ in range(2)]
+    prev = None
+    for k in range(5):
+        cur = [q.submit_device_async(p, L, o) for (p, L), o in zip(subs, outs[k & 1])]
+        if prev is not None:
+            for pn in prev:
+                pn.wait()
+            for j in range(K):
+                assert torch.equal(outs[(k - 1) & 1][j], ref[j]), (chain, k - 1, j)
+        prev = cur
+    for pn in prev:
+        pn.wait()
+    for j in range(K):
+        assert torch.equal(outs[0][j], ref[j]), (chain, 4, j)
+    st = q.stats()
+    assert st["submissions"] == 5 * K and st["launches"] < st["submissions"], st
