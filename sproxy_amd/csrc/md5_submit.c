@@ -475,6 +475,7 @@ static int slot_enqueue(md5hip_batcher *b, struct slot *sl)
         const struct seg *g = &sl->segs[k];
         if (!g->on_device) { any_host = 1; continue; }
         const uint64_t len = (uint64_t)sl->dsz * g->count;
+        if (len == 0) continue;
         uint64_t extra = (len + DSC_PIECE - 1) / DSC_PIECE - 1;
         if (extra > spare) extra = spare;
         spare -= extra;
