@@ -249,8 +249,9 @@ int md5hip_fill_synthetic(void *d_dst, uint64_t nbytes, uint64_t seed, void *str
  * fewer than `inflight target` slots are running (an idle device takes work
  * at once), when it is chained behind a launch about to end
  * (md5hip_batcher_set_chain), or when a caller waits on, polls or flushes a
- * ticket in it while nothing runs (a synchronous submission is such a wait:
- * on a busy device it coalesces with the other callers' work).
+ * ticket in it while nothing runs.  A synchronous submission's slot goes at
+ * once while fewer than nslots - 1 launches run; past that it coalesces with
+ * the other callers' work in the last slot.
  * While the device is busy, everything submitted meanwhile is therefore
  * coalesced into the next launch.  A progress thread per batcher retires
  * finished slots, delivers digests and launches the open slot.

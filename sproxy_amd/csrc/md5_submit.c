@@ -241,6 +241,9 @@ struct slot {
      * launch's workgroups take CUs as the running one's finish (a BALANCED
      * workgroup holds 96 KiB of LDS, so two never share a CU) */
     int chain_overlap;
+    /* a synchronous caller's chunks are here: the slot goes while a slot is
+     * left over to coalesce the callers behind it (slot_try_launch) */
+    int urgent;
 };
 enum { WATCH_NONE = 0, WATCH_ACTIVE, WATCH_GAVE_UP };
 
@@ -508,6 +511,7 @@ static void slot_reset(struct slot *sl)
     sl->chain_ev = NULL;
     sl->chain_at = 0;
     sl->chain_overlap = 0;
+    sl->urgent = 0;
     sl->mode = MODE_NONE;
     sl->writers = sl->full = sl->flush = sl->err = sl->direct = 0;
     sl->n = sl->used = sl->nseg = sl->ndma = sl->ndsc = 0;
@@ -553,6 +557,10 @@ static void slot_try_launch(md5hip_batcher *b, struct slot *sl)
      * md5_batch_wait's hasten, re-applied whenever the slot is looked at,
      * since they sleep until it goes) */
     if (sl->nwait && b->inflight == 0) sl->flush = 1;
+    /* synchronous callers: up to nslots - 1 launches run at once (a netcache
+     * vector is a wave or two: concurrent small launches cost the device
+     * nothing), the last slot coalesces whoever comes while they run */
+    if (sl->urgent && b->inflight + 1 < b->nslots) sl->flush = 1;
     if (sl->n == 0) {                 /* nothing reserved (all chunks failed) */
         if (b->open == (int)(sl - b->s)) b->open = -1;
         slot_retire(b, sl, sl->err);
@@ -1474,12 +1482,13 @@ static int submit(md5hip_batcher *b, const struct chunk_src *src, uint64_t n, un
             sl->writers--;
         }
         i += m;
-        /* the caller waits right away: no linger on an idle device; on a
-         * busy one the slot keeps coalescing (it goes when fewer than
-         * `target` launches run, is chained behind the running one, or goes
-         * when that retires) -- forcing every synchronous call out at once
-         * made one launch per vector at ASIO scale (profiles/r04b/) */
-        if (urgent && i >= n && b->inflight == 0) sl->flush = 1;
+        /* the caller waits right away: no linger; the slot goes while fewer
+         * than nslots - 1 launches run, else it coalesces in the last slot
+         * (slot_try_launch) -- forcing every synchronous call out at once
+         * made one launch per vector at ASIO scale (profiles/r04b/), and
+         * holding them to `target` launches cost the 8-thread call site a
+         * fifth of its throughput (profiles/r04d/asio_threads.json) */
+        if (urgent && i >= n) sl->urgent = 1;
         slot_try_launch(b, sl);
     }
     tk_put(b, t, rc);                        /* the submission's own reference */
