@@ -4,7 +4,8 @@ OLD (build/ab/libmd5hip_old.so, the library before a change) against NEW
 (sproxy_amd/lib/libmd5hip.so).  Both are loaded with ctypes side by side;
 every workload runs both, interleaved, and their outputs are compared.
 
-Workloads (the descriptor LDS-DMA loader's users):
+Workloads:
+  c2        md5hip_digest_fixed_variant xdma1nt on 1,048,576 x 16 KiB (bench C2)
   ctx       md5hip_update_ctx on 1,048,576 contexts x 16 KiB (bench --config ctx)
   ragged16  md5hip_digest_desc_variant XDMA, netcache blocks packed at 16 B
   c3k3      BALANCED on 3 coalesced C3 batches (bench --config c3 coalesced leg)
@@ -32,6 +33,7 @@ def load(path):
     L.md5hip_update_ctx.argtypes = [vp, vp, vp, u64, vp]
     L.md5hip_init_ctx.argtypes = [vp, u64, vp]
     L.md5hip_digest_desc_variant.argtypes = [vp, vp, vp, vp, u64, vp, vp, ci]
+    L.md5hip_digest_fixed_variant.argtypes = [vp, u64, ctypes.c_uint32, u64, vp, vp, ci]
     return L
 
 
@@ -85,7 +87,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=9)
     ap.add_argument("--extra", nargs="*", default=[], help="name=path of more builds to compare")
     ap.add_argument("--old", default="build/ab/libmd5hip_old.so", help="the baseline build")
-    ap.add_argument("--only", default="", help="comma list of workloads (ctx,ragged16,c3k3_balanced,c3k6_balanced,c3_hybrid)")
+    ap.add_argument("--only", default="", help="comma list of workloads (c2,ctx,ragged16,c3k3_balanced,c3k6_balanced,c3_hybrid)")
     a = ap.parse_args()
     only = set(a.only.split(",")) if a.only else None
     libs = {"old": load(os.path.join(REPO, a.old))}
@@ -96,6 +98,8 @@ def main():
     st = torch.cuda.current_stream().cuda_stream
     res = {}
 
+    if only is None or "c2" in only:
+        c2_ab(libs, st, res, a.rounds)
     # ctx: 1 M contexts x 16 KiB (one update launch; contexts re-initialised per run)
     if only is None or "ctx" in only:
         ctx_ab(libs, st, res, a.rounds)
@@ -105,6 +109,19 @@ def main():
         if only is None or name in only:
             c3_ab(libs, st, res, a.rounds, K, name, var)
     print(json.dumps(res))
+
+
+def c2_ab(libs, st, res, rounds):
+    """C2: 1,048,576 x 16 KiB fixed-length, md5_fixed_xdma1nt (variant 10)"""
+    n, L = 1 << 20, 16384
+    data = m.arena_empty(n * L)
+    m.fill_synthetic(data, seed=0xC2)
+    dig = torch.empty((n, 16), dtype=torch.uint8, device="cuda")
+    run = lambda Lb: Lb.md5hip_digest_fixed_variant(data.data_ptr(), n, L, L, dig.data_ptr(), st, 10)  # noqa
+    res["c2"] = ab(libs, run, lambda: dig, rounds)
+    print(json.dumps({"c2": res["c2"]}), flush=True)
+    del data, dig
+    torch.cuda.empty_cache()
 
 
 def ctx_ab(libs, st, res, rounds):
