@@ -30,13 +30,17 @@
 extern "C" {
 #endif
 
-/* ABI 3 (round 4): md5_batch_submit_device_after (an ordering flag apart from
+/* ABI 4 (round 5): device failure -- md5hip_batcher_health /
+ * md5hip_batcher_inject_fault, md5hip_pool_get_health / _device_health /
+ * _inject_fault (appended); md5hip_batcher_set_chain rejects modes outside
+ * 0..2 with -EINVAL.
+ * ABI 3 (round 4): md5_batch_submit_device_after (an ordering flag apart from
  * the producer stream, so the null stream can be ordered on), the LINES
  * descriptor kernel and md5hip_plan_desc_at (appended); round 3 had
  * already grown MD5HIP_DESC_NUM_VARIANTS 6 -> 7 (FED) and CRC32HIP_NUM_VARIANTS
  * 7 -> 8 (SPLIT) -- appended values, compatible -- and made the pool route a
  * submission whole (same results; set_digest no longer drains). */
-#define MD5HIP_ABI_VERSION 3
+#define MD5HIP_ABI_VERSION 4
 
 /* Fixed-length kernels for md5hip_digest_fixed_variant.  ABI 2: the round-1
  * A/B variants (values 2-9) moved to the diagnostic library (removed in round 4;
@@ -299,8 +303,27 @@ int md5hip_batcher_set_linger(md5hip_batcher *b, uint32_t max_us);
  * default): the same, except that when both launches are BALANCED the hash
  * kernel does not wait -- its workgroups take CUs as the running launch's
  * finish (one BALANCED workgroup fills a CU's LDS, so the two never share a
- * CU); 0: off. */
+ * CU); 0: off.  Other values: -EINVAL. */
 int md5hip_batcher_set_chain(md5hip_batcher *b, int mode);
+
+/* ABI 4: device failure.  blk_make_crc cannot fail (blk_io.c:354-430); a
+ * batcher can.  When a launch's completion event reports an error (a kernel
+ * fault, a lost or reset device), or an enqueue fails and the slot's stream
+ * then reports one, the batcher is FAILED for good:
+ *   - the tickets of that launch complete with -EIO;
+ *   - tickets still coalescing in the open slot complete with -ENODEV;
+ *   - every later submission returns -ENODEV at once, touching nothing;
+ *   - no digest of a failed launch is written anywhere.
+ * Launches already in flight complete as their own events say.  The library
+ * never falls back to the host: what the call site does instead (and that a
+ * device error is never a checksum mismatch) is INTEGRATION.md §2j.
+ * md5hip_batcher_health: 0 healthy, -ENODEV failed.
+ * md5hip_batcher_inject_fault: test control for that policy -- the
+ * after-th launch from now (1 = the next) is reported as a device fault once
+ * it has really finished (its event is still waited for); 0 cancels;
+ * returns -ENODEV if the batcher has failed already. */
+int md5hip_batcher_health(const md5hip_batcher *b);
+int md5hip_batcher_inject_fault(md5hip_batcher *b, uint64_t after);
 
 struct md5hip_batcher_stats {
     uint64_t submissions;             /* tickets issued */
@@ -487,6 +510,27 @@ struct md5hip_pool_stats {
 int md5hip_pool_get_stats(md5hip_pool *p, struct md5hip_pool_stats *out);
 /* Device g's batcher counters (launches, coalesced launches, ...). */
 int md5hip_pool_device_stats(md5hip_pool *p, uint32_t g, struct md5hip_batcher_stats *out);
+
+/* ABI 4: failed devices (md5hip_batcher_health).  The router never picks a
+ * failed device.  A submission that finds its device failed before the
+ * device took its chunks (-ENODEV) is routed to another one; a synchronous
+ * submission (or split part) whose launch then fails is resubmitted on a
+ * healthy device from the caller's still-valid buffers, so it returns 0 as
+ * long as one device is left.  An asynchronous ticket whose launch fails
+ * completes with -EIO (its buffers may be gone by the wait).  With every
+ * device failed, submissions return -ENODEV.
+ * md5hip_pool_device_health: 0 / -ENODEV for device index g (-EINVAL
+ * past ndev); md5hip_pool_inject_fault: md5hip_batcher_inject_fault on
+ * device index g. */
+struct md5hip_pool_health {
+    uint32_t ndev;
+    uint32_t nfailed;                 /* devices failed */
+    uint64_t failed_mask;             /* bit g: device index g failed (g < 64) */
+    uint64_t failovers;               /* submissions or parts moved off a failed device */
+};
+int md5hip_pool_get_health(md5hip_pool *p, struct md5hip_pool_health *out);
+int md5hip_pool_device_health(md5hip_pool *p, uint32_t g);
+int md5hip_pool_inject_fault(md5hip_pool *p, uint32_t g, uint64_t after);
 
 /* The pool's split, exposed for callers and tests (host only, synchronous):
  * first[0..nparts] such that part g is chunks [first[g], first[g+1]).

@@ -12,6 +12,14 @@ checked against the oracle).
                     (httpd.c:8627) and 1 MiB next to 16 KiB, vectors of 8 and
                     64 blocks, 1 / 8 / 64 callers, through the batcher and on
                     the calling thread (product MD5Init/Update/Final)
+  --matrix bigchunk VERDICT r04 item 2: the rest of netcache's chunk_size
+                    range (clamped to 4-10,240 KiB, httpd.c:7968): 2, 4 and
+                    10 MiB blocks in vectors of 1, 4 and 8, 1 / 8 / 64
+                    callers, batcher vs the calling thread
+  --matrix watch    VERDICT r04 item 3: the blocked caller's watcher policy
+                    (MD5HIP_WATCH spin / tail / block, md5_submit.c
+                    watch_launch) at 8 / 64 / 256 callers of 64 x 16 KiB from
+                    registered pages, batcher and pool, interleaved rounds
 
 Writes one JSON file (--out) with every run; prints each run as it ends.
 usage: asio_scale.py --matrix threads|chunk [--secs 3] [--out FILE]"""
@@ -26,13 +34,16 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 EXE = os.path.join(REPO, "build", "c", "asio_scale")
 
 
-def run(target, threads, blocks, L, secs, mode="pageable", timeout=150):
+def run(target, threads, blocks, L, secs, mode="pageable", timeout=150, env=None, tag=None):
     cmd = [EXE, target, str(threads), str(blocks), str(L), str(secs), mode]
     t0 = time.time()
-    out = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout)
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout,
+                         env=dict(os.environ, **(env or {})))
     line = out.stdout.strip().splitlines()[-1] if out.stdout.strip() else "{}"
     rec = json.loads(line)
     rec["exit"] = out.returncode
+    if tag:
+        rec.update(tag)
     rec["run_s"] = round(time.time() - t0, 1)
     if out.returncode != 0:
         rec["stderr"] = out.stderr[-2000:]
@@ -42,7 +53,8 @@ def run(target, threads, blocks, L, secs, mode="pageable", timeout=150):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--matrix", choices=["threads", "chunk"], required=True)
+    ap.add_argument("--matrix", choices=["threads", "chunk", "bigchunk", "watch"], required=True)
+    ap.add_argument("--rounds", type=int, default=2)
     ap.add_argument("--secs", type=float, default=3.0)
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
@@ -52,6 +64,19 @@ def main():
             for target in ("batcher", "pool"):
                 for T in (8, 64, 256):
                     runs.append(run(target, T, 64, 16384, a.secs, mode))
+    elif a.matrix == "watch":
+        for r in range(a.rounds):
+            for target in ("batcher", "pool"):
+                for T in (8, 64, 256):
+                    for pol in ("spin", "tail", "block"):
+                        runs.append(run(target, T, 64, 16384, a.secs, "registered",
+                                        env={"MD5HIP_WATCH": pol}, tag={"watch": pol, "round": r}))
+    elif a.matrix == "bigchunk":
+        for L in (2 << 20, 4 << 20, 10 << 20):
+            for B in (1, 4, 8):
+                for T in (1, 8, 64):
+                    for target in ("batcher", "host"):
+                        runs.append(run(target, T, B, L, a.secs, timeout=300))
     else:
         for L in (16384, 131072, 1 << 20):
             for B in (8, 64):

@@ -51,6 +51,12 @@ class MD5HipPoolStats(ctypes.Structure):
     _fields_ = [(n, ctypes.c_uint64) for n in ("submissions", "routed_whole", "split", "parts")]
 
 
+class MD5HipPoolHealth(ctypes.Structure):
+    """struct md5hip_pool_health (include/md5hip.h, ABI 4)."""
+    _fields_ = [("ndev", ctypes.c_uint32), ("nfailed", ctypes.c_uint32),
+                ("failed_mask", ctypes.c_uint64), ("failovers", ctypes.c_uint64)]
+
+
 class MD5HipError(RuntimeError):
     def __init__(self, fn, rc):
         name = errno.errorcode.get(-rc, str(rc))
@@ -145,6 +151,11 @@ def lib():
         "nc_header_seal": (i, [vp]),
         "nc_header_verify": (i, [vp]),
         "md5hip_batch_verify_headers": (i, [vp, vp, u64, vp]),
+        "md5hip_batcher_health": (i, [vp]),
+        "md5hip_batcher_inject_fault": (i, [vp, u64]),
+        "md5hip_pool_get_health": (i, [vp, ctypes.POINTER(MD5HipPoolHealth)]),
+        "md5hip_pool_device_health": (i, [vp, u32]),
+        "md5hip_pool_inject_fault": (i, [vp, u32, u64]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -179,7 +190,9 @@ EXPORTS = ["MD5Init", "MD5Update", "MD5Final", "nc_MD5Init", "nc_MD5Update", "nc
            "md5hip_final_ctx", "md5hip_pool_set_split", "md5hip_pool_submit_async",
            "md5hip_pool_submit_iov_async", "md5hip_pool_wait", "md5hip_pool_poll",
            "md5hip_pool_get_stats", "md5hip_pool_device_stats", "md5_batch_submit_device_on",
-           "md5_batch_submit_device_after", "md5hip_plan_desc_at", "md5hip_batcher_set_chain"]
+           "md5_batch_submit_device_after", "md5hip_plan_desc_at", "md5hip_batcher_set_chain",
+           "md5hip_batcher_health", "md5hip_batcher_inject_fault", "md5hip_pool_get_health",
+           "md5hip_pool_device_health", "md5hip_pool_inject_fault"]
 
 
 def check(fn, rc):

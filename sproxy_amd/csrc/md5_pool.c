@@ -21,6 +21,12 @@
  * counters, the multi-part ticket table) and is never held across a batcher
  * call that waits for the device.  No thread is created per call.
  *
+ * Failed devices (md5hip_batcher_health): never routed to.  A part that
+ * finds its device failed before the device took it (-ENODEV) goes to
+ * another; a synchronous submission or part whose launch failed with its
+ * device is resubmitted on a healthy one from the caller's buffers (still
+ * valid: the call has not returned); an asynchronous ticket keeps its -EIO.
+ *
  * Tickets: a submission routed whole is (batcher ticket << 6) | device; a
  * split one is bit 63 | id, its parts kept in `mt` (ascending ids) until all
  * of them have completed, then dropped (an error is kept in `failed`).
@@ -59,6 +65,7 @@ struct md5hip_pool {
     uint64_t split_bytes;             /* 0 = one batcher slice */
     uint32_t rr;                      /* rotating start for ties */
     struct md5hip_pool_stats st;
+    uint64_t st_failovers;            /* md5hip_pool_health.failovers */
     /* split tickets still running, ascending ids; [mt_lo, mt_lo + mt_n) of a ring */
     struct mt_entry **mt;
     uint64_t mt_cap, mt_lo, mt_n, mt_next;
@@ -176,6 +183,34 @@ int md5hip_pool_device_stats(md5hip_pool *p, uint32_t g, struct md5hip_batcher_s
     return md5hip_batcher_get_stats(p->b[g], out);
 }
 
+int md5hip_pool_device_health(md5hip_pool *p, uint32_t g)
+{
+    if (!p || g >= p->ndev) return -EINVAL;
+    return md5hip_batcher_health(p->b[g]);
+}
+
+int md5hip_pool_get_health(md5hip_pool *p, struct md5hip_pool_health *out)
+{
+    if (!p || !out) return -EINVAL;
+    memset(out, 0, sizeof *out);
+    out->ndev = p->ndev;
+    for (uint32_t g = 0; g < p->ndev; g++)
+        if (md5hip_batcher_health(p->b[g])) {
+            out->nfailed++;
+            if (g < 64) out->failed_mask |= 1ull << g;
+        }
+    pthread_mutex_lock(&p->mu);
+    out->failovers = p->st_failovers;
+    pthread_mutex_unlock(&p->mu);
+    return 0;
+}
+
+int md5hip_pool_inject_fault(md5hip_pool *p, uint32_t g, uint64_t after)
+{
+    if (!p || g >= p->ndev) return -EINVAL;
+    return md5hip_batcher_inject_fault(p->b[g], after);
+}
+
 /* ------------------------------------------------------------------------
  * Routing
  * ------------------------------------------------------------------------ */
@@ -184,25 +219,33 @@ static uint64_t dev_load(md5hip_pool *p, uint32_t g)
     return md5hip_batcher_load(p->b[g]) + __atomic_load_n(&p->claim[g], __ATOMIC_RELAXED);
 }
 
-/* The k least-loaded devices (ties from a rotating start), their weight w
- * claimed on each; into sel[0..k). */
-static void route(md5hip_pool *p, uint32_t k, const uint64_t *w, uint32_t *sel)
+static int dev_ok(md5hip_pool *p, uint32_t g) { return md5hip_batcher_health(p->b[g]) == 0; }
+
+/* The k least-loaded healthy devices (ties from a rotating start), their
+ * weight w claimed on each; into sel[0..k).  Returns how many were chosen:
+ * fewer than k when fewer devices are healthy (0: every device failed). */
+static uint32_t route(md5hip_pool *p, uint32_t k, const uint64_t *w, uint32_t *sel)
 {
     const uint32_t G = p->ndev;
     const uint32_t r0 = __atomic_fetch_add(&p->rr, 1, __ATOMIC_RELAXED);
     uint64_t load[POOL_MAX_DEV];
-    int used[POOL_MAX_DEV] = {0};
-    for (uint32_t g = 0; g < G; g++) load[g] = dev_load(p, g);
+    int used[POOL_MAX_DEV];
+    for (uint32_t g = 0; g < G; g++) {
+        used[g] = !dev_ok(p, g);                      /* a failed device is never picked */
+        load[g] = dev_load(p, g);
+    }
     for (uint32_t j = 0; j < k; j++) {
         uint32_t best = G;
         for (uint32_t q = 0; q < G; q++) {
             const uint32_t g = (r0 + q) % G;
             if (!used[g] && (best == G || load[g] < load[best])) best = g;
         }
+        if (best == G) return j;
         used[best] = 1;
         sel[j] = best;
         __atomic_fetch_add(&p->claim[best], w[j], __ATOMIC_RELAXED);
     }
+    return k;
 }
 
 static void unclaim(md5hip_pool *p, uint32_t g, uint64_t w)
@@ -363,6 +406,41 @@ static uint64_t src_weight(const struct pool_src *s, uint64_t i)
     return chunk_weight(L);
 }
 
+static void count_failover(md5hip_pool *p)
+{
+    pthread_mutex_lock(&p->mu);
+    p->st_failovers++;
+    pthread_mutex_unlock(&p->mu);
+}
+
+/* Chunks [lo, hi) whole to one healthy device (weight w): *g, *t its device
+ * and ticket.  sync: waited here, and resubmitted elsewhere while the launch
+ * failed because its device did (the caller's buffers are still valid).
+ * Either way a device that failed before taking the chunks (-ENODEV) is
+ * left for another.  -ENODEV once no device is healthy. */
+static int submit_range(md5hip_pool *p, int kind, uint32_t fastcrc, const struct pool_src *s,
+                        uint64_t lo, uint64_t hi, uint64_t w, unsigned char *digests, int sync,
+                        uint32_t *g_out, uint64_t *t_out)
+{
+    for (;;) {
+        uint32_t g;
+        if (!route(p, 1, &w, &g)) return -ENODEV;     /* every device failed */
+        /* asynchronous even for a synchronous caller, so the claim ends as
+         * soon as the batcher holds the chunks (its own load counts them) */
+        uint64_t t = 0;
+        int rc = part_submit(p, g, kind, fastcrc, s, lo, hi, digests, &t, sync);
+        unclaim(p, g, w);
+        if (rc == 0 && sync) rc = md5_batch_wait(p->b[g], t);
+        if ((rc == -ENODEV || (sync && rc == -EIO)) && !dev_ok(p, g)) {
+            count_failover(p);                        /* moved off the failed device */
+            continue;
+        }
+        *g_out = g;
+        *t_out = t;
+        return rc;
+    }
+}
+
 /* ticket NULL = synchronous; kind < 0 = the pool's current digest kind */
 static int pool_submit(md5hip_pool *p, const struct pool_src *s, uint64_t n, unsigned char *digests,
                        uint64_t *ticket, int kind, uint32_t fastcrc)
@@ -379,31 +457,30 @@ static int pool_submit(md5hip_pool *p, const struct pool_src *s, uint64_t n, uns
     pthread_mutex_unlock(&p->mu);
     if (split == 0) split = md5hip_batcher_slice(p->b[0]);
     const uint32_t dsz = kind == MD5HIP_DIGEST_CRC32 ? 4 : 16;
+    const int sync = ticket == NULL;
     uint64_t total = 0;
     if (s->kind == SRC_FIXED) {
         total = n * chunk_weight(s->len);
     } else {
         for (uint64_t i = 0; i < n; i++) total += src_weight(s, i);
     }
+    uint32_t healthy = 0;
+    for (uint32_t g = 0; g < p->ndev; g++) healthy += dev_ok(p, g);
+    if (healthy == 0) return -ENODEV;
     uint32_t k = 1;
-    if (total > split && p->ndev > 1) {
+    if (total > split && healthy > 1) {
         const uint64_t want = (total + split - 1) / split;
-        k = want < p->ndev ? (uint32_t)want : p->ndev;
+        k = want < healthy ? (uint32_t)want : healthy;
         if (k > n) k = (uint32_t)n;
     }
     if (k == 1) {                                     /* the common case: whole */
-        uint32_t g;
-        route(p, 1, &total, &g);
-        /* asynchronous even for a synchronous caller, so the claim ends as
-         * soon as the batcher holds the chunks (its own load counts them) */
+        uint32_t g = 0;
         uint64_t t = 0;
-        int rc = part_submit(p, g, kind, fastcrc, s, 0, n, digests, &t, ticket == NULL);
-        unclaim(p, g, total);
+        const int rc = submit_range(p, kind, fastcrc, s, 0, n, total, digests, sync, &g, &t);
         pthread_mutex_lock(&p->mu);
         p->st.routed_whole++;
         p->st.parts++;
         pthread_mutex_unlock(&p->mu);
-        if (rc == 0 && !ticket) rc = md5_batch_wait(p->b[g], t);
         if (ticket && rc == 0 && t) *ticket = (t << 6) | g;
         return rc;
     }
@@ -427,18 +504,32 @@ static int pool_submit(md5hip_pool *p, const struct pool_src *s, uint64_t n, uns
         else for (uint64_t i = first[j]; i < first[j + 1]; i++) w[j] += src_weight(s, i);
     }
     uint32_t sel[POOL_MAX_DEV];
-    route(p, k, w, sel);
+    const uint32_t got = route(p, k, w, sel);         /* < k: a device failed since the count */
     struct mt_entry *e = malloc(sizeof *e + k * sizeof(struct mt_part));
     int rc = e ? 0 : -ENOMEM;
     uint32_t np = 0;
+    uint32_t pj[POOL_MAX_DEV];                        /* part index of each submitted part */
     for (uint32_t j = 0; j < k; j++) {
         if (rc == 0 && first[j + 1] > first[j]) {
             uint64_t t = 0;
-            rc = part_submit(p, sel[j], kind, fastcrc, s, first[j], first[j + 1],
-                             digests + (size_t)dsz * first[j], &t, ticket == NULL);
-            if (rc == 0 && t) e->part[np++] = (struct mt_part){sel[j], t};
+            uint32_t g = j < got ? sel[j] : 0;
+            int r = j < got ? part_submit(p, g, kind, fastcrc, s, first[j], first[j + 1],
+                                          digests + (size_t)dsz * first[j], &t, sync)
+                            : -ENODEV;
+            if (r == -ENODEV && (j >= got || !dev_ok(p, g))) {
+                if (j < got) count_failover(p);
+                /* its device failed before taking the part: any healthy one
+                 * (submitted asynchronously like the others; waited below) */
+                r = submit_range(p, kind, fastcrc, s, first[j], first[j + 1], w[j],
+                                 digests + (size_t)dsz * first[j], 0, &g, &t);
+            }
+            rc = r;
+            if (rc == 0 && t) {
+                pj[np] = j;
+                e->part[np++] = (struct mt_part){g, t};
+            }
         }
-        unclaim(p, sel[j], w[j]);
+        if (j < got) unclaim(p, sel[j], w[j]);
     }
     pthread_mutex_lock(&p->mu);
     p->st.split++;
@@ -446,11 +537,20 @@ static int pool_submit(md5hip_pool *p, const struct pool_src *s, uint64_t n, uns
     pthread_mutex_unlock(&p->mu);
     if (!e) return rc;
     e->nparts = np;
-    if (rc || !ticket) {
+    if (rc || sync) {
         /* synchronous, or a part failed: the submitted parts finish before
-         * the caller may reuse its buffers */
-        for (uint32_t j = 0; j < np; j++) {
-            const int r = md5_batch_wait(p->b[e->part[j].dev], e->part[j].t);
+         * the caller may reuse its buffers.  Synchronously, a part whose
+         * launch failed with its device goes again on a healthy one. */
+        for (uint32_t q = 0; q < np; q++) {
+            int r = md5_batch_wait(p->b[e->part[q].dev], e->part[q].t);
+            if (sync && rc == 0 && (r == -EIO || r == -ENODEV) && !dev_ok(p, e->part[q].dev)) {
+                const uint32_t j = pj[q];
+                uint32_t g;
+                uint64_t t;
+                count_failover(p);
+                r = submit_range(p, kind, fastcrc, s, first[j], first[j + 1], w[j],
+                                 digests + (size_t)dsz * first[j], 1, &g, &t);
+            }
             if (r && !rc) rc = r;
         }
         free(e);

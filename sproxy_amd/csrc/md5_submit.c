@@ -36,6 +36,16 @@
  * Errors: 0 / negative errno (include/md5hip.h); -E2BIG when one chunk
  * exceeds the slot's staging; -EFAULT when registered memory vanished
  * under a zero-copy submission.
+ *
+ * Device failure.  blk_make_crc cannot fail (blk_io.c:354-430); this can.
+ * A launch whose completion event reports an error, or an enqueue failure
+ * after which the slot's stream reports one, marks the batcher FAILED
+ * (sticky): that launch's tickets get -EIO, tickets still coalescing in the
+ * open slot and every later submission get -ENODEV at once, and nothing is
+ * enqueued on the device again.  Launches already in flight complete as
+ * their events say.  No digest of a failed launch is delivered.  The pool
+ * (md5_pool.c) routes around a failed batcher; what the call site does with
+ * -EIO / -ENODEV is INTEGRATION.md §2j.
  */
 #include <errno.h>
 #include <pthread.h>
@@ -244,8 +254,11 @@ struct slot {
     /* a synchronous caller's chunks are here: the slot goes while a slot is
      * left over to coalesce the callers behind it (slot_try_launch) */
     int urgent;
+    /* md5hip_batcher_inject_fault: this launch completes as a device fault */
+    int inject;
 };
 enum { WATCH_NONE = 0, WATCH_ACTIVE, WATCH_GAVE_UP };
+enum watch_policy { WATCH_POLICY_SPIN = 0, WATCH_POLICY_TAIL = 1, WATCH_POLICY_BLOCK = 2 };
 
 struct md5hip_batcher {
     int device;
@@ -275,6 +288,9 @@ struct md5hip_batcher {
     int poll_fast;            /* the progress thread polls launches every 10 us now */
     int chain;                /* chain the open slot behind the running launch: 0 off, 1 on, 2 (default) on + BALANCED tails overlap */
     hipEvent_t after_ev;     /* recorded on a producer's stream (md5_batch_submit_device_on) */
+    int failed;               /* 0, or -ENODEV once the device failed (sticky; read lock-free by the pool) */
+    int watch_policy;         /* enum watch_policy (watch_launch), MD5HIP_WATCH at create */
+    uint64_t inject_at;       /* md5hip_batcher_inject_fault: launch number that faults, 0 = none */
 };
 
 #define CK(x) do { if ((x) != hipSuccess) { rc = -ENODEV; goto fail; } } while (0)
@@ -402,8 +418,8 @@ static int slot_enqueue(md5hip_batcher *b, struct slot *sl)
     int rc = 0;
     const uint64_t n = sl->n;
     if (sl->mode == MODE_FIXED) {
-        if (hipMemcpyAsync(sl->d_data, sl->fx_src, sl->fx_bytes, hipMemcpyHostToDevice, sl->stream))
-            return -EIO;
+        /* the bytes are on their way already (host_fixed enqueued the copy
+         * on this stream outside b->mu) */
         if (sl->chain_ev && hipStreamWaitEvent(sl->stream, sl->chain_ev, 0) != hipSuccess) return -EIO;
         rc = sl->kind == MD5HIP_DIGEST_CRC32
                  ? crc32hip_fixed(sl->d_data, n, sl->fx_len, sl->fx_stride, sl->fastcrc,
@@ -512,6 +528,7 @@ static void slot_reset(struct slot *sl)
     sl->chain_at = 0;
     sl->chain_overlap = 0;
     sl->urgent = 0;
+    sl->inject = 0;
     sl->mode = MODE_NONE;
     sl->writers = sl->full = sl->flush = sl->err = sl->direct = 0;
     sl->n = sl->used = sl->nseg = sl->ndma = sl->ndsc = 0;
@@ -540,13 +557,69 @@ static void slot_retire(md5hip_batcher *b, struct slot *sl, int err)
     sl->load = 0;
     if (sl->state == SLOT_INFLIGHT) {
         b->inflight--;
-        const uint64_t t = now_us();               /* a chained launch's start is estimated */
-        const double d = t > sl->launched_us ? (double)(t - sl->launched_us) : 0.0;
-        b->launch_ema_us = b->launch_ema_us > 0 ? 0.75 * b->launch_ema_us + 0.25 * d : d;
+        /* a chained launch's start is estimated (chain_at): one that retires
+         * before it (a BALANCED overlap started early) gives no sample */
+        const uint64_t t = now_us();
+        if (t > sl->launched_us) {
+            const double d = (double)(t - sl->launched_us);
+            b->launch_ema_us = b->launch_ema_us > 0 ? 0.75 * b->launch_ema_us + 0.25 * d : d;
+        }
     }
     slot_reset(sl);
     if (sl->nwait) pthread_cond_broadcast(&sl->cv);   /* its waiters only */
     pthread_cond_broadcast(&b->done_cv);              /* slot_take / drain / destroy */
+}
+
+/* Is the device behind this HIP status gone (a fault, a lost or reset
+ * device) rather than the call merely refused?  Completion events report
+ * only these; an enqueue error is classified by the stream's state after it. */
+static int hip_lost(hipError_t e)
+{
+    switch (e) {
+    case hipSuccess: case hipErrorNotReady:
+    case hipErrorInvalidValue: case hipErrorOutOfMemory: case hipErrorInvalidDevicePointer:
+    case hipErrorInvalidMemcpyDirection: case hipErrorInvalidConfiguration:
+    case hipErrorInvalidResourceHandle: case hipErrorNotSupported:
+        return 0;
+    default:
+        return 1;
+    }
+}
+
+/* The device failed (mu held): sticky.  Tickets coalescing in the open slot
+ * are retired with -ENODEV (or when their writers are done: sl->err); slots
+ * in flight finish as their events say; callers blocked on a slot are woken
+ * by its retire, everything waiting for a free slot by done_cv. */
+static void batcher_fail(md5hip_batcher *b)
+{
+    if (b->failed) return;
+    __atomic_store_n(&b->failed, -ENODEV, __ATOMIC_RELEASE);
+    b->inject_at = 0;
+    for (uint32_t k = 0; k < b->nslots; k++) {
+        struct slot *sl = &b->s[k];
+        if (sl->state != SLOT_OPEN) continue;
+        if (b->open == (int)k) b->open = -1;
+        sl->full = 1;
+        if (!sl->err) sl->err = -ENODEV;
+        if (!sl->writers) slot_retire(b, sl, sl->err);
+    }
+    pthread_cond_broadcast(&b->done_cv);
+    pthread_cond_broadcast(&b->work_cv);
+}
+
+/* A launch's completion (mu not needed): its event, or the injected fault
+ * once the launch has really finished. */
+static hipError_t launch_status(hipEvent_t ev, int inject)
+{
+    const hipError_t e = hipEventQuery(ev);
+    return e == hipSuccess && inject ? hipErrorLaunchFailure : e;
+}
+
+/* Retire in-flight slot `sl` whose completion status is `e` (mu held). */
+static void slot_complete(md5hip_batcher *b, struct slot *sl, hipError_t e)
+{
+    slot_retire(b, sl, e == hipSuccess ? 0 : -EIO);
+    if (e != hipSuccess) batcher_fail(b);
 }
 
 /* Launch slot `sl` if it may go now (mu held). */
@@ -572,10 +645,17 @@ static void slot_try_launch(md5hip_batcher *b, struct slot *sl)
         return;
     }
     if (b->open == (int)(sl - b->s)) b->open = -1;
-    const int rc = sl->err ? sl->err : slot_enqueue(b, sl);
+    const int rc = sl->err ? sl->err : b->failed ? b->failed : slot_enqueue(b, sl);
     if (rc) {
+        /* an enqueue that failed because the device did: the stream says so */
+        const int lost = !sl->err && !b->failed && hip_lost(hipStreamQuery(sl->stream));
         slot_retire(b, sl, rc);
+        if (lost) batcher_fail(b);
         return;
+    }
+    if (b->inject_at && b->st.launches + 1 == b->inject_at) {
+        sl->inject = 1;
+        b->inject_at = 0;
     }
     sl->state = SLOT_INFLIGHT;
     sl->launched_us = now_us();
@@ -673,9 +753,9 @@ static void *progress_main(void *arg)
         for (uint32_t k = 0; k < b->nslots; k++) {
             struct slot *sl = &b->s[k];
             if (sl->state != SLOT_INFLIGHT) continue;
-            const hipError_t e = hipEventQuery(sl->done);
+            const hipError_t e = launch_status(sl->done, sl->inject);
             if (e == hipErrorNotReady) continue;
-            slot_retire(b, sl, e == hipSuccess ? 0 : -EIO);
+            slot_complete(b, sl, e);
             any = 1;
         }
         if (any) {
@@ -772,7 +852,8 @@ static void *progress_main(void *arg)
  * every state change that ends one (retire, launch) is made under b->mu and
  * broadcast or signalled, so no wake-up is lost.
  * ------------------------------------------------------------------------ */
-enum { WATCH_SPIN_US = 300, WATCH_LEAD_US = 200 };
+enum { WATCH_SPIN_US = 300, WATCH_LEAD_US = 200 };   /* WATCH_POLICY_SPIN */
+enum { WATCH_TAIL_US = 50 };                           /* WATCH_POLICY_TAIL */
 
 static void cpu_relax(void)
 {
@@ -781,25 +862,53 @@ static void cpu_relax(void)
 #endif
 }
 
-/* Watch in-flight slot `sl` (mu held on entry and exit, watch == NONE). */
+/* The watcher's sleep on the slot's condition variable until `us` from now
+ * ends within a few us of its deadline, not the default 50 us timer slack
+ * later (the caller's own slack is put back after). */
+static void watch_sleep(md5hip_batcher *b, struct slot *sl, uint64_t us)
+{
+    const int old = prctl(PR_GET_TIMERSLACK, 0, 0, 0, 0);
+    if (old > 2000) (void)prctl(PR_SET_TIMERSLACK, 2000UL, 0, 0, 0);
+    sl->nwait++;
+    wait_cv_us(b, &sl->cv, us);
+    sl->nwait--;
+    if (old > 2000) (void)prctl(PR_SET_TIMERSLACK, (unsigned long)old, 0, 0, 0);
+}
+
+/* Watch in-flight slot `sl` (mu held on entry and exit, watch == NONE).
+ * The policy (b->watch_policy, MD5HIP_WATCH at create):
+ *   SPIN   round 4: a launch due within 300 us is polled for up to 500 us
+ *          (a longer one slept through until 200 us before its end); past
+ *          that the watcher gives up and the progress thread retires it;
+ *   TAIL   sleep until 50 us before the launch is due, poll for at most
+ *          50 us, then block in hipEventSynchronize on the blocking-sync
+ *          event (the thread sleeps until the completion interrupt);
+ *   BLOCK  hipEventSynchronize at once. */
 static void watch_launch(md5hip_batcher *b, struct slot *sl)
 {
     const uint64_t gen = sl->gen;
+    const int pol = b->watch_policy;
+    const uint64_t spin = pol == WATCH_POLICY_SPIN ? WATCH_SPIN_US : WATCH_TAIL_US;
+    const uint64_t lead = pol == WATCH_POLICY_SPIN ? WATCH_LEAD_US : WATCH_TAIL_US;
     sl->watch = WATCH_ACTIVE;
-    for (;;) {                                  /* long launch: sleep most of it */
+    for (; pol != WATCH_POLICY_BLOCK;) {        /* long launch: sleep most of it */
         const uint64_t now = now_us(), end = sl->launched_us + (uint64_t)b->launch_ema_us;
-        if (end <= now + WATCH_SPIN_US) break;
-        sl->nwait++;
-        wait_cv_us(b, &sl->cv, end - now - WATCH_LEAD_US);
-        sl->nwait--;
+        if (end <= now + spin) break;
+        watch_sleep(b, sl, end - now - lead);
         if (sl->state != SLOT_INFLIGHT || sl->gen != gen) return;     /* retired meanwhile */
     }
     const hipEvent_t ev = sl->done;
+    const int inject = sl->inject;
     pthread_mutex_unlock(&b->mu);
-    hipError_t e;
-    const uint64_t t0 = now_us();
-    while ((e = hipEventQuery(ev)) == hipErrorNotReady && now_us() - t0 < WATCH_SPIN_US + WATCH_LEAD_US)
-        cpu_relax();
+    hipError_t e = hipErrorNotReady;
+    if (pol != WATCH_POLICY_BLOCK) {
+        const uint64_t t0 = now_us(), limit = pol == WATCH_POLICY_SPIN ? WATCH_SPIN_US + WATCH_LEAD_US : WATCH_TAIL_US;
+        while ((e = launch_status(ev, inject)) == hipErrorNotReady && now_us() - t0 < limit) cpu_relax();
+    }
+    if (e == hipErrorNotReady && pol != WATCH_POLICY_SPIN) {
+        e = hipEventSynchronize(ev);
+        if (e == hipSuccess && inject) e = hipErrorLaunchFailure;
+    }
     pthread_mutex_lock(&b->mu);
     /* the same launch still in flight? (the progress thread may have retired
      * it, and the slot may even be in flight again with other work: then
@@ -809,7 +918,7 @@ static void watch_launch(md5hip_batcher *b, struct slot *sl)
         sl->watch = WATCH_GAVE_UP;              /* nobody spins on it again */
         return;
     }
-    slot_retire(b, sl, e == hipSuccess ? 0 : -EIO);
+    slot_complete(b, sl, e);
     if (b->open >= 0) slot_try_launch(b, &b->s[b->open]);
     pthread_cond_broadcast(&b->work_cv);
 }
@@ -937,6 +1046,16 @@ static int batcher_new(int device, uint64_t slice_bytes, uint32_t nslots, uint64
     b->linger_max_us = 5000;
     b->chain = 2;
     b->open = -1;
+    {
+        const char *w = getenv("MD5HIP_WATCH");      /* spin / tail / block (A/B of the watcher) */
+        b->watch_policy = !w ? WATCH_POLICY_TAIL
+                        : !strcmp(w, "spin") ? WATCH_POLICY_SPIN
+                        : !strcmp(w, "block") ? WATCH_POLICY_BLOCK : WATCH_POLICY_TAIL;
+    }
+    /* blocking-sync completion events: a watcher that blocks on one sleeps
+     * until the interrupt instead of polling the signal */
+    const unsigned done_flags = hipEventDisableTiming |
+                                (b->watch_policy == WATCH_POLICY_SPIN ? 0u : hipEventBlockingSync);
     b->s = calloc(nslots, sizeof *b->s);
     /* ticket 0 = "nothing": complete at once */
     if (!b->s || tk_ring_init(&b->tk, 1)) { rc = -ENOMEM; goto fail; }
@@ -945,7 +1064,7 @@ static int batcher_new(int device, uint64_t slice_bytes, uint32_t nslots, uint64
     for (uint32_t k = 0; k < nslots; k++) {
         struct slot *sl = &b->s[k];
         CK(hipStreamCreateWithFlags(&sl->stream, hipStreamNonBlocking));
-        CK(hipEventCreateWithFlags(&sl->done, hipEventDisableTiming));
+        CK(hipEventCreateWithFlags(&sl->done, done_flags));
         CK(hipEventCreateWithFlags(&sl->kdone, hipEventDisableTiming));
         CK(hipHostMalloc((void **)&sl->h_data, b->cap, hipHostMallocDefault));
         /* fine-grained: a small slot's kernel reads them in place (slot_prepare) */
@@ -1090,11 +1209,27 @@ int md5hip_batcher_set_linger(md5hip_batcher *b, uint32_t max_us)
 
 int md5hip_batcher_set_chain(md5hip_batcher *b, int mode)
 {
-    if (!b) return -EINVAL;
+    if (!b || mode < 0 || mode > 2) return -EINVAL;
     pthread_mutex_lock(&b->mu);
-    b->chain = mode >= 2 ? 2 : mode != 0;
+    b->chain = mode;
     pthread_mutex_unlock(&b->mu);
     return 0;
+}
+
+int md5hip_batcher_health(const md5hip_batcher *b)
+{
+    if (!b) return -EINVAL;
+    return __atomic_load_n(&b->failed, __ATOMIC_ACQUIRE);
+}
+
+int md5hip_batcher_inject_fault(md5hip_batcher *b, uint64_t after)
+{
+    if (!b) return -EINVAL;
+    pthread_mutex_lock(&b->mu);
+    int rc = b->failed;
+    if (!rc) b->inject_at = after ? b->st.launches + after : 0;
+    pthread_mutex_unlock(&b->mu);
+    return rc;
 }
 
 int md5hip_batcher_get_stats(md5hip_batcher *b, struct md5hip_batcher_stats *out)
@@ -1420,7 +1555,7 @@ static int submit(md5hip_batcher *b, const struct chunk_src *src, uint64_t n, un
         kind = b->kind;
         fastcrc = b->fastcrc;
     }
-    rc = tk_new(b, &t);
+    rc = b->failed ? b->failed : tk_new(b, &t);
     if (rc == 0 && after && hipEventRecord(b->after_ev, *after) != hipSuccess) {
         tk_put(b, t, 0);
         rc = -EINVAL;                              /* not a stream of this device */
@@ -1434,7 +1569,12 @@ static int submit(md5hip_batcher *b, const struct chunk_src *src, uint64_t n, un
     const uint32_t dsz = kind == MD5HIP_DIGEST_CRC32 ? 4 : 16;
     uint64_t i = 0;
     while (i < n) {
-        struct slot *sl = slot_open(b, mode, kind, fastcrc);
+        struct slot *sl = b->failed ? NULL : slot_open(b, mode, kind, fastcrc);
+        if (!sl || b->failed) {              /* the device failed meanwhile (slot_open may wait) */
+            if (sl) slot_try_launch(b, sl);  /* an empty slot it opened retires */
+            rc = -ENODEV;
+            break;
+        }
         const uint64_t at = sl->n;
         const uint64_t lo = sl->used;
         const long got = reserve(b, sl, src, i, n, zc);
@@ -1685,7 +1825,7 @@ static int host_fixed(md5hip_batcher *b, int kind, uint32_t fastcrc, const void 
     }
     const uint32_t dsz = kind == MD5HIP_DIGEST_CRC32 ? 4 : 16;
     uint64_t t = 0;
-    int rc = tk_new(b, &t);
+    int rc = b->failed ? b->failed : tk_new(b, &t);
     if (rc) {
         pthread_mutex_unlock(&b->mu);
         dev_leave(&g);
@@ -1696,7 +1836,12 @@ static int host_fixed(md5hip_batcher *b, int kind, uint32_t fastcrc, const void 
         const uint64_t m = n - i < per ? n - i : per;
         /* straight from the caller's (ideally pinned) buffer: no host gather,
          * a slot of its own (the open slot keeps coalescing other work) */
-        struct slot *sl = slot_take(b, MODE_FIXED, kind, fastcrc);
+        struct slot *sl = b->failed ? NULL : slot_take(b, MODE_FIXED, kind, fastcrc);
+        if (!sl || b->failed) {              /* the device failed (slot_take may wait) */
+            if (sl) slot_retire(b, sl, -ENODEV);
+            rc = -ENODEV;
+            break;
+        }
         sl->n = m;
         sl->fx_src = src + i * stride;
         sl->fx_bytes = (m - 1) * stride + len;
@@ -1710,6 +1855,19 @@ static int host_fixed(md5hip_batcher *b, int kind, uint32_t fastcrc, const void 
             break;
         }
         tk_ring_ref(&b->tk, t);
+        /* the H2D copy outside the lock, the slot held by this writer: from
+         * pageable memory it is synchronous (a 128 MiB slice is tens of ms
+         * over PCIe), and every other submitter and waiter needs b->mu
+         * meanwhile.  Nothing else touches a FIXED slot's stream until its
+         * writers are done (slot_try_launch waits for writers == 0). */
+        sl->writers++;
+        pthread_mutex_unlock(&b->mu);
+        const hipError_t ce = hipMemcpyAsync(sl->d_data, sl->fx_src, sl->fx_bytes, hipMemcpyHostToDevice,
+                                             sl->stream);
+        pthread_mutex_lock(&b->mu);
+        sl->writers--;
+        if (ce != hipSuccess && !sl->err) sl->err = -EIO;
+        if (ce != hipSuccess && hip_lost(hipStreamQuery(sl->stream))) batcher_fail(b);
         slot_try_launch(b, sl);
     }
     tk_put(b, t, rc);

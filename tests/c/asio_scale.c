@@ -30,6 +30,12 @@
  * over the timed window (CLOCK_PROCESS_CPUTIME_ID, which includes the
  * batchers' progress threads and the HIP runtime's) is reported per call too.  Prints one JSON object.
  *
+ * ASIO_FIXED_BG_MIB=M (batcher target): one more thread calls
+ * md5hip_batch_host_fixed on an M MiB PAGEABLE array of 16 KiB chunks over
+ * and over during the timed window (its H2D copy is synchronous from pageable
+ * memory); its call times are reported as "bg_fixed" and its digests checked
+ * -- the submitters' latency must not include that copy.
+ *
  * usage: asio_scale TARGET THREADS BLOCKS BLOCK_BYTES SECS [MODE [SLICE_MIB NSLOTS]]
  * Exit 0 = every digest equal to the oracle's; 1 = a mismatch or error;
  * 77 = no usable HIP device.
@@ -174,6 +180,40 @@ static void *worker(void *arg)
     return NULL;
 }
 
+/* ASIO_FIXED_BG_MIB: host_fixed over a pageable array beside the callers */
+struct bg {
+    size_t bytes;
+    unsigned char *buf;
+    unsigned char (*want)[16], (*got)[16];
+    double *lat;
+    size_t ncalls, cap;
+    int rc, bad;
+};
+static struct bg g_bg;
+
+static void *bg_fixed(void *arg)
+{
+    struct bg *g = arg;
+    const uint64_t n = g->bytes / 16384;
+    pthread_barrier_wait(&g_go);
+    const double t_end = g_t_end;
+    while (!g->rc && now() < t_end) {
+        memset(g->got, 0, 16 * n);
+        const double t0 = now();
+        const int rc = md5hip_batch_host_fixed(g_b, g->buf, n, 16384, 16384, &g->got[0][0]);
+        const double t1 = now();
+        if (rc) { g->rc = rc; break; }
+        g->bad += memcmp(g->got, g->want, 16 * n) != 0;
+        if (g->ncalls == g->cap) {
+            g->cap = g->cap ? 2 * g->cap : 256;
+            g->lat = realloc(g->lat, sizeof(double) * g->cap);
+            if (!g->lat) { g->rc = -ENOMEM; break; }
+        }
+        g->lat[g->ncalls++] = (t1 - t0) * 1e6;
+    }
+    return NULL;
+}
+
 static int cmp_d(const void *a, const void *b)
 {
     const double x = *(const double *)a, y = *(const double *)b;
@@ -223,11 +263,27 @@ int main(int argc, char **argv)
         printf("{\"error\": \"create\", \"rc\": %d}\n", rc);
         return 1;
     }
+    {
+        const char *e = getenv("ASIO_FIXED_BG_MIB");
+        if (e && g_b) g_bg.bytes = (size_t)atoi(e) << 20;
+    }
+    pthread_t bg_th;
+    if (g_bg.bytes) {
+        const uint64_t n = g_bg.bytes / 16384;
+        g_bg.buf = malloc(g_bg.bytes);                     /* pageable */
+        g_bg.want = malloc(16 * n);
+        g_bg.got = malloc(16 * n);
+        if (!g_bg.buf || !g_bg.want || !g_bg.got) return 1;
+        oracle_xorshift_fill(g_bg.buf, g_bg.bytes, 0xB6ull);
+        for (uint64_t i = 0; i < n; i++) oracle_md5(g_bg.buf + i * 16384, 16384, g_bg.want[i]);
+    }
+    const unsigned nbar = (unsigned)g_threads + 1 + (g_bg.bytes ? 1u : 0u);
     struct job *jobs = calloc((size_t)g_threads, sizeof *jobs);
     pthread_t *th = calloc((size_t)g_threads, sizeof *th);
     pthread_barrier_init(&g_start, NULL, (unsigned)g_threads + 1);
     pthread_barrier_init(&g_warm, NULL, (unsigned)g_threads + 1);
-    pthread_barrier_init(&g_go, NULL, (unsigned)g_threads + 1);
+    pthread_barrier_init(&g_go, NULL, nbar);
+    if (g_bg.bytes && pthread_create(&bg_th, NULL, bg_fixed, &g_bg)) return 1;
     pthread_attr_t at;
     pthread_attr_init(&at);
     pthread_attr_setstacksize(&at, 256u << 10);
@@ -246,6 +302,7 @@ int main(int argc, char **argv)
     g_t_end = w0 + g_secs;
     pthread_barrier_wait(&g_go);                  /* (the barrier orders g_t_end) */
     for (int t = 0; t < g_threads; t++) pthread_join(th[t], NULL);
+    if (g_bg.bytes) pthread_join(bg_th, NULL);
     const double wall = now() - w0, pcpu = process_cpu() - p0;
     getrusage(RUSAGE_SELF, &ru1);
     const double usr = (ru1.ru_utime.tv_sec - ru0.ru_utime.tv_sec) + (ru1.ru_utime.tv_usec - ru0.ru_utime.tv_usec) * 1e-6;
@@ -290,13 +347,23 @@ int main(int argc, char **argv)
            "\"process_cpu_us_per_call\": %.2f, \"process_cpu_cores\": %.2f, "
            "\"process_user_sys_us_per_call\": [%.2f, %.2f], \"gib_s\": %.3f, "
            "\"launches\": %llu, \"coalesced_launches\": %llu, \"max_tickets_per_launch\": %llu, "
-           "\"mismatches\": %d, \"rc\": %d}\n",
+           "\"mismatches\": %d, \"rc\": %d",
            argv[1], g_register ? "registered" : "pageable", g_nvec, g_threads, g_blocks, g_len, wall, total, pct(lat, total, 50), pct(lat, total, 90),
            pct(lat, total, 99), total ? lat[total - 1] : 0.0, total ? cpu_sum / (double)total : 0.0,
            pct(cpu, total, 50), pct(cpu, total, 99), total ? pcpu * 1e6 / (double)total : 0.0, pcpu / wall,
            total ? usr * 1e6 / (double)total : 0.0, total ? sys * 1e6 / (double)total : 0.0,
            bytes / wall / (double)(1u << 30), (unsigned long long)st.launches,
            (unsigned long long)st.coalesced_launches, (unsigned long long)st.max_tickets_per_launch, bad, err);
+    if (g_bg.bytes) {
+        qsort(g_bg.lat, g_bg.ncalls, sizeof *g_bg.lat, cmp_d);
+        printf(", \"bg_fixed\": {\"mib\": %zu, \"calls\": %zu, \"lat_us\": {\"min\": %.1f, \"p50\": %.1f, "
+               "\"max\": %.1f}, \"mismatches\": %d, \"rc\": %d}",
+               g_bg.bytes >> 20, g_bg.ncalls, g_bg.ncalls ? g_bg.lat[0] : 0.0, pct(g_bg.lat, g_bg.ncalls, 50),
+               g_bg.ncalls ? g_bg.lat[g_bg.ncalls - 1] : 0.0, g_bg.bad, g_bg.rc);
+        bad += g_bg.bad;
+        if (g_bg.rc && !err) err = g_bg.rc;
+    }
+    printf("}\n");
     if (g_b) md5hip_batcher_destroy(g_b);
     if (g_p) md5hip_pool_destroy(g_p);
     for (int t = 0; t < g_threads; t++) {

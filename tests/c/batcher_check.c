@@ -24,7 +24,14 @@
  * must return with correct digests within the round's deadline (the lost
  * wake-up of round 3 hung here).  Then large_device(): large
  * device-resident vectors, coalesced, with their device digests scattered
- * in pieces.  Exits 0 when every check holds.
+ * in pieces.  Then device_lost(): the failure policy (md5_submit.c header,
+ * md5_pool.c) -- a device lost after launch K, as its completion event
+ * reporting the fault and as the launch itself failing: the failing ticket
+ * gets -EIO, tickets coalescing behind it and every later call -ENODEV,
+ * nothing is enqueued on the device again, no caller hangs; a 2-device pool
+ * moves a synchronous submission off the failed device and never routes to
+ * it again; 8 threads at once while a device dies under them.
+ * Exits 0 when every check holds.
  */
 #include <errno.h>
 #include <pthread.h>
@@ -53,6 +60,8 @@ extern uint32_t fake_hip_fail_len;
 extern unsigned long fake_hip_wrong_device;
 extern int fake_hip_hold, fake_hip_slow_query;
 void fake_hip_mark_thread(void);
+void fake_hip_lose_device(int dev, int after_kernels, int how);
+int fake_hip_device_faulted(int dev);
 static int g_stop;
 #define STOPPED() __atomic_load_n(&g_stop, __ATOMIC_RELAXED)
 #define STOP() __atomic_store_n(&g_stop, 1, __ATOMIC_RELAXED)
@@ -481,6 +490,259 @@ static int large_device(void)
     return 0;
 }
 
+/* ------------------------------------------------------------ device lost */
+#define LCHECK(c, ...)                                                      \
+    do {                                                                    \
+        if (!(c)) {                                                         \
+            printf("FAIL device lost line %d: %s: ", __LINE__, #c);         \
+            printf(__VA_ARGS__);                                            \
+            printf("\n");                                                   \
+            return 1;                                                       \
+        }                                                                   \
+    } while (0)
+
+/* a random vector of small chunks from the registered heap */
+static int pick(uint64_t *s, int maxn, const void **ptrs, uint32_t *lens, int *idx)
+{
+    const int n = 1 + (int)(rnd(s) % (uint64_t)maxn);
+    for (int i = 0; i < n; i++) {
+        idx[i] = (int)(rnd(s) % NCH);
+        ptrs[i] = g_heap + g_offs[idx[i]];
+        lens[i] = g_lens[idx[i]];
+    }
+    return n;
+}
+
+/* one batcher: the launch that faults gives -EIO, the rest -ENODEV */
+static int lost_single(int dev, int how, int use_inject)
+{
+    md5hip_batcher *b;
+    int rc = md5hip_batcher_create(dev, 1u << 20, 3, &b);
+    LCHECK(rc == 0, "create %d", rc);
+    md5hip_batcher_set_chain(b, 0);
+    md5hip_batcher_set_inflight(b, 1);
+    uint64_t s = 77u + (uint64_t)dev;
+    const void *ptrs[MAXV];
+    uint32_t lens[MAXV];
+    int idx[MAXV];
+    unsigned char dig[MAXV][16], dig2[MAXV][16];
+    int n = pick(&s, 40, ptrs, lens, idx);
+    LCHECK((rc = md5_batch_submit(b, ptrs, lens, (uint64_t)n, &dig[0][0])) == 0 && check_md5(dig, idx, n),
+           "healthy submit %d", rc);
+    LCHECK(md5hip_batcher_health(b) == 0, "healthy");
+    /* E goes in flight (held), F coalesces behind it in the open slot */
+    __atomic_store_n(&fake_hip_hold, 1, __ATOMIC_RELAXED);
+    if (use_inject) LCHECK(md5hip_batcher_inject_fault(b, 1) == 0, "inject");
+    else fake_hip_lose_device(dev, 1, how);
+    uint64_t te, tf;
+    n = pick(&s, 40, ptrs, lens, idx);
+    memset(dig, 0x5a, sizeof dig);
+    memset(dig2, 0x5a, sizeof dig2);
+    rc = md5_batch_submit_async(b, ptrs, lens, (uint64_t)n, &dig[0][0], &te);
+    if (how == 1 && !use_inject) {
+        /* the launch itself failed at enqueue: E is done, with -EIO */
+        LCHECK(rc == 0, "async E %d", rc);
+        LCHECK(md5_batch_wait(b, te) == -EIO, "E -EIO");
+        __atomic_store_n(&fake_hip_hold, 0, __ATOMIC_RELAXED);
+    } else {
+        LCHECK(rc == 0, "async E %d", rc);
+        LCHECK((rc = md5_batch_flush(b)) == 0, "flush %d", rc);
+        LCHECK((rc = md5_batch_submit_async(b, ptrs, lens, (uint64_t)n, &dig2[0][0], &tf)) == 0, "async F %d", rc);
+        LCHECK(md5_batch_poll(b, tf) == 0, "F coalescing");
+        __atomic_store_n(&fake_hip_hold, 0, __ATOMIC_RELAXED);
+        LCHECK((rc = md5_batch_wait(b, te)) == -EIO, "the faulting launch's ticket: %d", rc);
+        LCHECK((rc = md5_batch_wait(b, tf)) == -ENODEV, "the ticket behind it: %d", rc);
+        LCHECK((rc = md5_batch_wait(b, tf)) == -ENODEV, "kept: %d", rc);
+        for (int i = 0; i < n; i++) LCHECK(dig2[i][0] == 0x5a && dig2[i][15] == 0x5a, "F's digests untouched");
+    }
+    for (int i = 0; i < n; i++) LCHECK(dig[i][0] == 0x5a && dig[i][15] == 0x5a, "no digest of a failed launch");
+    LCHECK(md5hip_batcher_health(b) == -ENODEV, "failed: %d", md5hip_batcher_health(b));
+    /* every later call: -ENODEV at once, nothing enqueued */
+    struct md5hip_batcher_stats st0, st1;
+    md5hip_batcher_get_stats(b, &st0);
+    uint64_t t = 99;
+    LCHECK((rc = md5_batch_submit(b, ptrs, lens, (uint64_t)n, &dig[0][0])) == -ENODEV, "sync %d", rc);
+    LCHECK((rc = md5_batch_submit_async(b, ptrs, lens, (uint64_t)n, &dig[0][0], &t)) == -ENODEV && t == 0,
+           "async %d", rc);
+    LCHECK((rc = md5hip_batch_host_fixed(b, g_heap, 4, 4096, 4096, &dig[0][0])) == -ENODEV, "fixed %d", rc);
+    struct md5hip_iov seg = {g_heap, 100};
+    uint64_t first[2] = {0, 1};
+    unsigned char ok[1];
+    LCHECK((rc = md5hip_batch_verify_iov(b, &seg, first, 1, g_md5[0], ok)) == -ENODEV,
+           "verify: %d (a device error is not a mismatch count)", rc);
+    uint64_t dp = (uint64_t)(uintptr_t)g_heap;
+    uint32_t dl = 64;
+    LCHECK((rc = md5_batch_submit_device(b, &dp, &dl, 1, &dig[0][0], 0)) == -ENODEV, "device %d", rc);
+    md5hip_batcher_get_stats(b, &st1);
+    LCHECK(st1.launches == st0.launches, "launched on a failed device");
+    LCHECK(md5hip_batcher_inject_fault(b, 1) == -ENODEV, "inject on failed");
+    md5hip_batcher_destroy(b);
+    return 0;
+}
+
+/* a 2-device pool: a synchronous split part is moved off the failed device */
+static int lost_pool_split(int d0, int d1)
+{
+    const int devs[2] = {d0, d1};
+    md5hip_pool *p;
+    int rc = md5hip_pool_create(devs, 2, 1u << 20, 3, &p);
+    LCHECK(rc == 0, "pool %d", rc);
+    md5hip_pool_set_split(p, 4096);                  /* every vector over both devices */
+    uint64_t s = 5;
+    const void *ptrs[MAXV];
+    uint32_t lens[MAXV];
+    int idx[MAXV];
+    unsigned char dig[MAXV][16];
+    int n = pick(&s, MAXV, ptrs, lens, idx);
+    while (n < 20) n = pick(&s, MAXV, ptrs, lens, idx);
+    LCHECK(md5hip_pool_inject_fault(p, 0, 1) == 0, "inject");
+    memset(dig, 0, sizeof dig);
+    LCHECK((rc = md5hip_pool_submit(p, ptrs, lens, (uint64_t)n, &dig[0][0])) == 0, "sync split %d", rc);
+    LCHECK(check_md5(dig, idx, n), "digests after failover");
+    struct md5hip_pool_health h;
+    LCHECK(md5hip_pool_get_health(p, &h) == 0 && h.ndev == 2 && h.nfailed == 1 && h.failed_mask == 1 &&
+           h.failovers == 1, "health nfailed %u mask %llx failovers %llu", h.nfailed,
+           (unsigned long long)h.failed_mask, (unsigned long long)h.failovers);
+    LCHECK(md5hip_pool_device_health(p, 0) == -ENODEV && md5hip_pool_device_health(p, 1) == 0 &&
+           md5hip_pool_device_health(p, 2) == -EINVAL, "device health");
+    /* from now on only device 1 works: whole, split, async, host_fixed */
+    struct md5hip_batcher_stats b0, b1;
+    md5hip_pool_device_stats(p, 0, &b0);
+    for (int r = 0; r < 20; r++) {
+        n = pick(&s, MAXV, ptrs, lens, idx);
+        uint64_t t;
+        if (r % 3 == 0) {
+            LCHECK((rc = md5hip_pool_submit_async(p, ptrs, lens, (uint64_t)n, &dig[0][0], &t)) == 0, "async %d", rc);
+            LCHECK((rc = md5hip_pool_wait(p, t)) == 0, "async wait %d", rc);
+        } else if (r % 3 == 1) {
+            LCHECK((rc = md5hip_pool_submit(p, ptrs, lens, (uint64_t)n, &dig[0][0])) == 0, "sync %d", rc);
+        } else {
+            LCHECK((rc = md5hip_pool_host_fixed(p, g_heap, 8, 4096, 4096, &dig[0][0])) == 0, "fixed %d", rc);
+            continue;
+        }
+        LCHECK(check_md5(dig, idx, n), "digests round %d", r);
+    }
+    md5hip_pool_device_stats(p, 0, &b1);
+    LCHECK(b1.submissions == b0.submissions, "routed to the failed device");
+    md5hip_pool_destroy(p);
+    return 0;
+}
+
+/* every device failed: -ENODEV, no hang */
+static int lost_pool_all(int d0, int d1)
+{
+    const int devs[2] = {d0, d1};
+    md5hip_pool *p;
+    int rc = md5hip_pool_create(devs, 2, 1u << 20, 2, &p);
+    LCHECK(rc == 0, "pool %d", rc);
+    const void *ptrs[4] = {g_heap, g_heap, g_heap, g_heap};
+    uint32_t lens[4] = {10, 20, 30, 40};
+    unsigned char dig[4][16];
+    LCHECK(md5hip_pool_inject_fault(p, 0, 1) == 0 && md5hip_pool_inject_fault(p, 1, 1) == 0, "inject");
+    md5hip_pool_set_split(p, 1);                     /* one part per device */
+    LCHECK((rc = md5hip_pool_submit(p, ptrs, lens, 4, &dig[0][0])) == -EIO || rc == -ENODEV, "sync %d", rc);
+    struct md5hip_pool_health h;
+    md5hip_pool_get_health(p, &h);
+    LCHECK(h.nfailed == 2, "both failed: %u", h.nfailed);
+    uint64_t t = 7;
+    LCHECK((rc = md5hip_pool_submit(p, ptrs, lens, 4, &dig[0][0])) == -ENODEV, "sync after %d", rc);
+    LCHECK((rc = md5hip_pool_submit_async(p, ptrs, lens, 4, &dig[0][0], &t)) == -ENODEV && t == 0,
+           "async after %d", rc);
+    md5hip_pool_destroy(p);
+    return 0;
+}
+
+/* 8 threads on a pool while one of its devices dies under them: synchronous
+ * calls all succeed (moved), asynchronous ones succeed or get -EIO */
+struct lj {
+    md5hip_pool *p;
+    int t, ops, bad, sync_err, async_eio, other;
+};
+
+static void *lost_worker(void *arg)
+{
+    struct lj *j = arg;
+    uint64_t s = 0xC0FFEEull * (uint64_t)(j->t + 3);
+    const void *ptrs[MAXV];
+    uint32_t lens[MAXV];
+    int idx[MAXV];
+    unsigned char dig[MAXV][16];
+    struct md5hip_iov segs[MAXV];
+    uint64_t first[MAXV + 1];
+    for (int r = 0; r < j->ops; r++) {
+        const int n = pick(&s, 80, ptrs, lens, idx);
+        const int op = (int)(rnd(&s) % 4);
+        int rc;
+        memset(dig, 0, sizeof dig);
+        if (op == 0) {
+            rc = md5hip_pool_submit(j->p, ptrs, lens, (uint64_t)n, &dig[0][0]);
+        } else if (op == 1) {
+            for (int i = 0; i < n; i++) first[i] = (uint64_t)i, segs[i] = (struct md5hip_iov){ptrs[i], lens[i]};
+            first[n] = (uint64_t)n;
+            rc = md5hip_pool_submit_iov(j->p, segs, first, (uint64_t)n, &dig[0][0]);
+        } else if (op == 2) {
+            unsigned char ok[MAXV];
+            for (int i = 0; i < n; i++) first[i] = (uint64_t)i, segs[i] = (struct md5hip_iov){ptrs[i], lens[i]};
+            first[n] = (uint64_t)n;
+            for (int i = 0; i < n; i++) memcpy(dig[i], g_md5[idx[i]], 16);
+            rc = md5hip_pool_verify_iov(j->p, segs, first, (uint64_t)n, dig, ok);
+            if (rc != 0) j->sync_err++;                  /* 0 mismatches, never a device error */
+            continue;
+        } else {
+            uint64_t t;
+            rc = md5hip_pool_submit_async(j->p, ptrs, lens, (uint64_t)n, &dig[0][0], &t);
+            if (rc == 0) rc = md5hip_pool_wait(j->p, t);
+            if (rc == -EIO) { j->async_eio++; continue; }
+        }
+        if (rc) j->sync_err++;
+        else if (!check_md5(dig, idx, n)) j->bad++;
+    }
+    return NULL;
+}
+
+static int lost_pool_threads(int d0, int d1)
+{
+    const int devs[2] = {d0, d1};
+    md5hip_pool *p;
+    int rc = md5hip_pool_create(devs, 2, 1u << 20, 3, &p);
+    LCHECK(rc == 0, "pool %d", rc);
+    fake_hip_lose_device(d1, 6, 0);
+    enum { LT = 8 };
+    struct lj jobs[LT];
+    pthread_t th[LT];
+    for (int t = 0; t < LT; t++) {
+        jobs[t] = (struct lj){p, t, 40, 0, 0, 0, 0};
+        pthread_create(&th[t], NULL, lost_worker, &jobs[t]);
+    }
+    int eio = 0;
+    for (int t = 0; t < LT; t++) {
+        pthread_join(th[t], NULL);
+        LCHECK(jobs[t].bad == 0 && jobs[t].sync_err == 0, "thread %d: bad %d sync errors %d", t, jobs[t].bad,
+               jobs[t].sync_err);
+        eio += jobs[t].async_eio;
+    }
+    struct md5hip_pool_health h;
+    md5hip_pool_get_health(p, &h);
+    LCHECK(fake_hip_device_faulted(d1) && h.nfailed == 1 && h.failed_mask == 2, "health mask %llx",
+           (unsigned long long)h.failed_mask);
+    printf("device lost under 8 threads: %llu failovers, %d async -EIO\n", (unsigned long long)h.failovers, eio);
+    md5hip_pool_destroy(p);
+    return 0;
+}
+
+static int device_lost(void)
+{
+    /* devices 0-2 belong to the other phases; the fake runtime knows 0-7 */
+    if (lost_single(3, 0, 0)) return 1;               /* the completion event reports the fault */
+    if (lost_single(4, 1, 0)) return 1;               /* the launch itself fails */
+    if (lost_single(5, 0, 1)) return 1;               /* md5hip_batcher_inject_fault */
+    if (lost_pool_split(6, 7)) return 1;              /* inject on 6 */
+    if (lost_pool_all(3, 4)) return 1;                /* both already failed in the fake */
+    if (lost_pool_threads(7, 6)) return 1;            /* 7 still healthy: the fake fault hits 6 again */
+    printf("device lost: -EIO / -ENODEV / failover ok\n");
+    return 0;
+}
+
 /* a hang is a failure, not a stuck test */
 static void *watchdog(void *arg)
 {
@@ -534,6 +796,7 @@ int main(int argc, char **argv)
     pthread_detach(wd);
     if (blocked_callers(12)) return 1;
     if (large_device()) return 1;
+    if (device_lost()) return 1;
     /* error paths, one thread: a chunk over the slice, a never-issued
      * ticket, a launch that fails (sync and async; the failure is kept for
      * a second wait and does not touch later submissions) */

@@ -24,7 +24,14 @@
  *     then it answers NotReady to unmarked threads) -- a
  *     waiter's bounded spin then ends on NotReady just after the kernel
  *     finished, and the progress thread retires the launch before the waiter
- *     holds the lock again (the lost-wakeup race of a blocked caller).
+ *     holds the lock again (the lost-wakeup race of a blocked caller);
+ *   - device lost after launch K (fake_hip_lose_device): the K-th kernel
+ *     enqueued on a device from then on faults.  how 0: it is enqueued, and
+ *     every event recorded on that device from then on reports
+ *     hipErrorLaunchFailure when it completes; once one has, every copy,
+ *     kernel and stream wait on the device fails too.  how 1: that kernel's
+ *     launch itself fails, and everything after it.  hipStreamQuery reports
+ *     the loss either way (what the batcher classifies an enqueue error by).
  * Nothing here is part of the product.
  */
 #include <errno.h>
@@ -43,6 +50,8 @@
 
 struct ihipEvent_t {
     int left;                     /* queries still answered NotReady */
+    int bad;                      /* recorded on a device that had faulted: completes with an error */
+    int device;
     unsigned seed;
     int slow;                     /* recorded while fake_hip_slow_query was set */
     int slow_done;                /* the slow query of this record happened */
@@ -61,6 +70,61 @@ static void on_stream(hipStream_t stream)
 {
     if (stream && stream->device != t_device)
         __atomic_fetch_add(&fake_hip_wrong_device, 1, __ATOMIC_RELAXED);
+}
+
+/* device loss (all under g_lose_mu) */
+static pthread_mutex_t g_lose_mu = PTHREAD_MUTEX_INITIALIZER;
+static int g_lose_after[8], g_lose_how[8], g_kernels[8];
+static int g_faulted[8];          /* the fault happened */
+static int g_reported[8];         /* ... and the runtime has said so: enqueues fail */
+static unsigned long g_lost_kernels;
+
+static int stream_dev(hipStream_t s) { return s ? s->device : t_device; }
+
+void fake_hip_lose_device(int dev, int after_kernels, int how)
+{
+    pthread_mutex_lock(&g_lose_mu);
+    g_lose_after[dev] = g_kernels[dev] + after_kernels;
+    g_lose_how[dev] = how;
+    pthread_mutex_unlock(&g_lose_mu);
+}
+
+int fake_hip_device_faulted(int dev)
+{
+    pthread_mutex_lock(&g_lose_mu);
+    const int f = g_faulted[dev];
+    pthread_mutex_unlock(&g_lose_mu);
+    return f;
+}
+
+/* an enqueue on `s`: hipErrorLaunchFailure once its device's loss is known */
+static hipError_t enqueue_ok(hipStream_t s)
+{
+    pthread_mutex_lock(&g_lose_mu);
+    const int bad = g_reported[stream_dev(s)];
+    pthread_mutex_unlock(&g_lose_mu);
+    return bad ? hipErrorLaunchFailure : hipSuccess;
+}
+
+/* a kernel enqueued on `stream`: 0, or -EIO if the launch fails */
+static int kernel_begin(hipStream_t stream)
+{
+    on_stream(stream);
+    const int d = stream_dev(stream);
+    pthread_mutex_lock(&g_lose_mu);
+    int rc = g_reported[d] ? -EIO : 0;
+    if (!rc && g_lose_after[d] && ++g_kernels[d] >= g_lose_after[d] && !g_faulted[d]) {
+        g_faulted[d] = 1;
+        if (g_lose_how[d]) {
+            g_reported[d] = 1;
+            rc = -EIO;
+        }
+    } else if (!rc && !g_lose_after[d]) {
+        g_kernels[d]++;
+    }
+    if (rc) g_lost_kernels++;
+    pthread_mutex_unlock(&g_lose_mu);
+    return rc;
 }
 /* a launch holding a chunk of this length fails with -EIO (error paths) */
 uint32_t fake_hip_fail_len = 0xffffffffu;
@@ -87,7 +151,14 @@ hipError_t hipStreamCreateWithFlags(hipStream_t *stream, unsigned int flags)
     return hipSuccess;
 }
 hipError_t hipStreamDestroy(hipStream_t stream) { free(stream); return hipSuccess; }
-hipError_t hipStreamWaitEvent(hipStream_t stream, hipEvent_t event, unsigned int flags) { (void)stream; (void)event; (void)flags; return hipSuccess; }
+hipError_t hipStreamWaitEvent(hipStream_t stream, hipEvent_t event, unsigned int flags) { (void)event; (void)flags; return enqueue_ok(stream); }
+hipError_t hipStreamQuery(hipStream_t stream)
+{
+    pthread_mutex_lock(&g_lose_mu);
+    const int f = g_faulted[stream_dev(stream)];
+    pthread_mutex_unlock(&g_lose_mu);
+    return f ? hipErrorLaunchFailure : hipSuccess;
+}
 
 hipError_t hipEventCreateWithFlags(hipEvent_t *event, unsigned flags)
 {
@@ -100,8 +171,12 @@ hipError_t hipEventCreateWithFlags(hipEvent_t *event, unsigned flags)
 hipError_t hipEventDestroy(hipEvent_t event) { free(event); return hipSuccess; }
 hipError_t hipEventRecord(hipEvent_t event, hipStream_t stream)
 {
-    (void)stream;
+    pthread_mutex_lock(&g_lose_mu);
+    const int bad = g_faulted[stream_dev(stream)];
+    pthread_mutex_unlock(&g_lose_mu);
     pthread_mutex_lock(&g_ev_mu);
+    event->bad = bad;
+    event->device = stream_dev(stream);
     event->seed = event->seed * 1103515245u + 12345u;
     event->left = (int)((event->seed >> 16) % 4u);
     event->slow = __atomic_load_n(&fake_hip_slow_query, __ATOMIC_RELAXED);
@@ -130,7 +205,15 @@ hipError_t hipEventQuery(hipEvent_t event)
     }
     const int ready = event->left == 0;
     if (!ready) event->left--;
+    const int bad = ready && event->bad;
+    const int dev = event->device;
     pthread_mutex_unlock(&g_ev_mu);
+    if (bad) {                                    /* the runtime has seen the fault now */
+        pthread_mutex_lock(&g_lose_mu);
+        g_reported[dev] = 1;
+        pthread_mutex_unlock(&g_lose_mu);
+        return hipErrorLaunchFailure;
+    }
     return ready ? hipSuccess : hipErrorNotReady;
 }
 hipError_t hipEventSynchronize(hipEvent_t event)
@@ -141,14 +224,17 @@ hipError_t hipEventSynchronize(hipEvent_t event)
     }
     pthread_mutex_lock(&g_ev_mu);
     event->left = 0;
+    const int bad = event->bad;
     pthread_mutex_unlock(&g_ev_mu);
-    return hipSuccess;
+    return bad ? hipErrorLaunchFailure : hipSuccess;
 }
 
 hipError_t hipMemcpyAsync(void *dst, const void *src, size_t sizeBytes, hipMemcpyKind kind, hipStream_t stream)
 {
     (void)kind;
     on_stream(stream);
+    const hipError_t e = enqueue_ok(stream);
+    if (e != hipSuccess) return e;
     if (sizeBytes) memmove(dst, src, sizeBytes);
     return hipSuccess;
 }
@@ -171,7 +257,7 @@ static uint32_t blk_crc(const unsigned char *p, uint32_t len, uint32_t F)
 int md5hip_digest_fixed(const void *d_base, uint64_t n, uint32_t len, uint64_t stride,
                         unsigned char *d_digests, void *stream)
 {
-    on_stream((hipStream_t)stream);
+    if (kernel_begin((hipStream_t)stream)) return -EIO;
     for (uint64_t i = 0; i < n; i++) md5_of((const unsigned char *)d_base + i * stride, len, d_digests + 16 * i);
     return 0;
 }
@@ -179,7 +265,7 @@ int md5hip_digest_fixed(const void *d_base, uint64_t n, uint32_t len, uint64_t s
 int crc32hip_fixed(const void *d_base, uint64_t n, uint32_t len, uint64_t stride, uint32_t fastcrc,
                    uint32_t *d_crcs, void *stream)
 {
-    on_stream((hipStream_t)stream);
+    if (kernel_begin((hipStream_t)stream)) return -EIO;
     for (uint64_t i = 0; i < n; i++) d_crcs[i] = blk_crc((const unsigned char *)d_base + i * stride, len, fastcrc);
     return 0;
 }
@@ -188,7 +274,7 @@ int md5hip_digest_desc_variant(const void *d_base, const uint64_t *d_offsets, co
                                const uint32_t *d_order, uint64_t n, unsigned char *d_digests,
                                void *stream, int variant)
 {
-    on_stream((hipStream_t)stream);
+    if (kernel_begin((hipStream_t)stream)) return -EIO;
     (void)variant;
     if (((uintptr_t)d_digests & 15u) != 0) return -EINVAL;
     for (uint64_t k = 0; k < n; k++)
@@ -205,7 +291,7 @@ int md5hip_digest_desc_variant(const void *d_base, const uint64_t *d_offsets, co
 int crc32hip_desc(const void *d_base, const uint64_t *d_offsets, const uint32_t *d_lens,
                   const uint32_t *d_order, uint64_t n, uint32_t fastcrc, uint32_t *d_crcs, void *stream)
 {
-    on_stream((hipStream_t)stream);
+    if (kernel_begin((hipStream_t)stream)) return -EIO;
     for (uint64_t k = 0; k < n; k++) {
         const uint64_t c = d_order ? d_order[k] : k;
         if (c >= n) return -EINVAL;
@@ -235,6 +321,7 @@ int md5hip_crc_desc_choice(uint64_t n, uint64_t mean_len)
 int md5hip_gather_launch(const struct md5hip_seg *d_segs, uint64_t nseg, unsigned char *d_dst, void *stream)
 {
     on_stream((hipStream_t)stream);
+    if (enqueue_ok((hipStream_t)stream) != hipSuccess) return -EIO;
     for (uint64_t k = 0; k < nseg; k++)
         memmove((void *)((uintptr_t)d_dst + d_segs[k].dst), (const void *)(uintptr_t)d_segs[k].src, d_segs[k].len);
     return 0;
@@ -274,6 +361,7 @@ int md5hip_order_device(const uint32_t *d_lens, uint64_t n, uint32_t kmax, uint3
                         uint32_t *d_order, void *stream)
 {
     on_stream((hipStream_t)stream);
+    if (enqueue_ok((hipStream_t)stream) != hipSuccess) return -EIO;
     for (uint64_t i = 0; i < n; i++) {
         const uint32_t k = (d_lens[i] >> 6) + 1;
         if (k > kmax) continue;

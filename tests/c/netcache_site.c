@@ -33,6 +33,15 @@
  *      16 KiB page (md5hip_*_ctx, §2i)
  *  11. one batcher shared by four "ASIO" threads, each submitting its blocks
  *      asynchronously and collecting its own tickets (§2, §2g)
+ *  12. the failure policy (§2j): a device fault injected into the launch of
+ *      an origin-read vector -- the call returns -EIO, no checksum of that
+ *      vector is stored (memory-only policy: blocks kept off the disk path),
+ *      the next vector gets -ENODEV at once and is hashed on the calling
+ *      thread with the library's host CRC-32 (host policy), a cache-read
+ *      verify on the failed device resets no inode and falls back the same
+ *      way; a pool over device 0 listed twice moves a synchronous vector off
+ *      its failed half and returns every checksum, and never routes to it
+ *      again
  *
  * Exit 0 = all equal; 1 = a mismatch or error; 77 = no usable HIP device
  * (md5hip_batcher_create returned -ENODEV: the batched entries fail loudly,
@@ -50,6 +59,7 @@
 
 #include "md5.h"
 #include "md5hip.h"
+#include "nc_digest.h"
 
 /* oracle (checker) */
 void oracle_md5(const void *data, uint64_t len, unsigned char digest[16]);
@@ -67,6 +77,8 @@ typedef struct {
     uint64_t size;
     uint32_t chunk_size;
     uint32_t blockcrc[NBLK_MAX];
+    unsigned char cascade[NBLK_MAX];   /* block goes on to the disk cache (BS_CACHED_DIRTY, blk_io.c:867-871) */
+    int resets;                        /* dm_reset_inode_nolock calls (blk_io.c:693-703) */
 } fc_inode_t;
 
 static long long blk_valid_len(const fc_inode_t *inode, const fc_blk_t *blk)
@@ -165,6 +177,167 @@ static void *pool_thread(void *arg)
         for (int b = j->lo; b < j->hi; b++) j->bad += memcmp(dig[r][b - j->lo], j->want[b], 16) != 0;
     }
     return NULL;
+}
+
+/* ----------------------------------------------------------- §2j bindings */
+enum { POLICY_HOST = 0, POLICY_MEMORY_ONLY = 1 };
+
+/* the library's host CRC-32 of one block (product code, not the oracle):
+ * what the site computes on the calling thread when the device cannot */
+static uint32_t host_blk_crc(const struct md5hip_iov *segs, uint64_t s0, uint64_t s1, uint32_t fastcrc,
+                             unsigned char *tmp)
+{
+    uint64_t L = 0;
+    for (uint64_t s = s0; s < s1; s++) {
+        memcpy(tmp + L, segs[s].base, segs[s].len);
+        L += segs[s].len;
+    }
+    if (fastcrc == 0 || L <= fastcrc) return nc_crc32(tmp, L);           /* blk_io.c:408-424 */
+    return nc_crc32(tmp, fastcrc) ^ nc_crc32(tmp + (L - fastcrc), fastcrc);
+}
+
+/* origin read (blk_io.c:851-863) as INTEGRATION.md §2j binds it: a checksum
+ * is stored only from a call that returned 0 or from the site's own host
+ * code; a device error is never stored as a checksum.  Returns the batched
+ * call's rc. */
+static int origin_read_vector(md5hip_batcher *b, fc_inode_t *inode, fc_blk_t *const *blks, int lo, int hi,
+                              const struct md5hip_iov *segs, const uint64_t *first, int policy,
+                              uint32_t *crc_out, unsigned char *tmp)
+{
+    const int n = hi - lo;
+    uint64_t rebased[NBLK_MAX + 1];
+    for (int k = 0; k <= n; k++) rebased[k] = first[lo + k] - first[lo];
+    const int rc = md5_batch_submit_iov(b, segs + first[lo], rebased, (uint64_t)n, (unsigned char *)crc_out);
+    if (rc == 0) {
+        for (int k = 0; k < n; k++) {
+            inode->blockcrc[blks[lo + k]->blkno] = crc_out[k];      /* dm_update_block_crc_nolock */
+            inode->cascade[blks[lo + k]->blkno] = 1;
+        }
+        return 0;
+    }
+    for (int k = 0; k < n; k++) {
+        if (policy == POLICY_HOST) {
+            inode->blockcrc[blks[lo + k]->blkno] = host_blk_crc(segs, first[lo + k], first[lo + k + 1], 0, tmp);
+            inode->cascade[blks[lo + k]->blkno] = 1;
+        } else {
+            inode->cascade[blks[lo + k]->blkno] = 0;                /* BS_CACHED: memory only */
+        }
+    }
+    return rc;
+}
+
+/* cache read (blk_io.c:665-704): a mismatch resets the inode; a device error
+ * is not a mismatch -- the vector is verified on the calling thread instead.
+ * Returns the number of mismatching blocks. */
+static int cache_read_verify(md5hip_batcher *b, fc_inode_t *inode, fc_blk_t *const *blks, int nb,
+                             const struct md5hip_iov *segs, const uint64_t *first, unsigned char *ok,
+                             unsigned char *tmp, int *device_rc)
+{
+    uint32_t want[NBLK_MAX] = {0};
+    for (int k = 0; k < nb; k++) want[k] = inode->blockcrc[blks[k]->blkno];
+    int bad = md5hip_batch_verify_iov(b, segs, first, (uint64_t)nb, want, ok);
+    *device_rc = bad < 0 ? bad : 0;
+    if (bad < 0) {
+        bad = 0;
+        for (int k = 0; k < nb; k++) {
+            ok[k] = host_blk_crc(segs, first[k], first[k + 1], 0, tmp) == want[k];   /* dm_verify_block_crc */
+            bad += !ok[k];
+        }
+    }
+    for (int k = 0; k < nb; k++)
+        if (!ok[k]) inode->resets++;                                  /* EAGAIN + dm_reset_inode_nolock */
+    return bad;
+}
+
+static int failure_pass(fc_inode_t *inode, fc_blk_t *const *blks, int nblk, const struct md5hip_iov *segs,
+                        const uint64_t *first, const uint32_t *want_crc, const unsigned char (*want_md5)[16],
+                        unsigned char *tmp)
+{
+    const int nf0 = failures;
+    md5hip_batcher *b = NULL;
+    int rc = md5hip_batcher_create(0, 16u << 20, 3, &b);
+    CHECK(rc == 0, "failure batcher = %d", rc);
+    if (rc) return 1;
+    CHECK(md5hip_batcher_set_digest(b, MD5HIP_DIGEST_CRC32, 0) == 0, "set CRC-32");
+    const uint32_t SENT = 0xdeadbeefu;
+    for (int k = 0; k < nblk; k++) inode->blockcrc[k] = SENT, inode->cascade[k] = 1;
+    uint32_t crc[NBLK_MAX];
+    const int half = nblk / 2;
+
+    /* a healthy vector first */
+    rc = origin_read_vector(b, inode, blks, 0, 8, segs, first, POLICY_MEMORY_ONLY, crc, tmp);
+    CHECK(rc == 0, "healthy vector %d", rc);
+    for (int k = 0; k < 8; k++) CHECK(inode->blockcrc[k] == want_crc[k], "healthy crc %d", k);
+
+    /* A: the device faults under this vector's launch */
+    CHECK(md5hip_batcher_inject_fault(b, 1) == 0, "inject");
+    for (int k = 0; k < NBLK_MAX; k++) crc[k] = SENT;
+    rc = origin_read_vector(b, inode, blks, 8, half, segs, first, POLICY_MEMORY_ONLY, crc, tmp);
+    CHECK(rc == -EIO, "faulting vector: rc %d, want -EIO", rc);
+    for (int k = 8; k < half; k++) {
+        CHECK(crc[k - 8] == SENT, "device wrote a checksum for failed block %d", k);
+        CHECK(inode->blockcrc[k] == SENT, "a checksum was stored for failed block %d", k);
+        CHECK(inode->cascade[k] == 0, "failed block %d still goes to disk", k);
+    }
+    CHECK(md5hip_batcher_health(b) == -ENODEV, "batcher not failed: %d", md5hip_batcher_health(b));
+
+    /* B: the next vector is refused at once and hashed on the calling thread */
+    rc = origin_read_vector(b, inode, blks, half, nblk, segs, first, POLICY_HOST, crc, tmp);
+    CHECK(rc == -ENODEV, "next vector: rc %d, want -ENODEV", rc);
+    for (int k = half; k < nblk; k++) {
+        CHECK(inode->blockcrc[k] == want_crc[k], "host fallback crc %d", k);
+        CHECK(inode->cascade[k] == 1, "host-fallback block %d kept off disk", k);
+    }
+
+    /* C: cache read on the failed device: no inode reset from the device
+     * error; one really corrupted block is still caught (host verify) */
+    unsigned char ok[NBLK_MAX];
+    int drc = 0;
+    const int nb = nblk - half;
+    uint64_t rebased[NBLK_MAX + 1];
+    for (int k = 0; k <= nb; k++) rebased[k] = first[half + k] - first[half];
+    inode->resets = 0;
+    int bad = cache_read_verify(b, inode, blks + half, nb, segs + first[half], rebased, ok, tmp, &drc);
+    CHECK(drc == -ENODEV && bad == 0 && inode->resets == 0, "verify on a failed device: rc %d bad %d resets %d",
+          drc, bad, inode->resets);
+    unsigned char *victim = (unsigned char *)blks[half + 3]->pages[1]->memory + 99;
+    *victim ^= 0x08;
+    bad = cache_read_verify(b, inode, blks + half, nb, segs + first[half], rebased, ok, tmp, &drc);
+    *victim ^= 0x08;
+    CHECK(bad == 1 && !ok[3] && inode->resets == 1, "host verify: bad %d ok[3] %d resets %d", bad, ok[3],
+          inode->resets);
+    md5hip_batcher_destroy(b);
+
+    /* D: a pool over device 0 listed twice; its half 0 faults under a
+     * synchronous vector split over both halves */
+    md5hip_pool *pool = NULL;
+    const int devs[2] = {0, 0};
+    rc = md5hip_pool_create(devs, 2, 16u << 20, 3, &pool);
+    CHECK(rc == 0, "failure pool = %d", rc);
+    if (rc) return 1;
+    CHECK(md5hip_pool_set_split(pool, 64u << 10) == 0, "split");
+    CHECK(md5hip_pool_inject_fault(pool, 0, 1) == 0, "pool inject");
+    static unsigned char digest[NBLK_MAX][16];
+    memset(digest, 0, sizeof digest);
+    rc = md5hip_pool_submit_iov(pool, segs, first, (uint64_t)nblk, &digest[0][0]);
+    CHECK(rc == 0, "pool vector with a failed device: %d", rc);
+    for (int k = 0; k < nblk; k++) CHECK(memcmp(digest[k], want_md5[k], 16) == 0, "pool failover block %d", k);
+    struct md5hip_pool_health h;
+    CHECK(md5hip_pool_get_health(pool, &h) == 0 && h.nfailed == 1 && h.failed_mask == 1 && h.failovers == 1,
+          "pool health: nfailed %u mask %llx failovers %llu", h.nfailed, (unsigned long long)h.failed_mask,
+          (unsigned long long)h.failovers);
+    struct md5hip_batcher_stats s0, s1;
+    md5hip_pool_device_stats(pool, 0, &s0);
+    for (int r = 0; r < 4; r++) {
+        memset(digest, 0, sizeof digest);
+        rc = md5hip_pool_submit_iov(pool, segs, first, (uint64_t)nblk, &digest[0][0]);
+        CHECK(rc == 0, "pool after the fault: %d", rc);
+        for (int k = 0; k < nblk; k++) CHECK(memcmp(digest[k], want_md5[k], 16) == 0, "pool after, block %d", k);
+    }
+    md5hip_pool_device_stats(pool, 0, &s1);
+    CHECK(s1.launches == s0.launches && s1.submissions == s0.submissions, "the failed half was used again");
+    md5hip_pool_destroy(pool);
+    return failures != nf0;
 }
 
 /* the block's bytes, gathered on the host for the oracle */
@@ -496,6 +669,9 @@ int main(void)
         }
     }
 
+    /* 12. the failure policy (§2j) */
+    (void)failure_pass(&inode, blks, nblk, segs, first, want_crc, (const unsigned char (*)[16])want_md5, tmp);
+
     free(tmp);
     free(heap);
     if (failures) {
@@ -504,7 +680,7 @@ int main(void)
     }
     printf("netcache_site ok: %d blocks (%llu bytes, %d pages scattered), MD5 / CRC-32 / fastcrc / "
            "verify / async / zero-copy x3 / pool / MD5Init-Update-Final / arena+plan / device queue / "
-           "device contexts / shared batcher x4 threads bit-exact vs oracle\n",
+           "device contexts / shared batcher x4 threads bit-exact vs oracle; failure policy ok\n",
            nblk, (unsigned long long)inode.size, npages);
     return 0;
 }

@@ -5,7 +5,10 @@
  * the pool calls are replaced by a fake defined here, which hashes on the CPU
  * with the library's own host MD5 (md5_stream.c) / CRC-32 (nc_digest.c) and
  * completes a ticket only after a few polls, failing every 9th submission
- * with -EIO when asked to.  Built with ASan+UBSan and with TSan by
+ * with -EIO when asked to, and losing a device on request
+ * (md5hip_batcher_inject_fault: that submission completes with -EIO and
+ * garbage digests, the batcher reports -ENODEV from then on and refuses
+ * every submission with it).  Built with ASan+UBSan and with TSan by
  * tests/test_pool_host.py.  Exits 0 when every check holds, else prints the
  * failing check.
  */
@@ -44,7 +47,20 @@ struct md5hip_batcher {
     uint64_t *tk_weight;
     uint64_t submissions, launches;
     int device;
+    int lost;                      /* -ENODEV once "lost" (read lock-free: atomic) */
+    uint64_t lose_in;              /* the lose_in-th submission from now fails and loses the device */
 };
+
+int md5hip_batcher_health(const md5hip_batcher *b) { return __atomic_load_n(&b->lost, __ATOMIC_ACQUIRE); }
+
+int md5hip_batcher_inject_fault(md5hip_batcher *b, uint64_t after)
+{
+    pthread_mutex_lock(&b->mu);
+    const int rc = b->lost;
+    if (!rc) b->lose_in = after;
+    pthread_mutex_unlock(&b->mu);
+    return rc;
+}
 
 static int g_fail_every = 0;       /* every n-th submission (process-wide) fails */
 static uint64_t g_submit_count = 0;
@@ -117,6 +133,10 @@ static int fake_submit(md5hip_batcher *b, int kind, uint64_t weight, uint64_t *t
     *failed = g_fail_every && c % (uint64_t)g_fail_every == 0;
     (void)kind;
     pthread_mutex_lock(&b->mu);
+    if (b->lose_in && --b->lose_in == 0) {          /* this launch faults: the device is gone */
+        *failed = 1;
+        __atomic_store_n(&b->lost, -ENODEV, __ATOMIC_RELEASE);
+    }
     if (b->ntk == b->captk) {
         b->captk = b->captk ? 2 * b->captk : 64;
         b->tk = realloc(b->tk, b->captk * sizeof *b->tk);
@@ -157,6 +177,7 @@ int md5hip_submit_as(md5hip_batcher *b, int kind, uint32_t fastcrc, const void *
     (void)urgent;
     if (ticket) *ticket = 0;
     if (n == 0) return 0;
+    if (md5hip_batcher_health(b)) return -ENODEV;
     const uint32_t dsz = kind == MD5HIP_DIGEST_CRC32 ? 4 : 16;
     uint64_t weight = 0;
     for (uint64_t i = 0; i < n; i++) {
@@ -173,6 +194,7 @@ int md5hip_submit_as(md5hip_batcher *b, int kind, uint32_t fastcrc, const void *
     uint64_t t;
     int failed;
     fake_submit(b, kind, weight, &t, &failed);
+    if (failed) memset(digests, 0xAA, (size_t)dsz * n);  /* what a failed launch leaves */
     if (!ticket) {                                      /* synchronous */
         int err = 0;
         while (!fake_state(b, t, 1, &err)) {}
@@ -186,6 +208,8 @@ int md5hip_host_fixed_as(md5hip_batcher *b, int kind, uint32_t fastcrc, const vo
                          uint32_t len, uint64_t stride, unsigned char *digests, uint64_t *ticket)
 {
     (void)fastcrc;
+    if (ticket) *ticket = 0;
+    if (md5hip_batcher_health(b)) return -ENODEV;
     const uint32_t dsz = kind == MD5HIP_DIGEST_CRC32 ? 4 : 16;
     for (uint64_t i = 0; i < n; i++) {
         const struct md5hip_iov one = {(const unsigned char *)h_base + i * stride, len};
@@ -194,6 +218,7 @@ int md5hip_host_fixed_as(md5hip_batcher *b, int kind, uint32_t fastcrc, const vo
     uint64_t t;
     int failed;
     fake_submit(b, kind, n * ((uint64_t)len + 64), &t, &failed);
+    if (failed) memset(digests, 0xAA, (size_t)dsz * n);
     if (!ticket) {
         int err = 0;
         while (!fake_state(b, t, 1, &err)) {}
@@ -372,6 +397,60 @@ int main(void)
     }
     CHECK(fails > 0 && oks > 0, "failures %d, successes %d", fails, oks);
     g_fail_every = 0;
+
+    /* a lost device (md5_pool.c failover): a synchronous split part on it is
+     * moved to a healthy device and the call returns 0 with every digest;
+     * the device is never routed to again */
+    md5hip_pool_set_split(p, 1u << 20);
+    CHECK(md5hip_pool_inject_fault(p, 2, 1) == 0, "inject 2");
+    memset(dig, 0, sizeof dig);
+    CHECK(md5hip_pool_submit(p, ptrs, g_lens, 2000, &dig[0][0]) == 0, "sync split with a device lost");
+    for (int i = 0; i < 2000; i++) CHECK(memcmp(dig[i], g_want[i], 16) == 0, "failover digest %d", i);
+    struct md5hip_pool_health h;
+    CHECK(md5hip_pool_get_health(p, &h) == 0 && h.ndev == 4 && h.nfailed == 1 && h.failed_mask == 4 &&
+          h.failovers == 1, "health: nfailed %u mask %llx failovers %llu", h.nfailed,
+          (unsigned long long)h.failed_mask, (unsigned long long)h.failovers);
+    CHECK(md5hip_pool_device_health(p, 2) == -ENODEV && md5hip_pool_device_health(p, 1) == 0 &&
+          md5hip_pool_device_health(p, 4) == -EINVAL && md5hip_pool_inject_fault(p, 2, 1) == -ENODEV,
+          "device health");
+    struct md5hip_batcher_stats d2a, d2b;
+    md5hip_pool_device_stats(p, 2, &d2a);
+    for (int r = 0; r < 30; r++) {
+        const int n = r % 2 ? 2000 : 1 + r * 7;
+        memset(dig, 0, sizeof dig);
+        if (r % 3 == 0) {
+            uint64_t tt;
+            CHECK(md5hip_pool_submit_async(p, ptrs, g_lens, (uint64_t)n, &dig[0][0], &tt) == 0, "async after loss");
+            CHECK(md5hip_pool_wait(p, tt) == 0, "async wait after loss");
+        } else {
+            CHECK(md5hip_pool_submit(p, ptrs, g_lens, (uint64_t)n, &dig[0][0]) == 0, "sync after loss");
+        }
+        for (int i = 0; i < n; i++) CHECK(memcmp(dig[i], g_want[i], 16) == 0, "after loss %d/%d", r, i);
+    }
+    md5hip_pool_device_stats(p, 2, &d2b);
+    CHECK(d2b.submissions == d2a.submissions, "the failed device took %llu more",
+          (unsigned long long)(d2b.submissions - d2a.submissions));
+    /* an asynchronous split ticket whose part's device is lost keeps -EIO */
+    CHECK(md5hip_pool_inject_fault(p, 1, 1) == 0, "inject 1");
+    memset(dig, 0, sizeof dig);
+    CHECK(md5hip_pool_submit_async(p, ptrs, g_lens, 2000, &dig[0][0], &t) == 0, "async split, device 1 lost");
+    CHECK(md5hip_pool_wait(p, t) == -EIO, "async ticket -EIO");
+    CHECK(md5hip_pool_wait(p, t) == -EIO, "kept");
+    CHECK(md5hip_pool_get_health(p, &h) == 0 && h.nfailed == 2 && h.failed_mask == 6 && h.failovers == 1,
+          "two lost: mask %llx failovers %llu", (unsigned long long)h.failed_mask, (unsigned long long)h.failovers);
+    /* host_fixed while the last two devices are lost on the way: moved from
+     * one to the other, then -ENODEV with nothing left */
+    CHECK(md5hip_pool_inject_fault(p, 0, 1) == 0 && md5hip_pool_inject_fault(p, 3, 1) == 0, "inject 0, 3");
+    static unsigned char fx[64][16];
+    CHECK(md5hip_pool_host_fixed(p, g_blob, 64, 1000, 1000, &fx[0][0]) == -ENODEV, "fixed, last two lost");
+    CHECK(md5hip_pool_get_health(p, &h) == 0 && h.nfailed == 4 && h.failed_mask == 15 && h.failovers == 3,
+          "all lost: %u failovers %llu", h.nfailed, (unsigned long long)h.failovers);
+    t = 5;
+    CHECK(md5hip_pool_submit(p, ptrs, g_lens, 10, &dig[0][0]) == -ENODEV, "sync, all lost");
+    CHECK(md5hip_pool_submit_async(p, ptrs, g_lens, 10, &dig[0][0], &t) == -ENODEV && t == 0, "async, all lost");
+    CHECK(md5hip_pool_host_fixed(p, g_blob, 4, 1000, 1000, &fx[0][0]) == -ENODEV, "fixed, all lost");
+    md5hip_pool_destroy(p);
+    CHECK(md5hip_pool_create(devs, 4, 0, 0, &p) == 0 && p, "create again");
 
     /* eight threads at once, tickets waited in reverse, half polled first */
     md5hip_pool_set_split(p, 4u << 20);

@@ -21,10 +21,10 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 EXE = os.path.join(REPO, "build", "c", "asio_scale")
 
 
-def _run(*args, timeout=120):
+def _run(*args, timeout=120, **extra):
     if not os.path.exists(EXE):
         pytest.fail(f"{EXE} missing: run __graft_entry__.build() (make -C tests/c)")
-    env = dict(os.environ, ASIO_WS_MIB="512")           # vectors spanning 512 MiB: cold, and quick to set up
+    env = dict(os.environ, ASIO_WS_MIB="512", **extra)  # vectors spanning 512 MiB: cold, and quick to set up
     out = subprocess.run([EXE, *map(str, args)], capture_output=True, text=True, timeout=timeout, env=env)
     rec = json.loads(out.stdout.strip().splitlines()[-1])
     return out.returncode, rec
@@ -63,3 +63,19 @@ def test_asio_scale_cpu_per_call_bounded(cuda, target):
     assert c256 <= 1.5 * c8, (c8, c256)
     # the launches coalesce more callers as they grow
     assert res[256]["max_tickets_per_launch"] > res[8]["max_tickets_per_launch"]
+
+
+@pytest.mark.gpu
+def test_host_fixed_copy_is_not_under_the_batcher_lock(cuda):
+    """md5hip_batch_host_fixed from a 64 MiB PAGEABLE
+    array (its H2D copy is synchronous, milliseconds) on one thread while 7
+    threads make synchronous 64 x 16 KiB submits on the same batcher.  The
+    copy runs with the slot held as a writer and b->mu released
+    (md5_submit.c host_fixed), so no submitter's call waits for it: their
+    p99 latency stays below the fastest host_fixed call, and every digest of
+    both equals the oracle's."""
+    rc, rec = _run("batcher", 7, 64, 16384, 3.0, "pageable", ASIO_FIXED_BG_MIB="64")
+    assert rc == 0 and rec["mismatches"] == 0 and rec["rc"] == 0, rec
+    bg = rec["bg_fixed"]
+    assert bg["calls"] >= 3 and bg["mismatches"] == 0 and bg["rc"] == 0, bg
+    assert rec["lat_us"]["p99"] < bg["lat_us"]["min"], (rec["lat_us"], bg["lat_us"])

@@ -13,7 +13,14 @@ and every copy or kernel must be enqueued from its stream's device (waits
 and polls on another device's ticket included).  First, 64 blocked callers
 wait on one slot for 12 rounds, every other round with the watcher's spin
 ending on NotReady just as the launch completes (the round-3 lost wake-up,
-which hangs that phase).  Then large device-resident vectors (md5_submit.c
+which hangs that phase).  Then the device-failure policy: a device lost
+after launch K (its completion event reports the fault, or the launch itself
+fails, or md5hip_batcher_inject_fault) gives the failing ticket -EIO, the
+ticket coalescing behind it and every later call -ENODEV, with nothing
+enqueued again and no digest written; a 2-device pool moves a synchronous
+part off the failed device, never routes to it again, returns -ENODEV once
+every device failed, and 8 threads keep getting correct digests while a
+device dies under them.  Then large device-resident vectors (md5_submit.c
 reserve_device), three coalesced in one slot with their device digests
 scattered in pieces; the fake planner rejects a histogram that misses a
 chunk.  Runs under ASan+UBSan and under ThreadSanitizer
@@ -47,6 +54,7 @@ def _build_and_run(name, san, env_extra, secs):
     assert out.stdout.strip().endswith("batcher ok")
     assert "blocked callers: 12 rounds x 64 waiters on one slot ok" in out.stdout
     assert "large device submissions ok" in out.stdout
+    assert "device lost: -EIO / -ENODEV / failover ok" in out.stdout
 
 
 def test_batcher_under_asan():

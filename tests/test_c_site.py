@@ -2,7 +2,10 @@
 (tests/c/netcache_site.c) linked against libmd5hip.so: page-list blocks, MD5,
 CRC-32 / fastcrc, batched verify with one corrupted block, asynchronous
 submit, zero-copy gather modes, the multi-device pool and MD5Init/Update/Final,
-each block checked against the oracle.  No Python or torch between the caller
+each block checked against the oracle; then the failure policy of
+INTEGRATION.md §2j with a device fault injected under a vector (-EIO, no
+checksum stored, -ENODEV after, host fallback, no inode reset from a device
+error, pool failover).  No Python or torch between the caller
 and the library.  Built by __graft_entry__.build() (tests/c/Makefile)."""
 import os
 import subprocess
@@ -34,3 +37,4 @@ def test_c_site_on_gpu(cuda):
     out = _run(120)
     assert out.returncode == 0, (out.stdout + out.stderr)[-3000:]
     assert "netcache_site ok" in out.stdout
+    assert "failure policy ok" in out.stdout

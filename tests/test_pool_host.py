@@ -3,7 +3,9 @@ device: tests/c/pool_check.c links md5_pool.c against a fake batcher that
 hashes on the CPU (the library's host MD5 / CRC-32) and completes tickets
 only after a few polls, failing some on purpose.  Routing, whole and split
 submissions, digest placement, split-ticket bookkeeping, per-ticket errors,
-stats and 8 concurrent submitting threads -- under ASan+UBSan, and under
+stats, lost devices (a synchronous split part moved off the failed device,
+the device never routed to again, an asynchronous ticket keeping -EIO,
+-ENODEV once every device failed) and 8 concurrent submitting threads -- under ASan+UBSan, and under
 ThreadSanitizer for the lock-free routing and the ticket table."""
 import os
 import shutil
