@@ -32,7 +32,7 @@ extern "C" {
 
 /* ABI 4 (round 5): device failure -- md5hip_batcher_health /
  * md5hip_batcher_inject_fault, md5hip_pool_get_health / _device_health /
- * _inject_fault (appended); md5hip_batcher_set_chain rejects modes outside
+ * _inject_fault -- and md5_batch_submit_device_fixed (appended); md5hip_batcher_set_chain rejects modes outside
  * 0..2 with -EINVAL.
  * ABI 3 (round 4): md5_batch_submit_device_after (an ordering flag apart from
  * the producer stream, so the null stream can be ordered on), the LINES
@@ -402,6 +402,17 @@ int md5_batch_submit_device_on(md5hip_batcher *b, const uint64_t *d_ptrs, const 
 int md5_batch_submit_device_after(md5hip_batcher *b, const uint64_t *d_ptrs, const uint32_t *lens,
                                   uint64_t n, unsigned char *digests, int digests_on_device,
                                   void *producer_stream, int order, uint64_t *ticket);
+/* ABI 4: fixed-length device-resident chunks, digest i of (d_base +
+ * i*stride, len) -- the queue form of md5hip_digest_fixed / crc32hip_fixed:
+ * no per-chunk descriptor crosses PCIe (12 B per chunk through the other
+ * device entries, more than a fastcrc window's HBM bytes cost), each slice
+ * of at most max_chunks chunks is one launch of its own on the queue's
+ * streams (several in flight overlap), digests in the batcher's kind.
+ * producer_stream / order as md5_batch_submit_device_after; ticket NULL =
+ * synchronous. */
+int md5_batch_submit_device_fixed(md5hip_batcher *b, const void *d_base, uint64_t n, uint32_t len,
+                                  uint64_t stride, unsigned char *digests, int digests_on_device,
+                                  void *producer_stream, int order, uint64_t *ticket);
 /* Block until submission `ticket` has delivered its digests: 0 or -errno.
  * A ticket still coalescing in the open slot is launched at once when
  * nothing is in flight (no linger); otherwise its slot goes out as soon as a
@@ -516,9 +527,10 @@ int md5hip_pool_device_stats(md5hip_pool *p, uint32_t g, struct md5hip_batcher_s
  * device took its chunks (-ENODEV) is routed to another one; a synchronous
  * submission (or split part) whose launch then fails is resubmitted on a
  * healthy device from the caller's still-valid buffers, so it returns 0 as
- * long as one device is left.  An asynchronous ticket whose launch fails
- * completes with -EIO (its buffers may be gone by the wait).  With every
- * device failed, submissions return -ENODEV.
+ * long as one device is left.  An asynchronous ticket on a device that
+ * fails completes with -EIO (its launch failed) or -ENODEV (it had not
+ * been launched yet): it is not moved, as its buffers may be gone by the
+ * wait.  With every device failed, submissions return -ENODEV.
  * md5hip_pool_device_health: 0 / -ENODEV for device index g (-EINVAL
  * past ndev); md5hip_pool_inject_fault: md5hip_batcher_inject_fault on
  * device index g. */

@@ -156,6 +156,7 @@ def lib():
         "md5hip_pool_get_health": (i, [vp, ctypes.POINTER(MD5HipPoolHealth)]),
         "md5hip_pool_device_health": (i, [vp, u32]),
         "md5hip_pool_inject_fault": (i, [vp, u32, u64]),
+        "md5_batch_submit_device_fixed": (i, [vp, vp, u64, u32, u64, vp, i, vp, i, vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -192,7 +193,7 @@ EXPORTS = ["MD5Init", "MD5Update", "MD5Final", "nc_MD5Init", "nc_MD5Update", "nc
            "md5hip_pool_get_stats", "md5hip_pool_device_stats", "md5_batch_submit_device_on",
            "md5_batch_submit_device_after", "md5hip_plan_desc_at", "md5hip_batcher_set_chain",
            "md5hip_batcher_health", "md5hip_batcher_inject_fault", "md5hip_pool_get_health",
-           "md5hip_pool_device_health", "md5hip_pool_inject_fault"]
+           "md5hip_pool_device_health", "md5hip_pool_inject_fault", "md5_batch_submit_device_fixed"]
 
 
 def check(fn, rc):

@@ -1177,7 +1177,7 @@ md5_desc_fed(const uint8_t* __restrict__ base, const uint64_t* __restrict__ offs
 // (coalesced C3 submissions), the hardware's placement -- all waves resident
 // at once, ~5 per SIMD, a strided slice of the order on each -- leaves SIMDs
 // loaded unevenly: 1 MiB chains ran 2x their solo time sharing a SIMD and
-// SIMDs went idle from 54 % of the launch on (scripts/c3_trace_x.py,
+// SIMDs went idle from 54 % of the launch on (scripts/c3_trace_x.py, deleted in 4de68d0,
 // profiles/r02_c3_trace.json).  Here every SIMD takes the next-longest group
 // whenever its wave frees up.  ctr[0] hands out groups, ctr[1] counts waves
 // done; the last wave out resets both, so a counter serves the next launch

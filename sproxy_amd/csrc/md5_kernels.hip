@@ -251,7 +251,7 @@ int md5hip_digest_desc_variant(const void* d_base, const uint64_t* d_offsets,
   // LANE.  One wave per workgroup: a mixed batch has few waves, and the
   // dispatcher then spreads them one per CU instead of packing 4 onto one CU
   // where the long chunks' lane-direct loads contend for the CU's address unit
-  // (scripts/c3_trace.py: 28.7 -> 13.2 ms on the C3 batch).
+  // (scripts/c3_trace.py, deleted in 4de68d0: 28.7 -> 13.2 ms on the C3 batch).
   hipLaunchKernelGGL(md5_desc<false>, dim3((uint32_t)g), dim3(kDescBlock), 0, s, base, d_offsets,
                      d_lens, d_order, n, (uint64_t)0, 0u, (uint4*)d_digests);
   return launched();
@@ -550,7 +550,7 @@ int md5hip_plan_order(const uint32_t* lens, uint64_t n, uint32_t* order) {
 // tables can use large fragments throughout.  A lane-direct chain walks its
 // own chunk, so a wave touches 64 distinct pages per load; HYBRID's long
 // chains on C3 ran 9.7 ms in a 16 MiB-aligned buffer and 10.4-11.5 ms in a
-// 2 MiB-aligned one (scripts/alloc_probe.py).  The whole-line
+// 2 MiB-aligned one (scripts/alloc_probe.py, deleted in 4de68d0).  The whole-line
 // loaders are indifferent.
 // ---------------------------------------------------------------------------
 namespace {

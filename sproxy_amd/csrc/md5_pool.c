@@ -25,7 +25,8 @@
  * finds its device failed before the device took it (-ENODEV) goes to
  * another; a synchronous submission or part whose launch failed with its
  * device is resubmitted on a healthy one from the caller's buffers (still
- * valid: the call has not returned); an asynchronous ticket keeps its -EIO.
+ * valid: the call has not returned); an asynchronous ticket keeps its -EIO
+ * (or -ENODEV if it was still coalescing).
  *
  * Tickets: a submission routed whole is (batcher ticket << 6) | device; a
  * split one is bit 63 | id, its parts kept in `mt` (ascending ids) until all

@@ -208,8 +208,10 @@ struct slot {
     int state, mode, writers, full, flush, err;
     uint64_t n, used, nseg, ndma, ndsc;
     uint32_t kind, fastcrc, dsz;
-    /* MODE_FIXED (md5hip_batch_host_fixed): one contiguous host range */
+    /* MODE_FIXED (md5hip_batch_host_fixed): one contiguous host range, or
+     * (fx_dev, md5_batch_submit_device_fixed) one device range read in place */
     const unsigned char *fx_src;
+    int fx_dev;
     uint64_t fx_bytes, fx_stride;
     uint32_t fx_len;
     uint64_t tickets_in;              /* distinct tickets (stats) */
@@ -417,14 +419,23 @@ static int slot_enqueue(md5hip_batcher *b, struct slot *sl)
 {
     int rc = 0;
     const uint64_t n = sl->n;
+    /* one submission whose digests stay on the device and fill the slot in
+     * order: the kernel writes them in place (no scatter launch) */
+    const struct seg *g0 = sl->nsegs == 1 ? &sl->segs[0] : NULL;
+    unsigned char *dst = sl->d_dig;
+    if (g0 && g0->on_device && g0->first == 0 && g0->count == n && ((uintptr_t)g0->user & 15u) == 0) {
+        dst = g0->user;
+        sl->direct = 1;
+    }
     if (sl->mode == MODE_FIXED) {
-        /* the bytes are on their way already (host_fixed enqueued the copy
-         * on this stream outside b->mu) */
+        /* host_fixed: the bytes are on their way already (its copy was
+         * enqueued on this stream outside b->mu); device_fixed: they are
+         * read where the caller keeps them */
+        const void *src = sl->fx_dev ? (const void *)sl->fx_src : (const void *)sl->d_data;
         if (sl->chain_ev && hipStreamWaitEvent(sl->stream, sl->chain_ev, 0) != hipSuccess) return -EIO;
         rc = sl->kind == MD5HIP_DIGEST_CRC32
-                 ? crc32hip_fixed(sl->d_data, n, sl->fx_len, sl->fx_stride, sl->fastcrc,
-                                  (uint32_t *)sl->d_dig, sl->stream)
-                 : md5hip_digest_fixed(sl->d_data, n, sl->fx_len, sl->fx_stride, sl->d_dig, sl->stream);
+                 ? crc32hip_fixed(src, n, sl->fx_len, sl->fx_stride, sl->fastcrc, (uint32_t *)dst, sl->stream)
+                 : md5hip_digest_fixed(src, n, sl->fx_len, sl->fx_stride, dst, sl->stream);
         if (rc) return rc;
         if (hipEventRecord(sl->kdone, sl->stream)) return -EIO;
     } else {
@@ -452,15 +463,6 @@ static int slot_enqueue(md5hip_batcher *b, struct slot *sl)
                                        sl->stream) != hipSuccess)
                         return -EIO;
             }
-        }
-        /* one submission whose digests stay on the device and fill the slot
-         * in order: the kernel writes them in place (no scatter launch) */
-        const struct seg *g0 = sl->nsegs == 1 ? &sl->segs[0] : NULL;
-        unsigned char *dst = sl->d_dig;
-        if (g0 && g0->on_device && g0->first == 0 && g0->count == n &&
-            ((uintptr_t)g0->user & 15u) == 0) {
-            dst = g0->user;
-            sl->direct = 1;
         }
         /* a chained launch: bytes in and plan made beside the running
          * launch, the hash kernel after it */
@@ -529,6 +531,7 @@ static void slot_reset(struct slot *sl)
     sl->chain_overlap = 0;
     sl->urgent = 0;
     sl->inject = 0;
+    sl->fx_dev = 0;
     sl->mode = MODE_NONE;
     sl->writers = sl->full = sl->flush = sl->err = sl->direct = 0;
     sl->n = sl->used = sl->nseg = sl->ndma = sl->ndsc = 0;
@@ -647,8 +650,9 @@ static void slot_try_launch(md5hip_batcher *b, struct slot *sl)
     if (b->open == (int)(sl - b->s)) b->open = -1;
     const int rc = sl->err ? sl->err : b->failed ? b->failed : slot_enqueue(b, sl);
     if (rc) {
-        /* an enqueue that failed because the device did: the stream says so */
-        const int lost = !sl->err && !b->failed && hip_lost(hipStreamQuery(sl->stream));
+        /* an enqueue (here, or a descriptor copy or ordering made earlier:
+         * sl->err) that failed because the device did: the stream says so */
+        const int lost = !b->failed && rc != -ENODEV && hip_lost(hipStreamQuery(sl->stream));
         slot_retire(b, sl, rc);
         if (lost) batcher_fail(b);
         return;
@@ -1807,16 +1811,21 @@ int md5_batch_submit_device(md5hip_batcher *b, const uint64_t *d_ptrs, const uin
     return submit(b, &src, n, digests, digests_on_device != 0, 0, NULL, -1, 0, NULL);
 }
 
-/* Fixed-length chunks straight from one contiguous host range (MODE_FIXED:
- * one H2D copy per slot, no host gather).  ticket NULL = synchronous. */
-static int host_fixed(md5hip_batcher *b, int kind, uint32_t fastcrc, const void *h_base, uint64_t n,
-                      uint32_t len, uint64_t stride, unsigned char *digests, uint64_t *ticket)
+/* Fixed-length chunks from one contiguous range (MODE_FIXED), one slot per
+ * slice of it: host memory (dev_src 0: one H2D copy per slot, no host
+ * gather) or device memory (dev_src 1: read in place, no per-chunk
+ * descriptor -- md5_batch_submit_device_fixed).  Digests to host memory, or
+ * device memory when dig_dev.  after != NULL: the producer's stream, as
+ * submit().  ticket NULL = synchronous. */
+static int fixed_submit(md5hip_batcher *b, int kind, uint32_t fastcrc, const void *base, int dev_src,
+                        uint64_t n, uint32_t len, uint64_t stride, unsigned char *digests, int dig_dev,
+                        const hipStream_t *after, uint64_t *ticket)
 {
-    if (stride > b->cap) return -E2BIG;
+    if (!dev_src && stride > b->cap) return -E2BIG;
     struct dev_guard g;
     if (dev_enter(&g, b->device)) return -ENODEV;
-    const unsigned char *src = (const unsigned char *)h_base;
-    uint64_t per = b->cap / stride;
+    const unsigned char *src = (const unsigned char *)base;
+    uint64_t per = dev_src ? b->maxn : b->cap / stride;
     if (per > b->maxn) per = b->maxn;
     pthread_mutex_lock(&b->mu);
     if (kind < 0) {
@@ -1826,6 +1835,10 @@ static int host_fixed(md5hip_batcher *b, int kind, uint32_t fastcrc, const void 
     const uint32_t dsz = kind == MD5HIP_DIGEST_CRC32 ? 4 : 16;
     uint64_t t = 0;
     int rc = b->failed ? b->failed : tk_new(b, &t);
+    if (rc == 0 && after && hipEventRecord(b->after_ev, *after) != hipSuccess) {
+        tk_put(b, t, 0);
+        rc = -EINVAL;                              /* not a stream of this device */
+    }
     if (rc) {
         pthread_mutex_unlock(&b->mu);
         dev_leave(&g);
@@ -1834,8 +1847,8 @@ static int host_fixed(md5hip_batcher *b, int kind, uint32_t fastcrc, const void 
     b->st.submissions++;
     for (uint64_t i = 0; i < n && !rc; i += per) {
         const uint64_t m = n - i < per ? n - i : per;
-        /* straight from the caller's (ideally pinned) buffer: no host gather,
-         * a slot of its own (the open slot keeps coalescing other work) */
+        /* straight from the caller's buffer: a slot of its own (the open
+         * slot keeps coalescing other work) */
         struct slot *sl = b->failed ? NULL : slot_take(b, MODE_FIXED, kind, fastcrc);
         if (!sl || b->failed) {              /* the device failed (slot_take may wait) */
             if (sl) slot_retire(b, sl, -ENODEV);
@@ -1844,30 +1857,40 @@ static int host_fixed(md5hip_batcher *b, int kind, uint32_t fastcrc, const void 
         }
         sl->n = m;
         sl->fx_src = src + i * stride;
+        sl->fx_dev = dev_src;
         sl->fx_bytes = (m - 1) * stride + len;
         sl->fx_len = len;
         sl->fx_stride = stride;
         sl->full = 1;
         sl->load = m * ((uint64_t)len + 64);
         __atomic_store_n(&b->load_bytes, b->load_bytes + sl->load, __ATOMIC_RELAXED);
-        if ((rc = seg_push(sl, (struct seg){t, 0, m, digests + (size_t)dsz * i, 0}))) {
+        if ((rc = seg_push(sl, (struct seg){t, 0, m, digests + (size_t)dsz * i, dig_dev}))) {
             slot_retire(b, sl, rc);
             break;
         }
         tk_ring_ref(&b->tk, t);
-        /* the H2D copy outside the lock, the slot held by this writer: from
-         * pageable memory it is synchronous (a 128 MiB slice is tens of ms
-         * over PCIe), and every other submitter and waiter needs b->mu
-         * meanwhile.  Nothing else touches a FIXED slot's stream until its
-         * writers are done (slot_try_launch waits for writers == 0). */
-        sl->writers++;
-        pthread_mutex_unlock(&b->mu);
-        const hipError_t ce = hipMemcpyAsync(sl->d_data, sl->fx_src, sl->fx_bytes, hipMemcpyHostToDevice,
-                                             sl->stream);
-        pthread_mutex_lock(&b->mu);
-        sl->writers--;
-        if (ce != hipSuccess && !sl->err) sl->err = -EIO;
-        if (ce != hipSuccess && hip_lost(hipStreamQuery(sl->stream))) batcher_fail(b);
+        /* the producer's work before this call, before this slot's kernel
+         * (recorded again per slot: slot_take may have let another producer
+         * record the event meanwhile) */
+        if (after && (hipEventRecord(b->after_ev, *after) != hipSuccess ||
+                      hipStreamWaitEvent(sl->stream, b->after_ev, 0) != hipSuccess))
+            sl->err = -EIO;
+        if (!dev_src) {
+            /* the H2D copy outside the lock, the slot held by this writer:
+             * from pageable memory it is synchronous (a 128 MiB slice is tens
+             * of ms over PCIe), and every other submitter and waiter needs
+             * b->mu meanwhile.  Nothing else touches a FIXED slot's stream
+             * until its writers are done (slot_try_launch waits for
+             * writers == 0). */
+            sl->writers++;
+            pthread_mutex_unlock(&b->mu);
+            const hipError_t ce = hipMemcpyAsync(sl->d_data, sl->fx_src, sl->fx_bytes, hipMemcpyHostToDevice,
+                                                 sl->stream);
+            pthread_mutex_lock(&b->mu);
+            sl->writers--;
+            if (ce != hipSuccess && !sl->err) sl->err = -EIO;
+            if (ce != hipSuccess && hip_lost(hipStreamQuery(sl->stream))) batcher_fail(b);
+        }
         slot_try_launch(b, sl);
     }
     tk_put(b, t, rc);
@@ -1879,6 +1902,25 @@ static int host_fixed(md5hip_batcher *b, int kind, uint32_t fastcrc, const void 
     pthread_mutex_unlock(&b->mu);
     dev_leave(&g);
     return rc;
+}
+
+static int host_fixed(md5hip_batcher *b, int kind, uint32_t fastcrc, const void *h_base, uint64_t n,
+                      uint32_t len, uint64_t stride, unsigned char *digests, uint64_t *ticket)
+{
+    return fixed_submit(b, kind, fastcrc, h_base, 0, n, len, stride, digests, 0, NULL, ticket);
+}
+
+int md5_batch_submit_device_fixed(md5hip_batcher *b, const void *d_base, uint64_t n, uint32_t len,
+                                  uint64_t stride, unsigned char *digests, int digests_on_device,
+                                  void *producer_stream, int order, uint64_t *ticket)
+{
+    if (ticket) *ticket = 0;
+    if (!b) return -EINVAL;
+    if (n == 0) return 0;
+    if (!d_base || !digests || len > stride) return -EINVAL;
+    const hipStream_t after = (hipStream_t)producer_stream;
+    return fixed_submit(b, -1, 0, d_base, 1, n, len, stride, digests, digests_on_device != 0,
+                        order ? &after : NULL, ticket);
 }
 
 int md5_batch_submit_device_after(md5hip_batcher *b, const uint64_t *d_ptrs, const uint32_t *lens,

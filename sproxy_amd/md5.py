@@ -356,9 +356,10 @@ class Batcher:
                submit_device_async="md5_batch_submit_device_async",
                submit_device="md5_batch_submit_device", submit_device_on="md5_batch_submit_device_on",
                submit_device_after="md5_batch_submit_device_after",
+               submit_device_fixed="md5_batch_submit_device_fixed",
                set_inflight="md5hip_batcher_set_inflight",
                set_linger="md5hip_batcher_set_linger", set_chain="md5hip_batcher_set_chain",
-               stats="md5hip_batcher_get_stats")
+               stats="md5hip_batcher_get_stats", inject_fault="md5hip_batcher_inject_fault")
 
     def __init__(self, device: int = 0, slice_bytes: int = 0, nslots: int = 0,
                  kind: int = 0, fastcrc: int = 0):
@@ -518,13 +519,15 @@ class Batcher:
         """(stream handle, order) for md5_batch_submit_device_after:
         'current' = torch's current stream on the batcher's device -- its
         handle is 0 (NULL) when that is the default stream, which the library
-        then orders on as the null stream, never as "no ordering"; None = no
+        then orders on as the null stream, never as "no ordering"; without
+        torch, 'current' is the null stream of the batcher's device (what a
+        raw-HIP producer enqueues on when it names no stream); None = no
         ordering."""
         if isinstance(after, str):
             if after != "current":
                 raise ValueError("after: 'current', None or a stream")
             if torch is None:
-                raise RuntimeError("after='current' needs torch; pass a stream handle or None")
+                return None, 1
             return torch.cuda.current_stream(self.device).cuda_stream, 1
         if after is None:
             return None, 0
@@ -551,8 +554,42 @@ class Batcher:
                           *self._producer(after), None))
         return o if on_dev else self._ret(o, P.size)
 
+    def submit_device_fixed_async(self, base, n: int, length: int, stride: int = None, out=None,
+                                  after="current") -> "Batcher.Pending":
+        """md5_batch_submit_device_fixed (ABI 4): digest i of (base + i*stride,
+        length) for a device tensor (or device address) `base` on the
+        batcher's device, read in place -- no per-chunk descriptor; digests in
+        the batcher's kind into `out` (a device tensor, or by default a host
+        array returned by .wait()); `after` as submit_device_async."""
+        stride = stride or length
+        if n and length > stride:
+            raise ValueError("length > stride")
+        if torch is not None and isinstance(base, torch.Tensor):
+            if not base.is_cuda or base.device.index != self.device:
+                raise ValueError(f"base must be a device tensor on cuda:{self.device}")
+            if n and base.numel() * base.element_size() < (n - 1) * stride + length:
+                raise ValueError("base is smaller than n chunks of the stride")
+            addr = base.data_ptr()
+        else:
+            addr = int(base)
+        _, _, o, on_dev = self._dev_args(np.zeros(n, np.uint64), np.zeros(n, np.uint32), out)
+        t = ctypes.c_uint64()
+        dst = o.data_ptr() if on_dev else o.ctypes.data
+        check(*self._call("submit_device_fixed", ctypes.c_void_p(addr), n, length, stride, dst, on_dev,
+                          *self._producer(after), ctypes.byref(t)))
+        return Batcher.Pending(self, t.value, o, n, (base, o), on_dev)
+
     def flush(self):
         check(*self._call("flush"))
+
+    def health(self) -> int:
+        """0 healthy, -ENODEV once the device failed (ABI 4, sticky)."""
+        return lib().md5hip_batcher_health(self._h)
+
+    def inject_fault(self, after: int = 1):
+        """Test control (ABI 4): the after-th launch from now completes as a
+        device fault (its tickets -EIO, the batcher failed from then on)."""
+        check(*self._call("inject_fault", ctypes.c_uint64(after)))
 
     def set_inflight(self, target: int):
         """Launch the open slot at once while fewer than `target` slots run."""
@@ -650,6 +687,16 @@ class Pool(Batcher):
         """Submissions heavier than `nbytes` are cut over devices (0 = one slice)."""
         check(*self._call("set_split", nbytes))
 
+    def health(self) -> dict:
+        """md5hip_pool_get_health (ABI 4): failed devices and failovers."""
+        from ._lib import MD5HipPoolHealth
+        h = MD5HipPoolHealth()
+        check("md5hip_pool_get_health", lib().md5hip_pool_get_health(self._h, ctypes.byref(h)))
+        return {"ndev": h.ndev, "nfailed": h.nfailed, "failed_mask": h.failed_mask, "failovers": h.failovers}
+
+    def inject_fault(self, g: int, after: int = 1):
+        check("md5hip_pool_inject_fault", lib().md5hip_pool_inject_fault(self._h, g, ctypes.c_uint64(after)))
+
     def stats(self) -> dict:
         """Routing counters: submissions, routed_whole, split, parts."""
         st = MD5HipPoolStats()
@@ -665,7 +712,8 @@ class Pool(Batcher):
     def _unsupported(self, *a, **k):
         raise NotImplementedError("device-resident chunks belong to one device: use a Queue")
 
-    submit_device = submit_device_async = flush = set_inflight = set_linger = _unsupported
+    submit_device = submit_device_async = submit_device_fixed_async = flush = set_inflight = set_linger = \
+        _unsupported
 
 
 def register_host(arr: np.ndarray):

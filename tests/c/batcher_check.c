@@ -5,6 +5,7 @@
  * ASan+UBSan or TSan (tests/test_batcher_host.py).  Every thread picks
  * random operations -- synchronous / asynchronous submits of pointer lists
  * and page lists, verify with a flipped digest, host_fixed, device-resident
+ * fixed-length runs (md5_batch_submit_device_fixed), device-resident
  * submits with host or device digests (also ordered after a producer
  * stream), pool submits whole and split, CRC-32 on its own batcher, netcache
  * header verification, flush -- from pageable or registered memory, and
@@ -126,7 +127,7 @@ static void *worker(void *arg)
             lens[i] = g_lens[idx[i]];
             dptrs[i] = (uint64_t)(uintptr_t)(g_heap + g_offs[idx[i]]);
         }
-        const int op = (int)(rnd(&s) % 12);
+        const int op = (int)(rnd(&s) % 13);
         int rc = 0;
         memset(dig, 0, sizeof dig);
         switch (op) {
@@ -247,6 +248,32 @@ static void *worker(void *arg)
             uint32_t fc;
             if ((rc = md5hip_batcher_get_digest(g_crcb, &kind, &fc)) || kind != MD5HIP_DIGEST_CRC32 || fc)
                 fail("get_digest", t, rc);
+            break;
+        }
+        case 11: {
+            /* device-resident fixed-length chunks on the queue, host or device
+             * digests (the latter odd-aligned half the time: scattered) */
+            const uint32_t L = 4096;
+            const uint64_t k = rnd(&s) % 300;
+            const int m = 1 + (int)(rnd(&s) % 60);
+            const unsigned char *base = g_heap + k * L;
+            unsigned char *raw = malloc(16 * (size_t)m + 20);
+            unsigned char *d = rnd(&s) & 1 ? raw + (rnd(&s) & 1 ? 0 : 4) : &dig[0][0];
+            const int on_dev = d != &dig[0][0];
+            uint64_t tk = 0;
+            const int async = (int)(rnd(&s) & 1);
+            rc = md5_batch_submit_device_fixed(g_q, base, (uint64_t)m, L, L, d, on_dev, NULL, 0, async ? &tk : NULL);
+            if (!rc && async) rc = md5_batch_wait(g_q, tk);
+            for (int i = 0; i < m && !rc; i++) {
+                unsigned char w[16];
+                struct MD5Context c;
+                MD5Init(&c);
+                MD5Update(&c, base + (uint64_t)i * L, L);
+                MD5Final(w, &c);
+                if (memcmp(w, d + 16 * i, 16)) rc = -2500 - i;
+            }
+            free(raw);
+            if (rc) fail("device_fixed", t, rc);
             break;
         }
         default: {
@@ -653,10 +680,10 @@ static int lost_pool_all(int d0, int d1)
 }
 
 /* 8 threads on a pool while one of its devices dies under them: synchronous
- * calls all succeed (moved), asynchronous ones succeed or get -EIO */
+ * calls all succeed (moved), asynchronous ones succeed or get -EIO / -ENODEV */
 struct lj {
     md5hip_pool *p;
-    int t, ops, bad, sync_err, async_eio, other;
+    int t, ops, bad, sync_err, async_eio, other, last_rc;
 };
 
 static void *lost_worker(void *arg)
@@ -686,15 +713,17 @@ static void *lost_worker(void *arg)
             first[n] = (uint64_t)n;
             for (int i = 0; i < n; i++) memcpy(dig[i], g_md5[idx[i]], 16);
             rc = md5hip_pool_verify_iov(j->p, segs, first, (uint64_t)n, dig, ok);
-            if (rc != 0) j->sync_err++;                  /* 0 mismatches, never a device error */
+            if (rc != 0) j->sync_err++, j->last_rc = rc;   /* 0 mismatches, never a device error */
             continue;
         } else {
             uint64_t t;
             rc = md5hip_pool_submit_async(j->p, ptrs, lens, (uint64_t)n, &dig[0][0], &t);
             if (rc == 0) rc = md5hip_pool_wait(j->p, t);
-            if (rc == -EIO) { j->async_eio++; continue; }
+            /* its launch failed (-EIO), or it was still coalescing when the
+             * device failed (-ENODEV): an asynchronous ticket is not moved */
+            if (rc == -EIO || rc == -ENODEV) { j->async_eio++; continue; }
         }
-        if (rc) j->sync_err++;
+        if (rc) j->sync_err++, j->last_rc = rc;
         else if (!check_md5(dig, idx, n)) j->bad++;
     }
     return NULL;
@@ -711,21 +740,21 @@ static int lost_pool_threads(int d0, int d1)
     struct lj jobs[LT];
     pthread_t th[LT];
     for (int t = 0; t < LT; t++) {
-        jobs[t] = (struct lj){p, t, 40, 0, 0, 0, 0};
+        jobs[t] = (struct lj){p, t, 40, 0, 0, 0, 0, 0};
         pthread_create(&th[t], NULL, lost_worker, &jobs[t]);
     }
     int eio = 0;
+    for (int t = 0; t < LT; t++) pthread_join(th[t], NULL);
     for (int t = 0; t < LT; t++) {
-        pthread_join(th[t], NULL);
-        LCHECK(jobs[t].bad == 0 && jobs[t].sync_err == 0, "thread %d: bad %d sync errors %d", t, jobs[t].bad,
-               jobs[t].sync_err);
+        LCHECK(jobs[t].bad == 0 && jobs[t].sync_err == 0, "thread %d: bad %d sync errors %d (last rc %d)", t,
+               jobs[t].bad, jobs[t].sync_err, jobs[t].last_rc);
         eio += jobs[t].async_eio;
     }
     struct md5hip_pool_health h;
     md5hip_pool_get_health(p, &h);
     LCHECK(fake_hip_device_faulted(d1) && h.nfailed == 1 && h.failed_mask == 2, "health mask %llx",
            (unsigned long long)h.failed_mask);
-    printf("device lost under 8 threads: %llu failovers, %d async -EIO\n", (unsigned long long)h.failovers, eio);
+    printf("device lost under 8 threads: %llu failovers, %d async tickets failed\n", (unsigned long long)h.failovers, eio);
     md5hip_pool_destroy(p);
     return 0;
 }
@@ -761,6 +790,7 @@ static void *watchdog(void *arg)
 int main(int argc, char **argv)
 {
     const double secs = argc > 1 ? atof(argv[1]) : 4.0;
+    setvbuf(stdout, NULL, _IOLBF, 0);             /* a crash still shows the phase it was in */
     uint64_t s = 0x1234567ull, total = 0;
     for (int i = 0; i < NCH; i++) {
         const uint64_t r = rnd(&s);

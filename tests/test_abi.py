@@ -144,6 +144,28 @@ def test_argument_errors_before_device_work():
     assert L.md5hip_pool_device_stats(None, 0, None) == EINVAL
     assert L.md5hip_pool_set_digest(None, 0, 0) == EINVAL
     assert L.md5_batch_submit_device_on(None, None, None, 1, None, 0, None, None) == EINVAL
+    # set_chain: modes outside 0..2 are refused before the batcher is touched
+    assert L.md5hip_batcher_set_chain(None, 1) == EINVAL
+    assert L.md5hip_batcher_set_chain(ctypes.c_void_p(16), 3) == EINVAL
+    assert L.md5hip_batcher_set_chain(ctypes.c_void_p(16), -1) == EINVAL
+    # ABI 4 failure-policy entries
+    assert L.md5hip_batcher_health(None) == EINVAL
+    assert L.md5hip_batcher_inject_fault(None, 1) == EINVAL
+    assert L.md5hip_pool_get_health(None, None) == EINVAL
+    assert L.md5hip_pool_device_health(None, 0) == EINVAL
+    assert L.md5hip_pool_inject_fault(None, 0, 1) == EINVAL
+
+
+def test_producer_default_without_torch(monkeypatch):
+    """Batcher.submit_device*(after='current') without torch orders on the
+    null stream of the batcher's device (what a raw-HIP producer uses when
+    it names no stream), instead of failing on its own default argument."""
+    import types
+    monkeypatch.setattr(m, "torch", None)
+    b = types.SimpleNamespace(device=0)
+    assert m.Batcher._producer(b, "current") == (None, 1)
+    assert m.Batcher._producer(b, None) == (None, 0)
+    assert m.Batcher._producer(b, 1234) == (1234, 1)
 
 
 def test_plan_order_longest_first():

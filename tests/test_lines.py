@@ -36,11 +36,29 @@ def test_plan_desc_at_picks_lines_for_unlined_batches():
     assert m.plan_desc(lens)[1] == "xdma"
     assert m.plan_desc_at(lens, np.asarray(offs16, np.uint64))[1] == "lines"
     assert m.plan_desc_at(lens, np.asarray(offs128, np.uint64))[1] == "xdma"
-    # half or less of the bytes off their lines: XDMA stays
-    mixed = np.asarray([o if i % 2 else (o + 127) // 128 * 128 for i, o in enumerate(offs16)], np.uint64)
-    assert m.plan_desc_at(lens, mixed)[1] in ("xdma", "lines")
     with pytest.raises(ValueError):
         m.plan_desc_at(lens, np.zeros(3, np.uint64))
+
+
+def test_plan_desc_at_boundary_is_more_than_half_the_bytes():
+    """md5hip_lines_choice: LINES once 2 x unlined bytes > the batch's bytes.
+    Groups of 8 chunks (one of 9,000 B, seven of 16 KiB) are all 128-B
+    aligned, or all shifted 16 B off the line; half of the groups shifted is
+    exactly half the bytes (XDMA stays), and one lined chunk 16 B shorter
+    tips it over (LINES)."""
+    n = 256 * 64 * 3
+    lens = np.full(n, 16384, np.uint32)
+    lens[::8] = 9000
+    offs = np.arange(n, dtype=np.uint64) * np.uint64(16384 + 256) + np.uint64(128)
+    unlined = (np.arange(n) // 8) % 2 == 1                # every other group of 8
+    addrs = offs + np.where(unlined, 16, 0).astype(np.uint64)
+    assert 2 * int(lens[unlined].sum()) == int(lens.sum())
+    assert m.plan_desc(lens)[1] == "xdma"
+    assert m.plan_desc_at(lens, addrs)[1] == "xdma"       # exactly half: stays
+    shorter = lens.copy()
+    shorter[np.flatnonzero(~unlined)[-1]] -= 16
+    assert 2 * int(shorter[unlined].sum()) == int(shorter.sum()) + 16
+    assert m.plan_desc_at(shorter, addrs)[1] == "lines"   # just over half
 
 
 @pytest.mark.gpu
