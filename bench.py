@@ -7,7 +7,7 @@ whole batch, inputs already in HBM (filled on the device by
 md5hip_fill_synthetic, per-rank seed).  Per GPU: 1,048,576 x 16 KiB (C2) at
 N = 1, 2,097,152 x 16 KiB (the C4 shard: 16 M chunks over 8 GPUs) at N > 1.
 
-    python bench.py [--gpus N --steps K --warmup W] [--config c2|c3|c3q|c5|crc]
+    python bench.py [--gpus N --steps K --warmup W] [--config c2|c3|c3q|c5|crc|crcq|ctx]
 
 N > 1: one process per GPU.  Under torch.distributed.run (WORLD_SIZE set) the
 ranks are the launcher's and WORLD_SIZE must equal N.  A plain
@@ -55,7 +55,7 @@ def parse_args(argv):
     p.add_argument("--warmup", type=int, default=20,
                    help="untimed launches first: the board settles its clock over the first ~15 "
                         "launches of a 3 ms kernel (slow start, profiles/r01_bench_kernel_trace_startup.json)")
-    p.add_argument("--config", default="c2", choices=["c2", "c3", "c3q", "c5", "crc", "ctx"])
+    p.add_argument("--config", default="c2", choices=["c2", "c3", "c3q", "c5", "crc", "crcq", "ctx"])
     p.add_argument("--chunks", type=int, default=0,
                    help="chunks per GPU (weak scaling); 0 = 1,048,576 (C2) at N=1, "
                         "2,097,152 (the C4 shard) at N>1")
@@ -93,6 +93,9 @@ def parse_args(argv):
     p.add_argument("--c3q-slots", type=int, default=4, help="--config c3q: queue slots")
     p.add_argument("--c3q-chain", type=int, default=2,
                    help="--config c3q: chained launches (md5hip_batcher_set_chain: 0 off, 1 on, 2 = on + BALANCED tails overlap, the default)")
+    p.add_argument("--crcq-subs", type=int, default=4,
+                   help="--config crcq: fixed-length device submissions per step through one queue")
+    p.add_argument("--crcq-chunks", type=int, default=1 << 20, help="--config crcq: blocks per submission")
     p.add_argument("--c5-chunks", type=int, default=1 << 18)
     p.add_argument("--c5-slice", type=int, default=64 << 20)
     return p.parse_args(argv)
@@ -545,6 +548,95 @@ def run_crc(a, rank, world, local, device, backend):
     return per_rank_line(res, rank, world, local, device, backend, float(n) * L * a.steps, wall, par)
 
 
+def run_crcq(a, rank, world, local, device, backend):
+    """The block checksum as a STREAM through the product's device-input
+    queue: --crcq-subs fixed-length submissions of
+    --crcq-chunks blocks per step (md5_batch_submit_device_fixed, ABI 4: no
+    per-block descriptor crosses PCIe), each its own launch on the queue's
+    slot streams, pipelined as --config c3q (step k submitted before step
+    k-1's tickets are waited for).  CRC-32 with --fastcrc F (default 128):
+    blk_make_crc reads F bytes at each end of a block (blk_io.c:408-424), so
+    the algorithmic bytes are 2F + 4 per block."""
+    L = a.len
+    F = a.fastcrc if a.fastcrc else 128
+    K, n = max(1, a.crcq_subs), a.crcq_chunks
+    data = torch.empty(K * n * L, dtype=torch.uint8, device="cuda")
+    m.fill_synthetic(data, seed=0xC4C0 + rank)
+    torch.cuda.synchronize()
+    outs = [[torch.empty(n, dtype=torch.int32, device="cuda") for _ in range(K)] for _ in range(2)]
+    q = m.Queue(device=torch.cuda.current_device(), max_chunks=n, nslots=max(4, K + 1))
+    q.set_digest(m.Batcher.CRC32, F)
+    base = data.data_ptr()
+
+    def submit(k):
+        return [q.submit_device_fixed_async(base + j * n * L, n, L, L, out=outs[k & 1][j], after=None)
+                for j in range(K)]
+
+    def drain(pend):
+        for pn in reversed(pend):
+            pn.wait()
+
+    def timed(fn):
+        torch.cuda.synchronize()
+        barrier(world)
+        t0 = time.perf_counter()
+        fn()
+        torch.cuda.synchronize()
+        wall = time.perf_counter() - t0
+        barrier(world)
+        return wall, max_over_ranks(wall, world)
+
+    def pipelined():
+        prev = submit(0)
+        for k in range(1, a.steps):
+            cur = submit(k)
+            drain(prev)
+            prev = cur
+        drain(prev)
+
+    for _ in range(a.warmup):
+        drain(submit(0))
+    wall_d, wall_d_max = timed(lambda: [drain(submit(0)) for _ in range(a.steps)])
+    wall, wall_max = timed(pipelined)
+    stats = q.stats()
+    q.close()
+    blocks = float(K * n)
+    read = 2 * F if 0 < F < L else L
+    alg = blocks * (read + 4)
+    kname = m.crc_kernel_name(L, F)
+    wl = f"crcq{K}@{n}x{L}f{F}"
+    traffic, tnote = load_traffic(a.traffic, kname, wl)
+    vbusy = load_valu_busy(a.traffic, kname, wl)
+    step_s = wall_max / a.steps
+    res = {"metric": f"device-resident fastcrc={F} CRC-32 (netcache blk_make_crc) blocks/s through md5hip_queue",
+           "value": round(blocks * world * a.steps / wall_max, 1), "unit": "blocks/s", "n_gpus": world,
+           "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(step_s * 1e3, 4),
+           "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32",
+           "data": "synthetic (device-generated splitmix words, per-rank seed)",
+           "config": {"workload": f"fastcrc stream: {K} fixed-length submissions of {n} x {L} B blocks per "
+                                  f"step, device-resident, through md5hip_queue (md5_batch_submit_device_fixed)",
+                      "submissions": K, "blocks_per_submission": n, "chunk_bytes": L, "fastcrc": F,
+                      "kernel": kname, "queue": stats},
+           "roofline": {"bound": "hbm", "achieved": round(alg / step_s / 1e9, 1), "peak": HBM_PEAK_GBS,
+                        "unit": "GB/s", "frac": round(alg / step_s / 1e9 / HBM_PEAK_GBS, 4),
+                        "traffic": traffic, "traffic_source": tnote, "valu_busy_pmc": vbusy,
+                        "kernel": "md5hip::" + kname + " (queue launches)",
+                        "alg_bytes_per_step": int(alg),
+                        "alg_bytes_note": f"{read} B read per block (+4 B CRC written); achieved: wall-clock "
+                                          f"per pipelined step (submit + wait); traffic: HBM bytes per launch "
+                                          f"({n} blocks)"},
+           "drained": {"value": round(blocks * world * a.steps / wall_d_max, 1), "unit": "blocks/s",
+                       "ms_per_step": round(wall_d_max / a.steps * 1e3, 4),
+                       "frac": round(alg / (wall_d_max / a.steps) / 1e9 / HBM_PEAK_GBS, 4)}}
+    par = None
+    if a.parity_sample:
+        ps = [crc_sample(data[j * n * L:(j + 1) * n * L], n, L, F, outs[(a.steps - 1) & 1][j],
+                         a.parity_sample // K, rank + 10 * j) for j in range(K)]
+        par = {"checked": sum(p.get("checked", 0) for p in ps), "mismatches": sum(p.get("mismatches", 0) for p in ps),
+               "ok": all(p["ok"] for p in ps), "checker": ps[0].get("checker")}
+    return per_rank_line(res, rank, world, local, device, backend, blocks * L * a.steps, wall, par)
+
+
 def crc_sample(data, n, L, F, out, k, rank):
     """Parity of the CRC line: the first, the last and seeded-random blocks
     re-checksummed on the host after the timed region by the CRC-32
@@ -995,7 +1087,7 @@ def main(argv=None):
         res = run_dry(a, rank, world, local, device, backend)
     else:
         res = {"c2": run_c2, "c3": run_c3, "c3q": run_c3q, "c5": run_c5, "crc": run_crc,
-               "ctx": run_ctx}[a.config](a, rank, world, local, device, backend)
+               "crcq": run_crcq, "ctx": run_ctx}[a.config](a, rank, world, local, device, backend)
     if rank == 0 and world == 1 and not a.dry_run and not a.no_cpu_baseline:
         if a.config == "c2":
             res["cpu_baseline"] = cpu_baseline()

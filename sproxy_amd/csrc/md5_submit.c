@@ -1310,6 +1310,47 @@ static void src_copy(const struct chunk_src *s, uint64_t i, unsigned char *dst)
     }
 }
 
+/* Bytes [a, a + len) of chunk i to dst. */
+static void src_copy_range(const struct chunk_src *s, uint64_t i, uint64_t a, uint64_t len, unsigned char *dst)
+{
+    if (!len) return;
+    if (s->ptrs) {
+        memcpy(dst, (const unsigned char *)s->ptrs[i] + a, len);
+        return;
+    }
+    for (uint64_t j = s->seg_first[i]; j < s->seg_first[i + 1] && len; j++) {
+        const uint64_t sl = s->segs[j].len;
+        if (a >= sl) {
+            a -= sl;
+            continue;
+        }
+        const uint64_t take = sl - a < len ? sl - a : len;
+        memcpy(dst, (const unsigned char *)s->segs[j].base + a, take);
+        dst += take;
+        len -= take;
+        a = 0;
+    }
+}
+
+/* What a digest reads of an L-byte chunk: netcache's CRC-32 with a fastcrc
+ * window F < L reads only the first and the last F bytes (blk_io.c:408-424),
+ * so only those 2F bytes are staged and sent, as ONE 2F-byte chunk whose own
+ * fastcrc digest is the same crc(head) ^ crc(tail) (a 16 KiB block with
+ * F = 128: 256 B over PCIe instead of 16 KiB).  F = 0 (MD5 too): L. */
+static inline uint64_t staged_len(uint32_t F, uint64_t L) { return F && L > F ? 2ull * F : L; }
+
+/* chunk i as staged: whole, or its head and tail windows */
+static void src_copy_staged(const struct chunk_src *s, uint64_t i, uint32_t F, unsigned char *dst)
+{
+    const uint64_t L = F ? src_len(s, i) : 0;
+    if (!F || L <= F) {
+        src_copy(s, i, dst);
+        return;
+    }
+    src_copy_range(s, i, 0, F, dst);
+    src_copy_range(s, i, L - F, F, dst + F);
+}
+
 /* Host gather of chunks [first, first + m) to dst + off[j].  One thread's
  * memcpy from pageable memory into pinned staging runs ~15 GB/s (DESIGN.md
  * §5), well below PCIe, so a large range is cut by bytes into parts copied
@@ -1320,12 +1361,13 @@ struct gather_part {
     uint64_t first, jlo, jhi;
     const uint64_t *off;
     unsigned char *dst;
+    uint32_t win;                         /* fastcrc window of a CRC-32 slot (staged_len), else 0 */
 };
 
 static void *gather_run(void *arg)
 {
     const struct gather_part *p = arg;
-    for (uint64_t j = p->jlo; j < p->jhi; j++) src_copy(p->src, p->first + j, p->dst + p->off[j]);
+    for (uint64_t j = p->jlo; j < p->jhi; j++) src_copy_staged(p->src, p->first + j, p->win, p->dst + p->off[j]);
     return NULL;
 }
 
@@ -1345,7 +1387,7 @@ static void gather_threads_init(void)
 #define GATHER_PART_MIN (2ull << 20)    /* and at least this many bytes per part */
 
 static void gather_range(const struct chunk_src *src, uint64_t first, uint64_t m,
-                         const uint64_t *off, unsigned char *dst, uint64_t lo, uint64_t used)
+                         const uint64_t *off, unsigned char *dst, uint64_t lo, uint64_t used, uint32_t win)
 {
     pthread_once(&g_gather_once, gather_threads_init);
     const uint64_t bytes = used - lo;
@@ -1359,7 +1401,7 @@ static void gather_range(const struct chunk_src *src, uint64_t first, uint64_t m
     uint64_t j = 0;
     for (uint64_t t = 0; t < T; t++) {      /* part t: chunks whose offset < lo + (t+1) * bytes / T */
         const uint64_t lim = t + 1 == T ? UINT64_MAX : lo + (t + 1) * bytes / T;
-        part[t] = (struct gather_part){src, first, j, j, off, dst};
+        part[t] = (struct gather_part){src, first, j, j, off, dst, win};
         while (j < m && off[j] < lim) j++;
         part[t].jhi = j;
     }
@@ -1425,13 +1467,45 @@ static void reserve_device(md5hip_batcher *b, struct slot *sl, const struct chun
     sl->n += m;
 }
 
+/* One piece of a zero-copy chunk -- `len` registered bytes at host address
+ * p (registration r) -- to staging offset `at` of the slot's gather tables. */
+static void zc_piece(struct slot *sl, int dev, const void *p, uint32_t len, long r, uint64_t at)
+{
+    const uint64_t dsrc = (uint64_t)((uintptr_t)p + g_reg[r].delta[dev]);
+    /* device table: contiguous pieces merged up to 64 KiB, so a slice keeps
+     * >= ~1000 workgroups of gather work */
+    struct md5hip_seg *prev = sl->nseg ? &sl->h_seg[sl->nseg - 1] : NULL;
+    if (prev && prev->src + prev->len == dsrc && prev->dst + prev->len == at &&
+        (uint64_t)prev->len + len <= (64u << 10)) {
+        prev->len += len;
+    } else {
+        sl->h_seg[sl->nseg++] = (struct md5hip_seg){dsrc, at, len, 0};
+    }
+    /* DMA list: merged without limit (a copy has a fixed cost), but only
+     * within one registered range (one pinned allocation) */
+    const uint64_t q1 = sl->ndma;
+    if (q1 && sl->b_reg[q1 - 1] == r &&
+        (const unsigned char *)sl->b_src[q1 - 1] + sl->b_len[q1 - 1] == (const unsigned char *)p &&
+        (unsigned char *)sl->b_dst[q1 - 1] + sl->b_len[q1 - 1] == sl->d_data + at) {
+        sl->b_len[q1 - 1] += len;
+    } else {
+        sl->b_dst[q1] = sl->d_data + at;
+        sl->b_src[q1] = (void *)p;
+        sl->b_len[q1] = len;
+        sl->b_reg[q1] = r;
+        sl->ndma++;
+    }
+}
+
 /* Reserve chunks [i, n) of `src` into the open slot (mu held): descriptors,
  * staging offsets, zero-copy tables.  Returns the number reserved (the slot
- * is marked full when a chunk did not fit) or -errno. */
+ * is marked full when a chunk did not fit) or -errno.  A CRC-32 slot with a
+ * fastcrc window stages each longer chunk's two windows only (staged_len). */
 static long reserve(md5hip_batcher *b, struct slot *sl, const struct chunk_src *src, uint64_t i,
                     uint64_t n, int zc)
 {
     const int dev = b->device;
+    const uint32_t F = sl->kind == MD5HIP_DIGEST_CRC32 ? sl->fastcrc : 0;
     uint64_t j = i;
     if (sl->n == 0 && i < n) sl->opened_us = now_us();
     if (src->dptrs) {
@@ -1443,63 +1517,53 @@ static long reserve(md5hip_batcher *b, struct slot *sl, const struct chunk_src *
     if (zc) pthread_rwlock_rdlock(&g_reg_lock);
     while (j < n && sl->n < b->maxn) {
         const uint64_t L = src_len(src, j);
+        const uint64_t E = staged_len(F, L);
         {   /* host bytes (device-resident chunks: reserve_device above) */
             /* chunks packed on 128-B lines: the LDS-DMA loaders read 128-B
              * stages, and a stage off the line shares a line with the next
              * one (the nt policy is then off, md5_kernels.h) */
-            const uint64_t sz = (L + 127) & ~127ull;
+            const uint64_t sz = (E + 127) & ~127ull;
             if (sl->used + sz > b->cap) break;
             if (zc) {
                 const uint64_t ns = src_nseg(src, j);
-                if (sl->nseg + ns > b->segcap || sl->ndma + ns > b->segcap) break;
+                if (sl->nseg + ns + 2 > b->segcap || sl->ndma + ns + 2 > b->segcap) break;
+                /* the chunk's byte ranges staged: all of it, or its windows */
+                const int win = E != L;
+                const uint64_t ra[2] = {0, win ? L - F : 0}, rl[2] = {win ? F : L, win ? F : 0};
                 uint64_t at = sl->used;
-                for (uint64_t q = 0; q < ns; q++) {
-                    const void *p;
-                    uint32_t len;
-                    src_seg(src, j, q, &p, &len);
-                    if (!len) continue;
-                    const long r = reg_find((uintptr_t)p, len);
-                    if (r < 0) {                               /* unregistered under us */
-                        pthread_rwlock_unlock(&g_reg_lock);
-                        return -EFAULT;
+                for (int w = 0; w < 2; w++) {
+                    uint64_t a = ra[w], left = rl[w];
+                    for (uint64_t q = 0; q < ns && left; q++) {
+                        const void *p;
+                        uint32_t len;
+                        src_seg(src, j, q, &p, &len);
+                        if (a >= len) {
+                            a -= len;
+                            continue;
+                        }
+                        const uint32_t take = (uint32_t)(len - a < left ? len - a : left);
+                        const void *pp = (const unsigned char *)p + a;
+                        a = 0;
+                        left -= take;
+                        const long r = reg_find((uintptr_t)pp, take);
+                        if (r < 0) {                           /* unregistered under us */
+                            pthread_rwlock_unlock(&g_reg_lock);
+                            return -EFAULT;
+                        }
+                        zc_piece(sl, dev, pp, take, r, at);
+                        at += take;
                     }
-                    const uint64_t dsrc = (uint64_t)((uintptr_t)p + g_reg[r].delta[dev]);
-                    /* device table: contiguous pieces merged up to 64 KiB, so
-                     * a slice keeps >= ~1000 workgroups of gather work */
-                    struct md5hip_seg *prev = sl->nseg ? &sl->h_seg[sl->nseg - 1] : NULL;
-                    if (prev && prev->src + prev->len == dsrc && prev->dst + prev->len == at &&
-                        (uint64_t)prev->len + len <= (64u << 10)) {
-                        prev->len += len;
-                    } else {
-                        sl->h_seg[sl->nseg++] = (struct md5hip_seg){dsrc, at, len, 0};
-                    }
-                    /* DMA list: merged without limit (a copy has a fixed cost),
-                     * but only within one registered range (one pinned allocation) */
-                    const uint64_t q1 = sl->ndma;
-                    if (q1 && sl->b_reg[q1 - 1] == r &&
-                        (const unsigned char *)sl->b_src[q1 - 1] + sl->b_len[q1 - 1] ==
-                            (const unsigned char *)p &&
-                        (unsigned char *)sl->b_dst[q1 - 1] + sl->b_len[q1 - 1] == sl->d_data + at) {
-                        sl->b_len[q1 - 1] += len;
-                    } else {
-                        sl->b_dst[q1] = sl->d_data + at;
-                        sl->b_src[q1] = (void *)p;
-                        sl->b_len[q1] = len;
-                        sl->b_reg[q1] = r;
-                        sl->ndma++;
-                    }
-                    at += len;
                 }
             }
             sl->h_off[sl->n] = sl->used;
             sl->used += sz;
         }
-        sl->h_len[sl->n] = (uint32_t)L;
-        sl->load += L + 64;
-        sl->payload += L;
-        __atomic_store_n(&b->load_bytes, b->load_bytes + L + 64, __ATOMIC_RELAXED);
+        sl->h_len[sl->n] = (uint32_t)E;
+        sl->load += E + 64;
+        sl->payload += E;
+        __atomic_store_n(&b->load_bytes, b->load_bytes + E + 64, __ATOMIC_RELAXED);
         {
-            const uint64_t k = (L >> 6) + 1;
+            const uint64_t k = (E >> 6) + 1;
             if (k > sl->last_key) sl->unsorted = 1;
             sl->last_key = k > UINT32_MAX ? UINT32_MAX : (uint32_t)k;
             if (k > MD5HIP_HIST_KMAX) {
@@ -1621,7 +1685,8 @@ static int submit(md5hip_batcher *b, const struct chunk_src *src, uint64_t n, un
             /* copy outside the lock: other submitters may reserve behind us */
             sl->writers++;
             pthread_mutex_unlock(&b->mu);
-            gather_range(src, i, m, sl->h_off + at, sl->h_data, lo, hi);
+            gather_range(src, i, m, sl->h_off + at, sl->h_data, lo, hi,
+                         sl->kind == MD5HIP_DIGEST_CRC32 ? sl->fastcrc : 0);
             pthread_mutex_lock(&b->mu);
             sl->writers--;
         }

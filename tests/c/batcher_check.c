@@ -7,7 +7,8 @@
  * and page lists, verify with a flipped digest, host_fixed, device-resident
  * fixed-length runs (md5_batch_submit_device_fixed), device-resident
  * submits with host or device digests (also ordered after a producer
- * stream), pool submits whole and split, CRC-32 on its own batcher, netcache
+ * stream), pool submits whole and split, CRC-32 on its own batcher, fastcrc
+ * on page lists split across its windows (only the windows staged), netcache
  * header verification, flush -- from pageable or registered memory, and
  * checks every digest against the library's host MD5 computed up front; one
  * more thread keeps changing the batchers' knobs (inflight target, linger,
@@ -55,7 +56,7 @@ static uint32_t g_lens[NCH];
 static uint64_t g_offs[NCH];
 static unsigned char g_md5[NCH][16];
 static uint32_t g_crc[NCH];
-static md5hip_batcher *g_b, *g_q, *g_crcb;
+static md5hip_batcher *g_b, *g_q, *g_crcb, *g_fcrc;
 static md5hip_pool *g_pool;
 extern uint32_t fake_hip_fail_len;
 extern unsigned long fake_hip_wrong_device;
@@ -127,7 +128,7 @@ static void *worker(void *arg)
             lens[i] = g_lens[idx[i]];
             dptrs[i] = (uint64_t)(uintptr_t)(g_heap + g_offs[idx[i]]);
         }
-        const int op = (int)(rnd(&s) % 13);
+        const int op = (int)(rnd(&s) % 14);
         int rc = 0;
         memset(dig, 0, sizeof dig);
         switch (op) {
@@ -248,6 +249,30 @@ static void *worker(void *arg)
             uint32_t fc;
             if ((rc = md5hip_batcher_get_digest(g_crcb, &kind, &fc)) || kind != MD5HIP_DIGEST_CRC32 || fc)
                 fail("get_digest", t, rc);
+            break;
+        }
+        case 12: {
+            /* fastcrc 100 (blk_io.c:408-424) on page lists split at random
+             * points: the batcher stages (or maps) only each chunk's head and
+             * tail windows, which may straddle segments */
+            enum { FW = 100 };
+            uint64_t ns = 0;
+            for (int i = 0; i < n; i++) {
+                first[i] = ns;
+                const uint32_t a = lens[i] ? (uint32_t)(rnd(&s) % (lens[i] + 1)) : 0;
+                segs[ns++] = (struct md5hip_iov){ptrs[i], a};
+                segs[ns++] = (struct md5hip_iov){(const unsigned char *)ptrs[i] + a, lens[i] - a};
+            }
+            first[n] = ns;
+            uint32_t crc[MAXV];
+            rc = md5_batch_submit_iov(g_fcrc, segs, first, (uint64_t)n, (unsigned char *)crc);
+            for (int i = 0; i < n && !rc; i++) {
+                const unsigned char *p = ptrs[i];
+                const uint32_t L = lens[i];
+                const uint32_t want = L <= FW ? nc_crc32(p, L) : nc_crc32(p, FW) ^ nc_crc32(p + L - FW, FW);
+                if (crc[i] != want) rc = -3500 - i;
+            }
+            if (rc) fail("fastcrc windows", t, rc);
             break;
         }
         case 11: {
@@ -814,11 +839,13 @@ int main(int argc, char **argv)
     if (rc) { printf("FAIL register %d\n", rc); return 1; }
     if ((rc = md5hip_batcher_create(0, 1u << 20, 3, &g_b)) ||
         (rc = md5hip_queue_create(0, 4096, 4, &g_q)) ||
-        (rc = md5hip_batcher_create(0, 1u << 20, 2, &g_crcb))) {
+        (rc = md5hip_batcher_create(0, 1u << 20, 2, &g_crcb)) ||
+        (rc = md5hip_batcher_create(0, 1u << 20, 2, &g_fcrc))) {
         printf("FAIL create %d\n", rc);
         return 1;
     }
     md5hip_batcher_set_digest(g_crcb, MD5HIP_DIGEST_CRC32, 0);
+    md5hip_batcher_set_digest(g_fcrc, MD5HIP_DIGEST_CRC32, 100);
     static double wd_secs;
     wd_secs = secs + 60.0;
     pthread_t wd;
@@ -883,6 +910,7 @@ int main(int argc, char **argv)
     md5hip_batcher_destroy(g_b);
     md5hip_batcher_destroy(g_q);
     md5hip_batcher_destroy(g_crcb);
+    md5hip_batcher_destroy(g_fcrc);
     md5hip_host_unregister(g_heap);
     free(g_heap);
     free(g_pageable);

@@ -267,3 +267,39 @@ def test_gpu_crc_queue_long_blocks_split(cuda):
         got = np.asarray(got).view(np.uint32).reshape(-1)
         assert np.array_equal(got, want), len(lens)
     q.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("registered", [False, True])
+def test_gpu_fastcrc_host_blocks_stage_only_windows(cuda, registered):
+    """A CRC-32 batcher with a fastcrc window F stages (or maps, zero-copy)
+    only the first and last F bytes of each longer host block (md5_submit.c
+    staged_len): lengths around F and 2F, empty blocks, and page lists cut
+    inside either window.  Every CRC equals crc32.c's blk_make_crc rule
+    (blk_io.c:408-424), and the bytes staged are the windows' (stats)."""
+    F = 128
+    rng = np.random.default_rng(128 + registered)
+    lens = [0, 1, F - 1, F, F + 1, 2 * F - 1, 2 * F, 2 * F + 1, 16384, 65536] + \
+        [int(x) for x in rng.integers(0, 70000, 200)]
+    offs, total = gen.pack_offsets(lens, align=16)
+    buf = gen.xorshift_array(total + 4096, seed=777)
+    want = gen.oracle_crc32_batch(buf, offs, lens, F)
+    if registered:
+        m.register_host(buf)
+    try:
+        chunks = []
+        for o, L in zip(offs, lens):
+            cut = int(rng.integers(0, L + 1)) if L else 0
+            cut2 = int(rng.integers(cut, L + 1)) if L else 0
+            mv = memoryview(buf)[o:o + L]
+            chunks.append([mv[:cut], mv[cut:cut2], mv[cut2:]])
+        with m.Batcher(device=0, kind=m.Batcher.CRC32, fastcrc=F) as b:
+            got = b.submit_iov(chunks)
+            st = b.stats()
+        assert np.array_equal(np.asarray(got).view(np.uint32).reshape(-1), want)
+        staged = sum(((2 * F if L > F else L) + 127) & ~127 for L in lens)
+        if not registered:
+            assert st["bytes_staged"] == staged, (st["bytes_staged"], staged)
+    finally:
+        if registered:
+            m.unregister_host(buf)

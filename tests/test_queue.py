@@ -415,3 +415,76 @@ def test_queue_pipelined_stream_every_chain_mode(cuda, chain):
         assert torch.equal(outs[0][j], ref[j]), (chain, 4, j)
     st = q.stats()
     assert st["submissions"] == 5 * K and st["launches"] < st["submissions"], st
+
+
+def test_queue_device_fixed_md5_and_fastcrc(cuda):
+    """md5_batch_submit_device_fixed (ABI 4): fixed-length device-resident
+    runs read in place, no per-chunk descriptor.  MD5 with host digests,
+    in-place device digests and unaligned (scattered) device digests, a run
+    longer than one slot (several launches), a stride wider than the
+    length, ordering after a producer stream; CRC-32 whole and fastcrc
+    windows (blk_io.c:408-424).  Every digest against the oracle."""
+    n, L, S = 3000, 5000, 5120
+    host = gen.xorshift_array(n * S + 64, seed=4242)
+    offs = [i * S for i in range(n)]
+    want = gen.oracle_digests(host, offs, [L] * n)
+    dev = torch.from_numpy(host.copy()).to(cuda)
+    with m.Queue(device=0, max_chunks=1024) as q:                      # 3 slots' worth
+        got = q.submit_device_fixed_async(dev, n, L, S, after=None).wait()
+        assert np.array_equal(got, want)
+        out = torch.empty((n, 16), dtype=torch.uint8, device=cuda)
+        q.submit_device_fixed_async(dev, n, L, S, out=out).wait()      # ordered after torch's stream
+        assert np.array_equal(out.cpu().numpy(), want)
+        raw = torch.zeros(n * 16 + 4, dtype=torch.uint8, device=cuda)
+        odd = raw[4:].view(n, 16)
+        q.submit_device_fixed_async(dev, n, L, S, out=odd).wait()
+        assert np.array_equal(odd.cpu().numpy(), want)
+        # the producer's write lands before the kernel reads it
+        s = torch.cuda.Stream()
+        with torch.cuda.stream(s):
+            dev2 = torch.empty_like(dev)
+            dev2.copy_(dev)
+            pend = q.submit_device_fixed_async(dev2, n, L, S, after=s)
+        assert np.array_equal(pend.wait(), want)
+        for F in (0, 128, 4096):
+            q.set_digest(m.Batcher.CRC32, F)
+            crc = q.submit_device_fixed_async(dev, n, L, S, after=None).wait()
+            assert np.array_equal(crc, gen.oracle_crc32_batch(host, offs, [L] * n, fastcrc=F)), F
+        st = q.stats()
+    assert st["launches"] >= 3 * 7
+
+
+def test_batcher_failure_policy_with_an_injected_fault(cuda):
+    """INTEGRATION.md §2j on the GPU: the launch that faults gives its
+    ticket -EIO and writes no digest; the batcher is failed from then on
+    (-ENODEV at once, nothing launched); a pool over device 0 listed three
+    times moves a synchronous submission off its failed member and never
+    uses it again."""
+    import errno
+    rng = np.random.default_rng(99)
+    lens = [int(x) for x in rng.integers(1, 40000, 64)]
+    dev, ptrs, L, want = _arena_batch(lens, 991, cuda)
+    host = [bytes(dev[int(p - dev.data_ptr()):int(p - dev.data_ptr()) + int(n)].cpu().numpy())
+            for p, n in zip(ptrs, L)]
+    with m.Queue(device=0) as q:
+        assert np.array_equal(q.submit_device(ptrs, L), want) and q.health() == 0
+        q.inject_fault(1)
+        out = np.full((len(lens), 16), 0x5A, dtype=np.uint8)
+        with pytest.raises(m.MD5HipError) as e:
+            q.submit_device(ptrs, L, out=out)
+        assert e.value.rc == -errno.EIO and (out == 0x5A).all()
+        assert q.health() == -errno.ENODEV
+        launches = q.stats()["launches"]
+        with pytest.raises(m.MD5HipError) as e:
+            q.submit(host)
+        assert e.value.rc == -errno.ENODEV and q.stats()["launches"] == launches
+    with m.Pool(devices=(0, 0, 0)) as p:
+        p.set_split(64 << 10)                                          # every member takes a part
+        p.inject_fault(1, 1)
+        assert np.array_equal(p.submit(host), want)
+        h = p.health()
+        assert h["nfailed"] == 1 and h["failed_mask"] == 2 and h["failovers"] == 1, h
+        before = p.device_stats(1)["submissions"]
+        for _ in range(3):
+            assert np.array_equal(p.submit(host), want)
+        assert p.device_stats(1)["submissions"] == before
