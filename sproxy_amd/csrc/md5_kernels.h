@@ -555,9 +555,6 @@ __device__ __forceinline__ void desc_xpose_group(H& h, const uint8_t* __restrict
       // for BALANCED) measured 1.0-1.4 % slower on 3 and 6 coalesced C3
       // batches (profiles/r04h/balanced3_ab.json).
       static_assert(D == 1 && !kHalf, "LDS-DMA images: full 8 KiB stages");
-      // s_waitcnt immediates (gfx9: vmcnt 3:0 + 15:14, expcnt 6:4, lgkmcnt
-      // 11:8), vmcnt and expcnt left at their maxima
-      constexpr unsigned kLgkm4 = 0xC47Fu, kLgkm0 = 0xC07Fu;
       const bool lined = __ballot(((uint32_t)(uintptr_t)chunk & 127u) != 0 && live && nst != 0) == 0;
       const uint32_t rmin = wave_min(nst ? nst : smax) - 1u;
       auto* limg = (__attribute__((address_space(3))) uint8_t*)img;
@@ -617,13 +614,10 @@ __device__ __forceinline__ void desc_xpose_group(H& h, const uint8_t* __restrict
             if constexpr (b == 0) issue(stg + 1, I1{});
             else issue(stg + 1, I0{});
           }
-          // block 0's rows: the builtin, not asm, so the compiler's own
-          // waitcnt pass knows only rows 4-7 are still out (with an asm wait
-          // it adds lgkmcnt(0) before block 0's first use, serializing all 8)
-          __builtin_amdgcn_s_waitcnt(kLgkm4);
+          asm volatile("s_waitcnt lgkmcnt(4)" ::: "memory");   // block 0's rows
           __builtin_amdgcn_sched_barrier(0);
           if (stg < nst) h.block(st, w[0]);
-          __builtin_amdgcn_s_waitcnt(kLgkm0);
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
           __builtin_amdgcn_sched_barrier(0);
           if (stg < nst) h.block(st, w[1]);
         };
@@ -662,10 +656,10 @@ __device__ __forceinline__ void desc_xpose_group(H& h, const uint8_t* __restrict
                  std::integral_constant<int, 4>{}, std::integral_constant<int, 5>{},
                  std::integral_constant<int, 6>{}, std::integral_constant<int, 7>{});
           }
-          __builtin_amdgcn_s_waitcnt(kLgkm4);                  // as in stage(): a wait the compiler sees
+          asm volatile("s_waitcnt lgkmcnt(4)" ::: "memory");
           __builtin_amdgcn_sched_barrier(0);
           h.block(st, w[0]);
-          __builtin_amdgcn_s_waitcnt(kLgkm0);
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
           __builtin_amdgcn_sched_barrier(0);
           h.block(st, w[1]);
         };
