@@ -34,8 +34,10 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 EXE = os.path.join(REPO, "build", "c", "asio_scale")
 
 
-def run(target, threads, blocks, L, secs, mode="pageable", timeout=150, env=None, tag=None):
+def run(target, threads, blocks, L, secs, mode="pageable", timeout=150, env=None, tag=None, slice_mib=0):
     cmd = [EXE, target, str(threads), str(blocks), str(L), str(secs), mode]
+    if slice_mib:
+        cmd += [str(slice_mib), "4"]
     t0 = time.time()
     out = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout,
                          env=dict(os.environ, **(env or {})))
@@ -55,6 +57,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--matrix", choices=["threads", "chunk", "bigchunk", "watch"], required=True)
     ap.add_argument("--rounds", type=int, default=2)
+    ap.add_argument("--policies", default="spin,tail,block", help="--matrix watch: MD5HIP_WATCH values")
+    ap.add_argument("--slice-mib", type=int, default=0, help="batcher slice (0 = the library default)")
     ap.add_argument("--secs", type=float, default=3.0)
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
@@ -68,15 +72,21 @@ def main():
         for r in range(a.rounds):
             for target in ("batcher", "pool"):
                 for T in (8, 64, 256):
-                    for pol in ("spin", "tail", "block"):
+                    for pol in a.policies.split(","):
                         runs.append(run(target, T, 64, 16384, a.secs, "registered",
                                         env={"MD5HIP_WATCH": pol}, tag={"watch": pol, "round": r}))
     elif a.matrix == "bigchunk":
-        for L in (2 << 20, 4 << 20, 10 << 20):
-            for B in (1, 4, 8):
-                for T in (1, 8, 64):
-                    for target in ("batcher", "host"):
-                        runs.append(run(target, T, B, L, a.secs, timeout=300))
+        if a.slice_mib:      # the queue alone, with slices sized for many long chains in flight
+            for L in (2 << 20, 10 << 20):
+                for B in (4, 8):
+                    runs.append(run("batcher", 64, B, L, a.secs, timeout=300, slice_mib=a.slice_mib,
+                                    tag={"slice_mib": a.slice_mib}))
+        else:
+            for L in (2 << 20, 4 << 20, 10 << 20):
+                for B in (1, 4, 8):
+                    for T in (1, 8, 64):
+                        for target in ("batcher", "host"):
+                            runs.append(run(target, T, B, L, a.secs, timeout=300))
     else:
         for L in (16384, 131072, 1 << 20):
             for B in (8, 64):

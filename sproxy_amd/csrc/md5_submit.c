@@ -872,7 +872,7 @@ static void *progress_main(void *arg)
  * broadcast or signalled, so no wake-up is lost.
  * ------------------------------------------------------------------------ */
 enum { WATCH_SPIN_US = 300, WATCH_LEAD_US = 200 };   /* WATCH_POLICY_SPIN */
-enum { WATCH_TAIL_US = 50 };                           /* WATCH_POLICY_TAIL */
+enum { WATCH_TAIL_US = 50, WATCH_TAIL_SPIN_US = 150 };  /* WATCH_POLICY_TAIL */
 
 static void cpu_relax(void)
 {
@@ -895,14 +895,18 @@ static void watch_sleep(md5hip_batcher *b, struct slot *sl, uint64_t us)
 }
 
 /* Watch in-flight slot `sl` (mu held on entry and exit, watch == NONE).
- * The policy (b->watch_policy, MD5HIP_WATCH at create):
+ * The policy (b->watch_policy, MD5HIP_WATCH at create; profiles/r05e/):
+ *   TAIL   (default) sleep on the slot until 50 us before the launch is due
+ *          (recent launches' wall time), then poll its event for at most
+ *          150 us; past that the watcher gives up and sleeps too, and the
+ *          progress thread (polling every 10 us meanwhile) retires it.  At
+ *          8 callers a call costs its thread 33-39 us of CPU instead of
+ *          SPIN's 122 (the whole ~150 us launch polled), same latency;
  *   SPIN   round 4: a launch due within 300 us is polled for up to 500 us
- *          (a longer one slept through until 200 us before its end); past
- *          that the watcher gives up and the progress thread retires it;
- *   TAIL   sleep until 50 us before the launch is due, poll for at most
- *          50 us, then block in hipEventSynchronize on the blocking-sync
- *          event (the thread sleeps until the completion interrupt);
- *   BLOCK  hipEventSynchronize at once. */
+ *          (a longer one slept through until 200 us before its end);
+ *   BLOCK  hipEventSynchronize on a blocking-sync event: measured, not
+ *          kept -- the wake-up after the interrupt costs ~1 ms per call
+ *          and ~190 us of CPU (r05e/asio_watch.json). */
 static void watch_launch(md5hip_batcher *b, struct slot *sl)
 {
     const uint64_t gen = sl->gen;
@@ -921,10 +925,10 @@ static void watch_launch(md5hip_batcher *b, struct slot *sl)
     pthread_mutex_unlock(&b->mu);
     hipError_t e = hipErrorNotReady;
     if (pol != WATCH_POLICY_BLOCK) {
-        const uint64_t t0 = now_us(), limit = pol == WATCH_POLICY_SPIN ? WATCH_SPIN_US + WATCH_LEAD_US : WATCH_TAIL_US;
+        const uint64_t t0 = now_us(), limit = pol == WATCH_POLICY_SPIN ? WATCH_SPIN_US + WATCH_LEAD_US
+                                                                       : WATCH_TAIL_SPIN_US;
         while ((e = launch_status(ev, inject)) == hipErrorNotReady && now_us() - t0 < limit) cpu_relax();
-    }
-    if (e == hipErrorNotReady && pol != WATCH_POLICY_SPIN) {
+    } else {
         e = hipEventSynchronize(ev);
         if (e == hipSuccess && inject) e = hipErrorLaunchFailure;
     }
@@ -1071,10 +1075,9 @@ static int batcher_new(int device, uint64_t slice_bytes, uint32_t nslots, uint64
                         : !strcmp(w, "spin") ? WATCH_POLICY_SPIN
                         : !strcmp(w, "block") ? WATCH_POLICY_BLOCK : WATCH_POLICY_TAIL;
     }
-    /* blocking-sync completion events: a watcher that blocks on one sleeps
-     * until the interrupt instead of polling the signal */
+    /* BLOCK's watcher sleeps in hipEventSynchronize: blocking-sync events */
     const unsigned done_flags = hipEventDisableTiming |
-                                (b->watch_policy == WATCH_POLICY_SPIN ? 0u : hipEventBlockingSync);
+                                (b->watch_policy == WATCH_POLICY_BLOCK ? hipEventBlockingSync : 0u);
     b->s = calloc(nslots, sizeof *b->s);
     /* ticket 0 = "nothing": complete at once */
     if (!b->s || tk_ring_init(&b->tk, 1)) { rc = -ENOMEM; goto fail; }
