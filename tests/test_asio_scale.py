@@ -67,15 +67,20 @@ def test_asio_scale_cpu_per_call_bounded(cuda, target):
 
 @pytest.mark.gpu
 def test_host_fixed_copy_is_not_under_the_batcher_lock(cuda):
-    """md5hip_batch_host_fixed from a 64 MiB PAGEABLE
-    array (its H2D copy is synchronous, milliseconds) on one thread while 7
-    threads make synchronous 64 x 16 KiB submits on the same batcher.  The
-    copy runs with the slot held as a writer and b->mu released
-    (md5_submit.c host_fixed), so no submitter's call waits for it: their
-    p99 latency stays below the fastest host_fixed call, and every digest of
-    both equals the oracle's."""
-    rc, rec = _run("batcher", 7, 64, 16384, 3.0, "pageable", ASIO_FIXED_BG_MIB="64")
+    """md5hip_batch_host_fixed from a 256 MiB PAGEABLE
+    array (two 128 MiB slices; from pageable memory each slice's H2D copy is
+    synchronous, milliseconds) on one thread, over and over, while 7 threads
+    make synchronous 64 x 16 KiB submits on the same batcher.  The copy runs
+    with the slot held as a writer and b->mu released (md5_submit.c
+    fixed_submit).  Were it under the lock, a submitter arriving during a
+    copy would wait for the rest of it, and with the copy running most of
+    the time the median call would carry a good part of one: here the
+    submitters' median stays under a quarter and their p90 under half of
+    the fastest host_fixed call, and every digest of both equals the
+    oracle's."""
+    rc, rec = _run("batcher", 7, 64, 16384, 3.0, "pageable", ASIO_FIXED_BG_MIB="256")
     assert rc == 0 and rec["mismatches"] == 0 and rec["rc"] == 0, rec
     bg = rec["bg_fixed"]
     assert bg["calls"] >= 3 and bg["mismatches"] == 0 and bg["rc"] == 0, bg
-    assert rec["lat_us"]["p99"] < bg["lat_us"]["min"], (rec["lat_us"], bg["lat_us"])
+    assert rec["lat_us"]["p50"] < bg["lat_us"]["min"] / 4, (rec["lat_us"], bg["lat_us"])
+    assert rec["lat_us"]["p90"] < bg["lat_us"]["min"] / 2, (rec["lat_us"], bg["lat_us"])
