@@ -17,5 +17,7 @@ timeout -k 10 300 python3 bench.py --config c3q --steps 5 --warmup 2 > $O/c3q.js
 python3 -c "import json;d=json.loads(open('$O/c3q.json').read().strip().splitlines()[-1]);print('c3q', d['value'], d['roofline']['frac'], 'drained', d['drained']['value'], d.get('parity',{}).get('ok'))"
 timeout -k 10 300 python3 bench.py --gpus 1 --steps 20 --warmup 5 > $O/c2_driver.json 2> $O/c2_driver.err || { echo "c2 driver failed"; exit 1; }
 python3 -c "import json;d=json.loads(open('$O/c2_driver.json').read().strip().splitlines()[-1]);print('c2 driver', d['value'], d['ms_per_step'], d['roofline']['frac'], d['cpu_baseline']['value'])"
+timeout -k 10 300 python3 bench.py --config c5 --steps 5 --warmup 2 > $O/c5.json 2> $O/c5.err || { echo "c5 failed"; tail -3 $O/c5.err; exit 1; }
+python3 -c "import json;d=json.loads(open('$O/c5.json').read().strip().splitlines()[-1]);print('c5', d['value'], d.get('parity',{}).get('ok'))"
 timeout -k 10 300 python3 -u scripts/asio_scale.py --matrix bigchunk --slice-mib 1024 --secs 2 --out $O/asio_bigchunk_1g.json > $O/asio_bigchunk_1g.log 2>&1 || { echo "bigchunk 1g failed"; tail -3 $O/asio_bigchunk_1g.log; exit 1; }
 echo done

@@ -1894,6 +1894,59 @@ int md5_batch_submit_device(md5hip_batcher *b, const uint64_t *d_ptrs, const uin
     return submit(b, &src, n, digests, digests_on_device != 0, 0, NULL, -1, 0, NULL);
 }
 
+/* Is [p, p + len) page-locked host memory the DMA engine can read in place
+ * (hipHostMalloc'd, hipHostRegister'ed, or registered here)? */
+static int host_pinned(const void *p, uint64_t len)
+{
+    pthread_rwlock_rdlock(&g_reg_lock);
+    const int reg = reg_find((uintptr_t)p, len) >= 0;
+    pthread_rwlock_unlock(&g_reg_lock);
+    if (reg) return 1;
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();                  /* pageable: not an error of ours */
+        return 0;
+    }
+    return a.type == hipMemoryTypeHost;
+}
+
+/* memcpy of `bytes` on MD5HIP_GATHER_THREADS threads (gather_range's rule:
+ * parts of >= 2 MiB once the copy passes 8 MiB; this thread copies the
+ * first part) */
+struct copy_part {
+    unsigned char *dst;
+    const unsigned char *src;
+    uint64_t len;
+};
+
+static void *copy_run(void *arg)
+{
+    const struct copy_part *c = arg;
+    memcpy(c->dst, c->src, c->len);
+    return NULL;
+}
+
+static void copy_parallel(void *dst, const void *src, uint64_t bytes)
+{
+    pthread_once(&g_gather_once, gather_threads_init);
+    uint64_t T = (uint64_t)g_gather_threads;
+    if (bytes < GATHER_SPLIT_MIN) T = 1;
+    if (T > bytes / GATHER_PART_MIN) T = bytes / GATHER_PART_MIN ? bytes / GATHER_PART_MIN : 1;
+    struct copy_part part[32];
+    pthread_t tid[32];
+    int started[32] = {0};
+    for (uint64_t t = 0; t < T; t++) {
+        const uint64_t a = bytes * t / T, z = bytes * (t + 1) / T;
+        part[t] = (struct copy_part){(unsigned char *)dst + a, (const unsigned char *)src + a, z - a};
+    }
+    for (uint64_t t = 1; t < T; t++) started[t] = pthread_create(&tid[t], NULL, copy_run, &part[t]) == 0;
+    copy_run(&part[0]);
+    for (uint64_t t = 1; t < T; t++) {
+        if (started[t]) pthread_join(tid[t], NULL);
+        else copy_run(&part[t]);
+    }
+}
+
 /* Fixed-length chunks from one contiguous range (MODE_FIXED), one slot per
  * slice of it: host memory (dev_src 0: one H2D copy per slot, no host
  * gather) or device memory (dev_src 1: read in place, no per-chunk
@@ -1910,6 +1963,11 @@ static int fixed_submit(md5hip_batcher *b, int kind, uint32_t fastcrc, const voi
     const unsigned char *src = (const unsigned char *)base;
     uint64_t per = dev_src ? b->maxn : b->cap / stride;
     if (per > b->maxn) per = b->maxn;
+    /* a pageable source is copied into the slot's pinned staging by this
+     * thread: HIP's own pageable H2D path stalls other threads' HIP calls on
+     * the device while it runs (submitters' p90 +2.7 ms beside 128 MiB
+     * slices, profiles/r05f/) */
+    const int pinned = !dev_src && n && host_pinned(base, (n - 1) * stride + len);
     pthread_mutex_lock(&b->mu);
     if (kind < 0) {
         kind = b->kind;
@@ -1959,16 +2017,20 @@ static int fixed_submit(md5hip_batcher *b, int kind, uint32_t fastcrc, const voi
                       hipStreamWaitEvent(sl->stream, b->after_ev, 0) != hipSuccess))
             sl->err = -EIO;
         if (!dev_src) {
-            /* the H2D copy outside the lock, the slot held by this writer:
-             * from pageable memory it is synchronous (a 128 MiB slice is tens
-             * of ms over PCIe), and every other submitter and waiter needs
-             * b->mu meanwhile.  Nothing else touches a FIXED slot's stream
-             * until its writers are done (slot_try_launch waits for
-             * writers == 0). */
+            /* the copy outside the lock, the slot held by this writer: a
+             * pageable source through the pinned staging (host_pinned), a
+             * pinned one by DMA in place; every other submitter and waiter
+             * needs b->mu meanwhile.  Nothing else touches a FIXED slot's
+             * stream or staging until its writers are done (slot_try_launch
+             * waits for writers == 0). */
             sl->writers++;
             pthread_mutex_unlock(&b->mu);
-            const hipError_t ce = hipMemcpyAsync(sl->d_data, sl->fx_src, sl->fx_bytes, hipMemcpyHostToDevice,
-                                                 sl->stream);
+            const void *from = sl->fx_src;
+            if (!pinned) {
+                copy_parallel(sl->h_data, sl->fx_src, sl->fx_bytes);
+                from = sl->h_data;
+            }
+            const hipError_t ce = hipMemcpyAsync(sl->d_data, from, sl->fx_bytes, hipMemcpyHostToDevice, sl->stream);
             pthread_mutex_lock(&b->mu);
             sl->writers--;
             if (ce != hipSuccess && !sl->err) sl->err = -EIO;

@@ -141,6 +141,9 @@ hipError_t hipHostFree(void *ptr) { free(ptr); return hipSuccess; }
 hipError_t hipHostRegister(void *hostPtr, size_t sizeBytes, unsigned int flags) { (void)hostPtr; (void)sizeBytes; (void)flags; return hipSuccess; }
 hipError_t hipHostUnregister(void *hostPtr) { (void)hostPtr; return hipSuccess; }
 hipError_t hipHostGetDevicePointer(void **devPtr, void *hstPtr, unsigned int flags) { (void)flags; *devPtr = hstPtr; return hipSuccess; }
+/* every host pointer looks pageable (host_fixed then stages through pinned) */
+hipError_t hipPointerGetAttributes(hipPointerAttribute_t *attributes, const void *ptr) { (void)attributes; (void)ptr; return hipErrorInvalidValue; }
+hipError_t hipGetLastError(void) { return hipSuccess; }
 
 hipError_t hipStreamCreateWithFlags(hipStream_t *stream, unsigned int flags)
 {
