@@ -564,7 +564,10 @@ def run_crcq(a, rank, world, local, device, backend):
     m.fill_synthetic(data, seed=0xC4C0 + rank)
     torch.cuda.synchronize()
     outs = [[torch.empty(n, dtype=torch.int32, device="cuda") for _ in range(K)] for _ in range(2)]
-    q = m.Queue(device=torch.cuda.current_device(), max_chunks=n, nslots=max(4, K + 1))
+    # two steps' worth of slots: step k's launches are all queued on the
+    # device while step k-1's run (one step's worth left the GPU waiting on
+    # the host for each retire, r05f: 0.35)
+    q = m.Queue(device=torch.cuda.current_device(), max_chunks=n, nslots=min(16, 2 * K + 1))
     q.set_digest(m.Batcher.CRC32, F)
     base = data.data_ptr()
 

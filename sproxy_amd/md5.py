@@ -501,19 +501,26 @@ class Batcher:
         L = np.ascontiguousarray(lens, dtype=np.uint32)
         if P.size != L.size:
             raise ValueError("ptrs and lens differ in length")
-        need = P.size * self.dsz
+        o, on_dev = self._dev_out(P.size, out)
+        return P, L, o, on_dev
+
+    def _dev_out(self, n, out):
+        """(digest destination, on_device) for n digests: a device tensor on
+        the batcher's device, a C-contiguous uint8 numpy array, or None (a
+        new host array)."""
+        need = n * self.dsz
         if torch is not None and isinstance(out, torch.Tensor):
             if not out.is_cuda or not out.is_contiguous() or out.numel() * out.element_size() < need:
                 raise ValueError(f"out must be a contiguous device tensor of >= n x {self.dsz} bytes")
             if out.device.index != self.device:
                 raise ValueError(f"out is on cuda:{out.device.index}, the batcher on cuda:{self.device}")
-            return P, L, out, 1
+            return out, 1
         if out is None:
-            out = self._out(P.size)
-        elif not (isinstance(out, np.ndarray) and out.dtype == np.uint8 and out.flags.c_contiguous
-                  and out.nbytes >= need):
+            return self._out(n), 0
+        if not (isinstance(out, np.ndarray) and out.dtype == np.uint8 and out.flags.c_contiguous
+                and out.nbytes >= need):
             raise ValueError(f"out must be a C-contiguous uint8 array of >= n x {self.dsz} bytes")
-        return P, L, out, 0
+        return out, 0
 
     def _producer(self, after):
         """(stream handle, order) for md5_batch_submit_device_after:
@@ -572,7 +579,7 @@ class Batcher:
             addr = base.data_ptr()
         else:
             addr = int(base)
-        _, _, o, on_dev = self._dev_args(np.zeros(n, np.uint64), np.zeros(n, np.uint32), out)
+        o, on_dev = self._dev_out(n, out)
         t = ctypes.c_uint64()
         dst = o.data_ptr() if on_dev else o.ctypes.data
         check(*self._call("submit_device_fixed", ctypes.c_void_p(addr), n, length, stride, dst, on_dev,
