@@ -93,7 +93,7 @@ def parse_args(argv):
     p.add_argument("--c3q-slots", type=int, default=4, help="--config c3q: queue slots")
     p.add_argument("--c3q-chain", type=int, default=2,
                    help="--config c3q: chained launches (md5hip_batcher_set_chain: 0 off, 1 on, 2 = on + BALANCED tails overlap, the default)")
-    p.add_argument("--crcq-subs", type=int, default=4,
+    p.add_argument("--crcq-subs", type=int, default=8,
                    help="--config crcq: fixed-length device submissions per step through one queue")
     p.add_argument("--crcq-chunks", type=int, default=1 << 20, help="--config crcq: blocks per submission")
     p.add_argument("--c5-chunks", type=int, default=1 << 18)
