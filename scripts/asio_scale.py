@@ -16,6 +16,12 @@ checked against the oracle).
                     range (clamped to 4-10,240 KiB, httpd.c:7968): 2, 4 and
                     10 MiB blocks in vectors of 1, 4 and 8, 1 / 8 / 64
                     callers, batcher vs the calling thread
+  --matrix fastcrc  netcache's CRC-32 with fastcrc = 128 (and whole-block
+                    CRC) at the call site, 64 x 16 KiB vectors from pageable
+                    pages, 1 / 8 / 64 callers: this library (host blocks stage
+                    only their windows) against the round-5 library before
+                    that change (build/abr05/old, via LD_LIBRARY_PATH) and the
+                    calling thread
   --matrix watch    VERDICT r04 item 3: the blocked caller's watcher policy
                     (MD5HIP_WATCH spin / tail / block, md5_submit.c
                     watch_launch) at 8 / 64 / 256 callers of 64 x 16 KiB from
@@ -55,7 +61,7 @@ def run(target, threads, blocks, L, secs, mode="pageable", timeout=150, env=None
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--matrix", choices=["threads", "chunk", "bigchunk", "watch"], required=True)
+    ap.add_argument("--matrix", choices=["threads", "chunk", "bigchunk", "watch", "fastcrc"], required=True)
     ap.add_argument("--rounds", type=int, default=2)
     ap.add_argument("--policies", default="spin,tail,block", help="--matrix watch: MD5HIP_WATCH values")
     ap.add_argument("--slice-mib", type=int, default=0, help="batcher slice (0 = the library default)")
@@ -75,6 +81,17 @@ def main():
                     for pol in a.policies.split(","):
                         runs.append(run(target, T, 64, 16384, a.secs, "registered",
                                         env={"MD5HIP_WATCH": pol}, tag={"watch": pol, "round": r}))
+    elif a.matrix == "fastcrc":
+        old = os.path.join(REPO, "build", "abr05", "old")
+        for F in (128, 0):
+            for T in (1, 8, 64):
+                for lib in ("new", "old"):
+                    env = {"ASIO_CRC": str(F)}
+                    if lib == "old":
+                        env["LD_LIBRARY_PATH"] = old + ":" + os.environ.get("LD_LIBRARY_PATH", "")
+                    runs.append(run("batcher", T, 64, 16384, a.secs, env=env, tag={"lib": lib}))
+                if F:
+                    runs.append(run("host", T, 64, 16384, a.secs, env={"ASIO_CRC": str(F)}, tag={"lib": "host"}))
     elif a.matrix == "bigchunk":
         if a.slice_mib:      # the queue alone, with slices sized for many long chains in flight
             for L in (2 << 20, 10 << 20):

@@ -36,6 +36,11 @@
  * memory); its call times are reported as "bg_fixed" and its digests checked
  * -- the submitters' latency must not include that copy.
  *
+ * ASIO_CRC=F: netcache's own CRC-32 (blk_make_crc, blk_io.c:354-430) with
+ * fastcrc window F (0 = whole block) instead of MD5: the batcher / pool set
+ * to MD5HIP_DIGEST_CRC32, the host leg the library's nc_crc32 over the same
+ * windows, the checker oracle/crc32_oracle.c's blk_make_crc rule.
+ *
  * usage: asio_scale TARGET THREADS BLOCKS BLOCK_BYTES SECS [MODE [SLICE_MIB NSLOTS]]
  * Exit 0 = every digest equal to the oracle's; 1 = a mismatch or error;
  * 77 = no usable HIP device.
@@ -52,8 +57,10 @@
 
 #include "md5.h"
 #include "md5hip.h"
+#include "nc_digest.h"
 
 void oracle_md5(const void *data, uint64_t len, unsigned char digest[16]);
+uint32_t oracle_blk_crc(const void *data, uint64_t remained, uint32_t fastcrc);
 void oracle_xorshift_fill(void *dst, uint64_t nbytes, uint64_t seed);
 
 enum target { T_BATCHER, T_POOL, T_HOST };
@@ -68,6 +75,8 @@ static pthread_barrier_t g_start, g_warm, g_go;
 static double g_t_end;          /* set between g_warm and g_go */
 static int g_nvec = 1;          /* vectors per thread (R) */
 static int g_register;          /* MODE registered */
+static int g_crc = -1;          /* ASIO_CRC: fastcrc window of a CRC-32 run, -1 = MD5 */
+static size_t g_dsz = 16;       /* digest bytes per block */
 
 static double now(void)
 {
@@ -93,7 +102,7 @@ struct job {
     unsigned char *buf;          /* g_nvec vectors of BLOCKS x BLOCK_BYTES */
     const void **ptrs;           /* g_nvec x BLOCKS */
     uint32_t *lens;              /* BLOCKS (the same for every vector of a thread) */
-    unsigned char (*want)[16], (*got)[16];   /* want: g_nvec x BLOCKS */
+    unsigned char *want, *got;   /* g_dsz-byte digests; want: g_nvec x BLOCKS */
     double *lat, *cpu;           /* per timed call */
     size_t ncalls, cap;
     int rc, bad;
@@ -104,15 +113,22 @@ static int one_call(struct job *j)
     const void **ptrs = j->ptrs + (size_t)j->cur * g_blocks;
     switch (g_target) {
     case T_BATCHER:
-        return md5_batch_submit(g_b, ptrs, j->lens, (uint64_t)g_blocks, &j->got[0][0]);
+        return md5_batch_submit(g_b, ptrs, j->lens, (uint64_t)g_blocks, j->got);
     case T_POOL:
-        return md5hip_pool_submit(g_p, ptrs, j->lens, (uint64_t)g_blocks, &j->got[0][0]);
+        return md5hip_pool_submit(g_p, ptrs, j->lens, (uint64_t)g_blocks, j->got);
     case T_HOST:
         for (int i = 0; i < g_blocks; i++) {
+            if (g_crc >= 0) {               /* the library's host CRC-32 over the same windows */
+                const unsigned char *p = ptrs[i];
+                const uint32_t L = j->lens[i], F = (uint32_t)g_crc;
+                const uint32_t c = !F || L <= F ? nc_crc32(p, L) : nc_crc32(p, F) ^ nc_crc32(p + L - F, F);
+                memcpy(j->got + 4 * (size_t)i, &c, 4);
+                continue;
+            }
             struct MD5Context c;
             MD5Init(&c);
             MD5Update(&c, ptrs[i], j->lens[i]);
-            MD5Final(j->got[i], &c);
+            MD5Final(j->got + 16 * (size_t)i, &c);
         }
         return 0;
     }
@@ -122,7 +138,7 @@ static int one_call(struct job *j)
 /* the call's digests against the oracle's for its vector; then the next vector */
 static int check_next(struct job *j)
 {
-    const int bad = memcmp(j->got, j->want + (size_t)j->cur * g_blocks, 16 * (size_t)g_blocks) != 0;
+    const int bad = memcmp(j->got, j->want + (size_t)j->cur * g_blocks * g_dsz, g_dsz * (size_t)g_blocks) != 0;
     j->cur = (j->cur + 1) % g_nvec;
     return bad;
 }
@@ -134,8 +150,8 @@ static void *worker(void *arg)
     j->buf = malloc(vec * g_nvec + 64);
     j->ptrs = malloc(sizeof(void *) * g_blocks * g_nvec);
     j->lens = malloc(sizeof(uint32_t) * g_blocks);
-    j->want = malloc(16 * (size_t)g_blocks * g_nvec);
-    j->got = malloc(16 * (size_t)g_blocks);
+    j->want = malloc(g_dsz * (size_t)g_blocks * g_nvec);
+    j->got = malloc(g_dsz * (size_t)g_blocks);
     if (!j->buf || !j->ptrs || !j->lens || !j->want || !j->got) j->rc = -ENOMEM;
     if (!j->rc) {
         oracle_xorshift_fill(j->buf, vec * g_nvec + 64, 0x5A11ull + (uint64_t)j->t * 7919u);
@@ -145,7 +161,12 @@ static void *worker(void *arg)
             for (int i = 0; i < g_blocks; i++) {
                 const size_t k = (size_t)v * g_blocks + i;
                 j->ptrs[k] = j->buf + v * vec + (size_t)i * g_len;
-                oracle_md5(j->ptrs[k], j->lens[i], j->want[k]);
+                if (g_crc >= 0) {
+                    const uint32_t c = oracle_blk_crc(j->ptrs[k], j->lens[i], (uint32_t)g_crc);
+                    memcpy(j->want + 4 * k, &c, 4);
+                } else {
+                    oracle_md5(j->ptrs[k], j->lens[i], j->want + 16 * k);
+                }
             }
         if (g_register) j->rc = md5hip_host_register(j->buf, vec * g_nvec + 64);
     }
@@ -158,7 +179,7 @@ static void *worker(void *arg)
     pthread_barrier_wait(&g_go);
     const double t_end = g_t_end;
     while (!j->rc && now() < t_end) {
-        memset(j->got, 0, 16 * (size_t)g_blocks);
+        memset(j->got, 0, g_dsz * (size_t)g_blocks);
         const double c0 = thread_cpu(), t0 = now();
         const int rc = one_call(j);
         const double t1 = now(), c1 = thread_cpu();
@@ -250,11 +271,20 @@ int main(int argc, char **argv)
         if (g_nvec < 1) g_nvec = 1;
     }
     int rc = 0;
+    {
+        const char *e = getenv("ASIO_CRC");
+        if (e && *e) {
+            g_crc = atoi(e);
+            g_dsz = 4;
+        }
+    }
     if (g_target == T_BATCHER) rc = md5hip_batcher_create(0, slice, nslots, &g_b);
     if (g_target == T_POOL) {
         const int devs[2] = {0, 0};
         rc = md5hip_pool_create(devs, 2, slice, nslots, &g_p);
     }
+    if (rc == 0 && g_crc >= 0 && g_b) rc = md5hip_batcher_set_digest(g_b, MD5HIP_DIGEST_CRC32, (uint32_t)g_crc);
+    if (rc == 0 && g_crc >= 0 && g_p) rc = md5hip_pool_set_digest(g_p, MD5HIP_DIGEST_CRC32, (uint32_t)g_crc);
     if (rc == -ENODEV) {
         printf("{\"error\": \"no usable HIP device\", \"rc\": %d}\n", rc);
         return 77;
@@ -265,7 +295,7 @@ int main(int argc, char **argv)
     }
     {
         const char *e = getenv("ASIO_FIXED_BG_MIB");
-        if (e && g_b) g_bg.bytes = (size_t)atoi(e) << 20;
+        if (e && g_b && g_crc < 0) g_bg.bytes = (size_t)atoi(e) << 20;   /* MD5 runs only */
     }
     pthread_t bg_th;
     if (g_bg.bytes) {
@@ -340,7 +370,8 @@ int main(int argc, char **argv)
                     st.max_tickets_per_launch = s2.max_tickets_per_launch;
             }
     }
-    printf("{\"target\": \"%s\", \"mode\": \"%s\", \"vectors_per_thread\": %d, \"threads\": %d, "
+    printf("{\"digest\": \"%s\", \"fastcrc\": %d, ", g_crc >= 0 ? "crc32" : "md5", g_crc >= 0 ? g_crc : 0);
+    printf("\"target\": \"%s\", \"mode\": \"%s\", \"vectors_per_thread\": %d, \"threads\": %d, "
            "\"blocks\": %d, \"block_bytes\": %u, \"secs\": %.3f, "
            "\"calls\": %zu, \"lat_us\": {\"p50\": %.1f, \"p90\": %.1f, \"p99\": %.1f, \"max\": %.1f}, "
            "\"thread_cpu_us_per_call\": {\"mean\": %.2f, \"p50\": %.2f, \"p99\": %.2f}, "
