@@ -46,6 +46,16 @@ def test_asio_probe_host_target_matches_oracle():
     assert rc == 0 and rec["mismatches"] == 0 and rec["calls"] > 0
 
 
+@pytest.mark.parametrize("fastcrc", [0, 128])
+def test_asio_probe_crc_host_leg_matches_oracle(fastcrc):
+    """ASIO_CRC: the host leg's CRC-32 (the library's nc_crc32 over
+    blk_make_crc's windows) against the oracle's blk_make_crc rule
+    (oracle/crc32_oracle.c), whole blocks and fastcrc = 128."""
+    rc, rec = _run("host", 2, 8, 16384, 0.2, ASIO_CRC=str(fastcrc))
+    assert rc == 0 and rec["mismatches"] == 0 and rec["calls"] > 0, rec
+    assert rec["digest"] == "crc32" and rec["fastcrc"] == fastcrc
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("target", ["batcher", "pool"])
 def test_asio_scale_cpu_per_call_bounded(cuda, target):
