@@ -1961,7 +1961,7 @@ static int fixed_submit(md5hip_batcher *b, int kind, uint32_t fastcrc, const voi
     struct dev_guard g;
     if (dev_enter(&g, b->device)) return -ENODEV;
     const unsigned char *src = (const unsigned char *)base;
-    uint64_t per = dev_src ? b->maxn : b->cap / stride;
+    uint64_t per = dev_src || !stride ? b->maxn : b->cap / stride;   /* stride 0: empty chunks */
     if (per > b->maxn) per = b->maxn;
     /* a pageable source is copied into the slot's pinned staging by this
      * thread: HIP's own pageable H2D path stalls other threads' HIP calls on

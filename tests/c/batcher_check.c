@@ -302,17 +302,21 @@ static void *worker(void *arg)
             break;
         }
         default: {
-            const uint32_t L = 4096;
+            /* 4 KiB pages; or ragged lengths at a larger stride; or empty
+             * chunks at stride 0 */
+            const uint32_t shape = (uint32_t)(rnd(&s) % 8);
+            const uint32_t L = shape < 5 ? 4096 : shape < 7 ? (uint32_t)(rnd(&s) % 4096) : 0;
+            const uint64_t S = shape < 5 ? 4096 : shape < 7 ? 4096 + 16 * (rnd(&s) % 8) : 0;
             const uint64_t k = rnd(&s) % 300;
             const int m = 1 + (int)(rnd(&s) % 60);
-            const unsigned char *base = g_heap + k * L;
-            rc = rnd(&s) & 1 ? md5hip_batch_host_fixed(g_b, base, (uint64_t)m, L, L, &dig[0][0])
-                             : md5hip_pool_host_fixed(g_pool, base, (uint64_t)m, L, L, &dig[0][0]);
+            const unsigned char *base = g_heap + k * 4096;
+            rc = rnd(&s) & 1 ? md5hip_batch_host_fixed(g_b, base, (uint64_t)m, L, S, &dig[0][0])
+                             : md5hip_pool_host_fixed(g_pool, base, (uint64_t)m, L, S, &dig[0][0]);
             for (int i = 0; i < m && !rc; i++) {
                 unsigned char w[16];
                 struct MD5Context c;
                 MD5Init(&c);
-                MD5Update(&c, base + (uint64_t)i * L, L);
+                MD5Update(&c, base + (uint64_t)i * S, L);
                 MD5Final(w, &c);
                 if (memcmp(w, dig[i], 16)) rc = -2000 - i;
             }
