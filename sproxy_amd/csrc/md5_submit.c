@@ -1357,6 +1357,13 @@ static void src_copy_range(const struct chunk_src *s, uint64_t i, uint64_t a, ui
  * F = 128: 256 B over PCIe instead of 16 KiB).  F = 0 (MD5 too): L. */
 static inline uint64_t staged_len(uint32_t F, uint64_t L) { return F && L > F ? 2ull * F : L; }
 
+/* Table entries a zero-copy chunk of `ns` segments may take: one per
+ * segment, or per segment a window touches (two windows can share one),
+ * plus two spare.  submit() sends a chunk zero-copy only if this
+ * fits an empty slot (win = 1, whatever the digest), so reserve() always
+ * places it. */
+static inline uint64_t zc_pieces(uint64_t ns, int win) { return (win ? 2 * ns : ns) + 2; }
+
 /* chunk i as staged: whole, or its head and tail windows */
 static void src_copy_staged(const struct chunk_src *s, uint64_t i, uint32_t F, unsigned char *dst)
 {
@@ -1544,9 +1551,10 @@ static long reserve(md5hip_batcher *b, struct slot *sl, const struct chunk_src *
             if (sl->used + sz > b->cap) break;
             if (zc) {
                 const uint64_t ns = src_nseg(src, j);
-                if (sl->nseg + ns + 2 > b->segcap || sl->ndma + ns + 2 > b->segcap) break;
                 /* the chunk's byte ranges staged: all of it, or its windows */
                 const int win = E != L;
+                const uint64_t need = zc_pieces(ns, win);
+                if (sl->nseg + need > b->segcap || sl->ndma + need > b->segcap) break;
                 const uint64_t ra[2] = {0, win ? L - F : 0}, rl[2] = {win ? F : L, win ? F : 0};
                 uint64_t at = sl->used;
                 for (int w = 0; w < 2; w++) {
@@ -1631,7 +1639,7 @@ static int submit(md5hip_batcher *b, const struct chunk_src *src, uint64_t n, un
         src_registered(src, n)) {
         zc = 1;
         for (uint64_t i = 0; i < n; i++)
-            if (src_nseg(src, i) > b->segcap) zc = 0;   /* a chunk too fragmented for one table */
+            if (zc_pieces(src_nseg(src, i), 1) > b->segcap) zc = 0;   /* too fragmented for one table */
     }
     const int mode = src->dptrs ? MODE_NONE : zc ? MODE_ZEROCOPY : MODE_STAGED;
     pthread_mutex_lock(&b->mu);
