@@ -1352,23 +1352,25 @@ static void src_copy_range(const struct chunk_src *s, uint64_t i, uint64_t a, ui
 
 /* What a digest reads of an L-byte chunk: netcache's CRC-32 with a fastcrc
  * window F < L reads only the first and the last F bytes (blk_io.c:408-424),
- * so only those 2F bytes are staged and sent, as ONE 2F-byte chunk whose own
- * fastcrc digest is the same crc(head) ^ crc(tail) (a 16 KiB block with
- * F = 128: 256 B over PCIe instead of 16 KiB).  F = 0 (MD5 too): L. */
-static inline uint64_t staged_len(uint32_t F, uint64_t L) { return F && L > F ? 2ull * F : L; }
+ * so for L > 2F only those 2F bytes are staged and sent, as ONE 2F-byte
+ * chunk whose own fastcrc digest is the same crc(head) ^ crc(tail) (a 16 KiB
+ * block with F = 128: 256 B over PCIe instead of 16 KiB).  Up to 2F, and
+ * for F = 0 (MD5 too), the whole chunk: never more than L bytes, so a chunk
+ * that passes submit()'s size check always fits an empty slot. */
+static inline uint64_t staged_len(uint32_t F, uint64_t L) { return F && L > 2ull * F ? 2ull * F : L; }
 
 /* Table entries a zero-copy chunk of `ns` segments may take: one per
- * segment, or per segment a window touches (two windows can share one),
- * plus two spare.  submit() sends a chunk zero-copy only if this
- * fits an empty slot (win = 1, whatever the digest), so reserve() always
- * places it. */
-static inline uint64_t zc_pieces(uint64_t ns, int win) { return (win ? 2 * ns : ns) + 2; }
+ * segment, one more when it is sent as two windows (one segment may hold
+ * both), plus two spare.  submit() sends a chunk zero-copy only if this fits
+ * an empty slot (win = 1, whatever the digest), so reserve() always places
+ * it. */
+static inline uint64_t zc_pieces(uint64_t ns, int win) { return ns + (win ? 1 : 0) + 2; }
 
 /* chunk i as staged: whole, or its head and tail windows */
 static void src_copy_staged(const struct chunk_src *s, uint64_t i, uint32_t F, unsigned char *dst)
 {
     const uint64_t L = F ? src_len(s, i) : 0;
-    if (!F || L <= F) {
+    if (staged_len(F, L) == L) {
         src_copy(s, i, dst);
         return;
     }

@@ -32,7 +32,9 @@
  * gets -EIO, tickets coalescing behind it and every later call -ENODEV,
  * nothing is enqueued on the device again, no caller hangs; a 2-device pool
  * moves a synchronous submission off the failed device and never routes to
- * it again; 8 threads at once while a device dies under them.
+ * it again; 8 threads at once while a device dies under them.  Then
+ * fragmented(): chunks of ~4,096 one-byte registered segments, at the edge of
+ * a slot's zero-copy table, MD5 and fastcrc.
  * Exits 0 when every check holds.
  */
 #include <errno.h>
@@ -805,12 +807,13 @@ static int device_lost(void)
  * zero-copy table size (4,096 entries for a 1 MiB slice): a chunk goes
  * zero-copy only if its pieces fit an empty slot, else it is staged; either
  * way it is placed (a chunk one table entry too big once closed slot after
- * empty slot without end), and a fastcrc chunk counts two pieces per segment. */
+ * empty slot without end); a fastcrc chunk sent as its two windows takes one
+ * entry more. */
 static int fragmented(void)
 {
     static struct md5hip_iov segs[4200];
     static unsigned char flat[4200];
-    const uint64_t ns_md5[] = {4094, 4095, 4096, 4097}, ns_crc[] = {150, 2046, 2047, 2100};
+    const uint64_t ns_md5[] = {4094, 4095, 4096, 4097}, ns_crc[] = {150, 4093, 4094, 4097};
     for (int pass = 0; pass < 8; pass++) {
         const int crc = pass >= 4;
         const uint64_t ns = crc ? ns_crc[pass - 4] : ns_md5[pass];
