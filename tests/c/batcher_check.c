@@ -843,6 +843,22 @@ static int fragmented(void)
             return 1;
         }
     }
+    /* a fastcrc window over half the slice: a chunk between F and 2F bytes
+     * is staged whole (its two windows would not fit the slot) */
+    md5hip_batcher *wb = NULL;
+    int rc = md5hip_batcher_create(0, 1u << 20, 2, &wb);
+    if (!rc) rc = md5hip_batcher_set_digest(wb, MD5HIP_DIGEST_CRC32, 600u << 10);
+    const uint32_t F = 600u << 10, L = 700u << 10;
+    const void *p[2] = {g_heap, g_pageable};
+    const uint32_t l[2] = {L, L};
+    uint32_t crc[2] = {0, 0};
+    if (!rc) rc = md5_batch_submit(wb, p, l, 2, (unsigned char *)crc);
+    const uint32_t want = nc_crc32(g_heap, F) ^ nc_crc32(g_heap + L - F, F);
+    md5hip_batcher_destroy(wb);
+    if (rc || crc[0] != want || crc[1] != want) {
+        printf("FAIL fastcrc window over half the slice: rc %d\n", rc);
+        return 1;
+    }
     printf("fragmented chunks: zero-copy or staged, every digest ok\n");
     return 0;
 }
