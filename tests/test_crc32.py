@@ -273,8 +273,8 @@ def test_gpu_crc_queue_long_blocks_split(cuda):
 @pytest.mark.parametrize("registered", [False, True])
 def test_gpu_fastcrc_host_blocks_stage_only_windows(cuda, registered):
     """A CRC-32 batcher with a fastcrc window F stages (or maps, zero-copy)
-    only the first and last F bytes of each longer host block (md5_submit.c
-    staged_len): lengths around F and 2F, empty blocks, and page lists cut
+    only the first and last F bytes of each host block over 2F bytes (shorter
+    ones whole; md5_submit.c staged_len): lengths around F and 2F, empty blocks, and page lists cut
     inside either window.  Every CRC equals crc32.c's blk_make_crc rule
     (blk_io.c:408-424), and the bytes staged are the windows' (stats)."""
     F = 128
@@ -297,9 +297,58 @@ def test_gpu_fastcrc_host_blocks_stage_only_windows(cuda, registered):
             got = b.submit_iov(chunks)
             st = b.stats()
         assert np.array_equal(np.asarray(got).view(np.uint32).reshape(-1), want)
-        staged = sum(((2 * F if L > F else L) + 127) & ~127 for L in lens)
+        staged = sum(((2 * F if L > 2 * F else L) + 127) & ~127 for L in lens)   # up to 2F: whole
         if not registered:
             assert st["bytes_staged"] == staged, (st["bytes_staged"], staged)
     finally:
         if registered:
             m.unregister_host(buf)
+
+
+
+@pytest.mark.gpu
+def test_gpu_fastcrc_window_over_half_the_slice(cuda):
+    """A fastcrc window F over half the batcher's slice: a block between F
+    and 2F bytes is staged whole (its two windows would not fit a slot), from
+    pageable and registered memory; CRCs as blk_make_crc (blk_io.c:408-424)."""
+    F = 600 << 10
+    lens = [700 << 10, F + 4, (1 << 20) - 128]
+    offs, total = gen.pack_offsets(lens, align=16)
+    buf = gen.xorshift_array(total + 4096, seed=4242)
+    want = gen.oracle_crc32_batch(buf, offs, lens, F)
+    for registered in (False, True):
+        if registered:
+            m.register_host(buf)
+        try:
+            with m.Batcher(device=0, slice_bytes=1 << 20, kind=m.Batcher.CRC32, fastcrc=F) as b:
+                got = b.submit([memoryview(buf)[o:o + n] for o, n in zip(offs, lens)])
+            assert np.array_equal(np.asarray(got).reshape(-1), want), registered
+        finally:
+            if registered:
+                m.unregister_host(buf)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["md5", "fastcrc"])
+def test_gpu_fragmented_chunks_at_the_zero_copy_table_edge(cuda, kind):
+    """Chunks of ~4,096 one-byte segments of registered memory (a 1 MiB
+    slice's zero-copy table holds 4,096 entries): a chunk goes zero-copy only
+    if its pieces fit an empty slot, else it is staged, and either way its
+    digest is right (md5_submit.c zc_pieces)."""
+    F = 100
+    buf = gen.xorshift_array(2 * 4200 + 64, seed=4096)
+    m.register_host(buf)
+    try:
+        mk = dict(kind=m.Batcher.CRC32, fastcrc=F) if kind == "fastcrc" else {}
+        with m.Batcher(device=0, slice_bytes=1 << 20, **mk) as b:
+            for ns in (4093, 4094, 4095, 4096, 4097):
+                segs = [memoryview(buf)[2 * k:2 * k + 1] for k in range(ns)]
+                flat = np.ascontiguousarray(buf[0:2 * ns:2])
+                got = np.asarray(b.submit_iov([segs])).reshape(-1)
+                if kind == "fastcrc":
+                    want = gen.oracle_crc32_batch(flat, [0], [ns], F)
+                else:
+                    want = gen.oracle_digests(flat, [0], [ns]).reshape(-1)
+                assert np.array_equal(got, want), ns
+    finally:
+        m.unregister_host(buf)
