@@ -73,3 +73,28 @@ def test_traffic_json_merges_fetch_write_and_valu_passes(tmp_path):
     assert abs(e["valu_busy"] - 0.75) < 1e-9 and e["gpu_cycles"] == 1000
     from sproxy_amd import md5 as m
     assert e["code_hash"] == m.kernel_code_hash("md5_fixed_xdma1nt")
+
+
+def test_cited_evidence_exists():
+    """Every `profiles/...` file the docs cite is in the tree, and every
+    `scripts/...` path they cite is either in the tree or in
+    scripts/README.md's table of deleted scripts (recoverable from git)."""
+    import glob
+    import re
+    deleted = open(os.path.join(REPO, "scripts", "README.md")).read()
+    missing = []
+    for doc in ("DESIGN.md", "INTEGRATION.md", "README.md", "DESIGN_HISTORY.md",
+                os.path.join("profiles", "README.md")):
+        text = open(os.path.join(REPO, doc)).read()
+        for ref in set(re.findall(r"`((?:profiles|scripts)/[^`\s]+)`", text)):
+            p = ref.split("::")[0].rstrip(".,;:")
+            if "{" in p or "<" in p or ".." in p or (p.startswith("scripts/") and "*" in p):
+                continue                                  # a family of files, not one path
+            if glob.glob(os.path.join(REPO, p)):
+                continue
+            name = os.path.splitext(os.path.basename(p.rstrip("/")))[0]
+            if p.startswith("scripts/") and name and f"`{name}`" in deleted or \
+                    p.startswith("scripts/") and os.path.basename(p) in deleted:
+                continue
+            missing.append((doc, p))
+    assert not missing, missing
