@@ -7,6 +7,9 @@ choosing at random per step among
   queue submit_device(_async) with host or device digests, ordered after
   the thread's own torch stream, and the same through a CRC-32 queue
   (blk_make_crc digests; small and long-block vectors pick the split kernel),
+  device-resident fixed-length runs on the queue (md5_batch_submit_device_fixed,
+  host or device digests), and fastcrc = 128 page lists through a CRC-32
+  batcher that stages only each block's windows,
 over random vectors (1-300 chunks, 0 B - 1 MiB, tails, zero-length) cut from
 a registered page heap or from pageable memory.  Every digest is checked
 against digests the oracle computed up front.  Prints one JSON summary; exits
@@ -62,6 +65,9 @@ def main():
     q = m.Queue(device=0, max_chunks=1 << 16)
     qc = m.Queue(device=0, max_chunks=1 << 16)    # CRC-32 (blk_make_crc) through its own queue
     qc.set_digest(m.Batcher.CRC32)
+    F = 128
+    fb = m.Batcher(device=0, slice_bytes=8 << 20, nslots=3, kind=m.Batcher.CRC32, fastcrc=F)
+    want_fast = gen.oracle_crc32_batch(heap, offs, lens, F)
     stop = time.perf_counter() + a.secs
     counts, errors = {}, []
     lock = threading.Lock()
@@ -82,7 +88,7 @@ def main():
                 bufs = [src[offs[i]:offs[i] + lens[i]] for i in idx]
                 exp = want[idx]
                 op = r.choice(["sync", "async", "iov", "iov_async", "verify", "qdev", "qdev_async", "fixed",
-                               "crc_qdev", "crc_qdev_async"])
+                               "crc_qdev", "crc_qdev_async", "qfixed", "fastcrc_iov"])
                 if op == "sync":
                     assert np.array_equal(pool.submit(bufs), exp), op
                 elif op == "async":
@@ -122,6 +128,27 @@ def main():
                             assert np.array_equal(got, ec), op
                         else:
                             held.append((qc.submit_device_async(ptrs, L), ec))
+                elif op == "qfixed":
+                    n = r.randint(1, 64)
+                    Lf = r.choice([64, 4096, 16384])
+                    S = Lf + r.choice([0, 0, 64, 128])
+                    j = r.randrange(0, (total - n * S) // 64) * 64
+                    exp2 = gen.oracle_digests(heap, [j + i * S for i in range(n)], [Lf] * n)
+                    with torch.cuda.stream(stream):
+                        out = torch.empty((n, 16), dtype=torch.uint8, device="cuda") if r.random() < 0.5 else None
+                        pend = q.submit_device_fixed_async(dev[j:], n, Lf, S, out=out)
+                    got = pend.wait()
+                    if out is not None:
+                        torch.cuda.synchronize()
+                        got = out.cpu().numpy()
+                    assert np.array_equal(np.asarray(got), exp2), op
+                elif op == "fastcrc_iov":
+                    pages = []
+                    for b in bufs:
+                        c1 = r.randint(0, len(b))
+                        pages.append([b[:c1], b[c1:]])
+                    got = np.asarray(fb.submit_iov(pages)).reshape(-1)
+                    assert np.array_equal(got, want_fast[idx]), op
                 else:
                     j = r.randrange(nchunks - 40)
                     n = r.randint(1, 40)
@@ -156,12 +183,15 @@ def main():
     pool.close()
     q.close()
     qc.close()
+    fst = fb.stats()
+    fb.close()
     m.unregister_host(heap)
     print(json.dumps({"secs": round(wall, 1), "threads": a.threads, "ops": counts,
                       "pool": st, "pool_device_launches": [d["launches"] for d in dstats],
                       "pool_coalesced": [d["coalesced_launches"] for d in dstats],
                       "queue": {k: qst[k] for k in ("submissions", "launches", "coalesced_launches")},
                       "crc_queue": {k: qcst[k] for k in ("submissions", "launches", "coalesced_launches")},
+                      "fastcrc_batcher": {k: fst[k] for k in ("submissions", "launches", "bytes_staged")},
                       "errors": errors}))
     return 1 if errors else 0
 
