@@ -352,3 +352,38 @@ def test_gpu_fragmented_chunks_at_the_zero_copy_table_edge(cuda, kind):
                 assert np.array_equal(got, want), ns
     finally:
         m.unregister_host(buf)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("registered", [False, True])
+def test_gpu_driver_test_shape(cuda, registered):
+    """netcache's own stress configuration (driver_test.c:583-586:
+    chunk_size 256 KiB, fastcrc 128) against its loopback origin, whose blocks
+    begin with "0123456789ABCDEF" (NC_VALIDATE_ORIGIN_DATA, bc_mgr.c:1419-1456):
+    vectors of 256 KiB blocks handed over as lists of 16 KiB pages, a short
+    last block included.  Store (blk_make_crc, blk_io.c:851-863) and verify
+    with one corrupted block (blk_io.c:665-704: only that block fails) through
+    one CRC-32 batcher with fastcrc 128, and the same vectors' MD5."""
+    F, B, P = 128, 256 << 10, 16 << 10
+    lens = [B] * 7 + [B - 5000]
+    offs = [k * B for k in range(len(lens))]
+    buf = gen.xorshift_array(len(lens) * B + 4096, seed=583)
+    for o in offs:
+        buf[o:o + 16] = np.frombuffer(b"0123456789ABCDEF", np.uint8)
+    if registered:
+        m.register_host(buf)
+    try:
+        pages = [[memoryview(buf)[o + a:o + min(a + P, L)] for a in range(0, L, P)] for o, L in zip(offs, lens)]
+        want = gen.oracle_crc32_batch(buf, offs, lens, F)
+        with m.Batcher(device=0, kind=m.Batcher.CRC32, fastcrc=F) as b:
+            got = np.asarray(b.submit_iov(pages)).reshape(-1)
+            assert np.array_equal(got, want)
+            bad = got.copy()
+            bad[3] ^= 1
+            ok, nbad = b.verify_iov(pages, bad)
+            assert nbad == 1 and not ok[3] and ok.sum() == len(lens) - 1
+        with m.Batcher(device=0) as b:
+            assert np.array_equal(np.asarray(b.submit_iov(pages)), gen.oracle_digests(buf, offs, lens))
+    finally:
+        if registered:
+            m.unregister_host(buf)
