@@ -66,6 +66,7 @@ def main():
     ap.add_argument("--policies", default="spin,tail,block", help="--matrix watch: MD5HIP_WATCH values")
     ap.add_argument("--slice-mib", type=int, default=0, help="batcher slice (0 = the library default)")
     ap.add_argument("--secs", type=float, default=3.0)
+    ap.add_argument("--sizes-kib", default="16,128,1024", help="--matrix chunk: block sizes in KiB")
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
     runs = []
@@ -105,7 +106,7 @@ def main():
                         for target in ("batcher", "host"):
                             runs.append(run(target, T, B, L, a.secs, timeout=300))
     else:
-        for L in (16384, 131072, 1 << 20):
+        for L in [int(k) << 10 for k in a.sizes_kib.split(",")]:
             for B in (8, 64):
                 for T in (1, 8, 64):
                     for target in ("batcher", "host"):
