@@ -92,9 +92,9 @@ def test_cited_evidence_exists():
                 continue                                  # a family of files, not one path
             if glob.glob(os.path.join(REPO, p)):
                 continue
-            name = os.path.splitext(os.path.basename(p.rstrip("/")))[0]
-            if p.startswith("scripts/") and name and f"`{name}`" in deleted or \
-                    p.startswith("scripts/") and os.path.basename(p) in deleted:
-                continue
+            base = os.path.basename(p.rstrip("/"))
+            listed = f"`{os.path.splitext(base)[0]}`" in deleted or base in deleted
+            if p.startswith("scripts/") and listed:
+                continue                                  # deleted; recoverable from git
             missing.append((doc, p))
     assert not missing, missing
