@@ -451,6 +451,16 @@ def test_queue_device_fixed_md5_and_fastcrc(cuda):
             crc = q.submit_device_fixed_async(dev, n, L, S, after=None).wait()
             assert np.array_equal(crc, gen.oracle_crc32_batch(host, offs, [L] * n, fastcrc=F)), F
         st = q.stats()
+        # a run whose chunks start off the 16-B grid (base + 3, stride 5,001):
+        # the kernels' unaligned paths, MD5 and CRC-32 whole and windowed
+        n2, S2 = 2000, 5001
+        offs2 = [3 + i * S2 for i in range(n2)]
+        for kind, F in ((m.Batcher.MD5, 0), (m.Batcher.CRC32, 0), (m.Batcher.CRC32, 128)):
+            q.set_digest(kind, F)
+            got = q.submit_device_fixed_async(dev[3:], n2, L, S2, after=None).wait()
+            want2 = gen.oracle_digests(host, offs2, [L] * n2) if kind == m.Batcher.MD5 else \
+                gen.oracle_crc32_batch(host, offs2, [L] * n2, fastcrc=F)
+            assert np.array_equal(got, want2), (kind, F)
     assert st["launches"] >= 3 * 7
 
 
