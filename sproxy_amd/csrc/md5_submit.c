@@ -1422,6 +1422,7 @@ static void gather_range(const struct chunk_src *src, uint64_t first, uint64_t m
     if (bytes < GATHER_SPLIT_MIN) T = 1;
     if (T > bytes / GATHER_PART_MIN) T = bytes / GATHER_PART_MIN ? bytes / GATHER_PART_MIN : 1;
     if (T > m) T = m ? m : 1;
+    T = T < 1 ? 1 : T > 32 ? 32 : T;                /* the arrays below */
     struct gather_part part[32];
     pthread_t tid[32];
     int started[32] = {0};
@@ -1942,6 +1943,7 @@ static void copy_parallel(void *dst, const void *src, uint64_t bytes)
     uint64_t T = (uint64_t)g_gather_threads;
     if (bytes < GATHER_SPLIT_MIN) T = 1;
     if (T > bytes / GATHER_PART_MIN) T = bytes / GATHER_PART_MIN ? bytes / GATHER_PART_MIN : 1;
+    T = T < 1 ? 1 : T > 32 ? 32 : T;                /* the arrays below */
     struct copy_part part[32];
     pthread_t tid[32];
     int started[32] = {0};
