@@ -102,15 +102,19 @@ int main(int argc, char **argv)
     uint64_t bytes = n * (uint64_t)len;
     unsigned char *data = malloc(bytes + 8);
     unsigned char *dig = malloc(DSZ * n);
-    if (!data || !dig) { fprintf(stderr, "oom\n"); return 1; }
+    double *t = malloc(sizeof(double) * reps);
+    pthread_t *tid = malloc(sizeof(pthread_t) * threads);
+    struct job *jobs = malloc(sizeof(struct job) * threads);
+    if (!data || !dig || !t || !tid || !jobs) {
+        fprintf(stderr, "oom\n");
+        free(data); free(dig); free(t); free(tid); free(jobs);
+        return 1;
+    }
     uint64_t s = 0x9E3779B97F4A7C15ull;
     for (uint64_t off = 0; off < bytes; off += 8) {
         s ^= s << 13; s ^= s >> 7; s ^= s << 17;
         for (int k = 0; k < 8; k++) data[off + k] = (unsigned char)(s >> (8 * k));
     }
-    double *t = malloc(sizeof(double) * reps);
-    pthread_t *tid = malloc(sizeof(pthread_t) * threads);
-    struct job *jobs = malloc(sizeof(struct job) * threads);
     for (int r = 0; r < reps; r++) {
         double t0 = now_s();
         for (int k = 0; k < threads; k++) {
