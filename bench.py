@@ -68,9 +68,15 @@ def parse_args(argv):
                    help="chunks per rank re-digested by the host reference after timing (0 = off)")
     p.add_argument("--dist-always", action="store_true",
                    help="bring the process group up even at WORLD_SIZE 1 (a one-GPU rehearsal "
-                        "of the RCCL control plane: init, barrier, MAX, object gathers)")
-    p.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
-                   help="control-plane backend for N > 1 (barrier + scalar MAX + gathers only)")
+                        "of the control plane: init, barrier, MAX, object gathers)")
+    p.add_argument("--dist-backend", default="gloo", choices=["nccl", "gloo"],
+                   help="control-plane backend for N > 1: a barrier, scalar MAX and object "
+                        "gathers, no data-path collective.  gloo by default: with an RCCL "
+                        "communicator up, the C2 kernel ran 3-5 %% slower on the same GPU "
+                        "(profiles/r05w/); nccl brings RCCL up for the same control plane")
+    p.add_argument("--share-gpu", action="store_true",
+                   help="N > 1 ranks on fewer GPUs (a rehearsal on a one-GPU box); without it "
+                        "every rank needs a GPU of its own")
     p.add_argument("--dry-run", action="store_true",
                    help="CPU only (no GPU): exercises launch, ranks and aggregation with the "
                         "product's host MD5 (md5_stream.c) on a small host batch")
@@ -130,8 +136,11 @@ def env_rank():
 
 def dist_setup(a):
     """One process per GPU.  The collectives are a barrier, scalar MAX/SUM
-    reductions and small object gathers, so gloo (CPU) serves as well as RCCL;
-    it lets N ranks share one GPU for a rehearsal on a one-GPU box."""
+    reductions and small object gathers -- the chunks are independent, so no
+    byte crosses between ranks -- and gloo (CPU) carries them by default: a
+    live RCCL communicator made the C2 kernel 3-5 % slower on its GPU
+    (profiles/r05w/).  With --share-gpu, N ranks may share one GPU (a
+    rehearsal on a one-GPU box)."""
     global COLL_DEVICE, COLL_ON
     rank, world, local = env_rank()
     if world != a.gpus:
@@ -142,8 +151,9 @@ def dist_setup(a):
         ndev = torch.cuda.device_count()
         if ndev < 1:
             raise SystemExit("bench.py: no HIP device visible (use --dry-run on a CPU host)")
-        if backend == "nccl" and world > 1 and local >= ndev:
-            raise SystemExit(f"bench.py: LOCAL_RANK {local} but only {ndev} GPUs visible")
+        if world > 1 and local >= ndev and (backend == "nccl" or not a.share_gpu):
+            raise SystemExit(f"bench.py: LOCAL_RANK {local} but only {ndev} GPUs visible"
+                             + ("" if backend == "nccl" else " (--share-gpu for a rehearsal)"))
         device = local % ndev
         torch.cuda.set_device(device)
     if world > 1 or a.dist_always:
