@@ -42,9 +42,7 @@ METRIC = "device-resident MD5 GiB/s on batched 16 KiB chunks at 1/2/4/8 MI355X"
 GIB = float(1 << 30)
 CPU_SHARE = 16                 # host cores a one-GPU box grants a job (the box's CPU share)
 
-torch = m = None               # imported after the launcher decision (see main)
-COLL_DEVICE = "cuda"           # where the control-plane scalars live (cpu under gloo)
-COLL_ON = False                # a process group is up (world > 1, or --dist-always)
+torch = m = shard = None       # imported after the launcher decision (see main)
 
 
 # --------------------------------------------------------------------------- launch
@@ -102,12 +100,19 @@ def parse_args(argv):
     p.add_argument("--crcq-subs", type=int, default=8,
                    help="--config crcq: fixed-length device submissions per step through one queue")
     p.add_argument("--crcq-chunks", type=int, default=1 << 20, help="--config crcq: blocks per submission")
+    p.add_argument("--crcq-fastcrc", type=int, default=128,
+                   help="--config crcq: blk_make_crc's fastcrc window F (0 = the whole block)")
+    p.add_argument("--extras", default="c3q,c5",
+                   help="--config c2 at one GPU: BASELINE configs measured after the headline's "
+                        "timed region and parity, as sub-records of the same line (c3q = the C3 "
+                        "stream through md5hip_queue, c5 = end to end from pinned host memory); "
+                        "'none' for the headline alone (profiling passes)")
     p.add_argument("--c5-chunks", type=int, default=1 << 18)
     p.add_argument("--c5-slice", type=int, default=64 << 20)
     return p.parse_args(argv)
 
 
-def free_port():
+def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
@@ -121,7 +126,7 @@ def spawn_ranks(a, argv):
     replaced (no exec) -- and return the child's exit status.  Rank 0 of the
     child prints the JSON line on the inherited stdout."""
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
-           f"--nproc-per-node={a.gpus}", "--master-addr=127.0.0.1", f"--master-port={free_port()}",
+           f"--nproc-per-node={a.gpus}", "--master-addr=127.0.0.1", f"--master-port={_free_port()}",
            os.path.abspath(__file__), *argv]
     env = dict(os.environ)
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
@@ -129,20 +134,12 @@ def spawn_ranks(a, argv):
     return subprocess.call(cmd, env=env)
 
 
-def env_rank():
-    return (int(os.environ.get("RANK", "0")), int(os.environ.get("WORLD_SIZE", "1")),
-            int(os.environ.get("LOCAL_RANK", "0")))
-
-
 def dist_setup(a):
-    """One process per GPU.  The collectives are a barrier, scalar MAX/SUM
-    reductions and small object gathers -- the chunks are independent, so no
-    byte crosses between ranks -- and gloo (CPU) carries them by default: a
-    live RCCL communicator made the C2 kernel 3-5 % slower on its GPU
-    (profiles/r05w/).  With --share-gpu, N ranks may share one GPU (a
-    rehearsal on a one-GPU box)."""
-    global COLL_DEVICE, COLL_ON
-    rank, world, local = env_rank()
+    """One process per GPU, the control plane from sproxy_amd/shard.py (a
+    barrier, scalar MAX/SUM reductions and small object gathers -- the chunks
+    are independent, so no byte crosses between ranks), over gloo by default.
+    With --share-gpu, N ranks may share one GPU (a rehearsal on a one-GPU box)."""
+    rank, world, local = shard.env_rank()
     if world != a.gpus:
         raise SystemExit(f"bench.py: --gpus {a.gpus} but WORLD_SIZE={world}")
     backend = "gloo" if a.dry_run else a.dist_backend
@@ -156,44 +153,8 @@ def dist_setup(a):
                              + ("" if backend == "nccl" else " (--share-gpu for a rehearsal)"))
         device = local % ndev
         torch.cuda.set_device(device)
-    if world > 1 or a.dist_always:
-        import torch.distributed as dist
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        if world == 1:                   # a one-rank group without a launcher
-            os.environ.setdefault("RANK", "0")
-            os.environ.setdefault("WORLD_SIZE", "1")
-            os.environ.setdefault("MASTER_PORT", str(free_port()))
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", device))
-        else:
-            dist.init_process_group("gloo")
-        COLL_DEVICE = "cuda" if backend == "nccl" else "cpu"
-        COLL_ON = True
+    shard.init_group(world, backend, device, always=a.dist_always)
     return rank, world, local, device, backend
-
-
-def barrier(world):
-    if COLL_ON:
-        import torch.distributed as dist
-        dist.barrier()
-
-
-def max_over_ranks(x, world):
-    if not COLL_ON:
-        return float(x)
-    import torch.distributed as dist
-    t = torch.tensor([float(x)], dtype=torch.float64, device=COLL_DEVICE)
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    return float(t.item())
-
-
-def gather_objects(obj, world):
-    if not COLL_ON:
-        return [obj]
-    import torch.distributed as dist
-    out = [None] * world
-    dist.all_gather_object(out, obj)
-    return out
 
 
 def device_info(rank, local, device):
@@ -215,7 +176,7 @@ def timed_steps(fn, steps, warmup, world):
     torch.cuda.synchronize()
     stream = torch.cuda.current_stream()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    barrier(world)
+    shard.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     e0.record(stream)
@@ -224,7 +185,7 @@ def timed_steps(fn, steps, warmup, world):
     e1.record(stream)
     torch.cuda.synchronize()
     t1 = time.perf_counter()
-    barrier(world)
+    shard.barrier()
     return t1 - t0, e0.elapsed_time(e1) / steps
 
 
@@ -297,13 +258,15 @@ def check_sample(buf, offs, lens, got, threads=8):
 
 
 def sample_fixed(data, out, n, L, k, seed):
-    """(parity dict) for k sampled chunks (first and last included) of a
+    """(parity dict) for k distinct random chunks plus the first and last of a
     fixed-length device batch; chunk rows gathered on the device, one D2H."""
     import numpy as np
     if k <= 0:
         return None
     rng = np.random.default_rng(seed)
-    idx = np.unique(np.concatenate([[0, n - 1], rng.integers(0, n, size=max(0, min(k, n) - 2))]))
+    # k distinct random chunks (drawn without replacement) plus the first and
+    # last: at least k checked (SURVEY §8(d): >= 4096)
+    idx = np.unique(np.concatenate([[0, n - 1], rng.choice(n, size=min(k, n), replace=False)]))
     it = torch.from_numpy(idx.astype(np.int64)).to(data.device)
     rows = data[: n * L].view(n, L).index_select(0, it).cpu().numpy().reshape(-1)
     got = out.index_select(0, it).cpu().numpy()
@@ -398,10 +361,10 @@ def per_rank_line(res, rank, world, local, device, backend, rank_bytes, rank_wal
     """Gather every rank's own rate, device and parity into the line."""
     mine = {"gib_s": round(rank_bytes / rank_wall / GIB, 2) if rank_wall else 0.0,
             "dev": device_info(rank, local, device), "parity": parity}
-    allr = gather_objects(mine, world)
+    allr = shard.gather_objects(mine)
     res["per_gpu"] = [r["gib_s"] for r in allr]
     devs = [r["dev"] for r in allr]
-    res["ranks_seen"] = {"world": world, "backend": backend if COLL_ON else None,
+    res["ranks_seen"] = {"world": world, "backend": backend if shard.group_on() else None,
                          "distinct_devices": len({(d["host"], d.get("uuid") or d["device"]) for d in devs
                                                   if d["device"] is not None}),
                          "ranks": devs}
@@ -410,7 +373,8 @@ def per_rank_line(res, rank, world, local, device, backend, rank_bytes, rank_wal
         res["parity"] = {"ok": all(p["ok"] for p in ps), "checked": sum(p["checked"] for p in ps),
                          "mismatches": sum(p.get("mismatches", 0) for p in ps),
                          "checker": ps[0]["checker"],
-                         "sample": "first + last + seeded-random chunks of every rank's batch, "
+                         "sample": ps[0].get("sample") or
+                                   "first + last + seeded distinct random chunks of every rank's batch, "
                                    "re-digested on the host after the timed region"}
     return res
 
@@ -429,13 +393,13 @@ def run_dry(a, rank, world, local, device, backend):
 
     for _ in range(a.warmup):
         step()
-    barrier(world)
+    shard.barrier()
     t0 = time.perf_counter()
     for _ in range(a.steps):
         step()
     wall = time.perf_counter() - t0
-    barrier(world)
-    wall_max = max_over_ranks(wall, world)
+    shard.barrier()
+    wall_max = shard.max_over_ranks(wall)
     par = None
     if a.parity_sample:
         k = min(n, a.parity_sample)
@@ -488,8 +452,8 @@ def run_c2(a, rank, world, local, device, backend):
     variant = m.VARIANTS[a.variant]
     fn = lambda: m.digest_fixed(data, n, L, out=out, variant=variant)  # noqa: E731
     wall, dev_ms = timed_steps(fn, a.steps, a.warmup, world)
-    wall_max = max_over_ranks(wall, world)
-    dev_ms_max = max_over_ranks(dev_ms, world)
+    wall_max = shard.max_over_ranks(wall)
+    dev_ms_max = shard.max_over_ranks(dev_ms)
     value = float(n_all) * L * a.steps / wall_max / GIB
     alg_bytes = float(n) * (L + 16)            # read every chunk once + 16-B digest write
     achieved = alg_bytes / (dev_ms_max * 1e-3) / 1e9
@@ -528,8 +492,8 @@ def run_crc(a, rank, world, local, device, backend):
     out = torch.empty(n, dtype=torch.int32, device="cuda")
     fn = lambda: m.crc32_fixed(data, n, L, fastcrc=F, out=out)  # noqa: E731
     wall, dev_ms = timed_steps(fn, a.steps, a.warmup, world)
-    wall_max = max_over_ranks(wall, world)
-    dev_ms_max = max_over_ranks(dev_ms, world)
+    wall_max = shard.max_over_ranks(wall)
+    dev_ms_max = shard.max_over_ranks(dev_ms)
     fast = 0 < F < L
     read = 2 * F if fast else L                 # bytes blk_make_crc reads per block
     alg_bytes = float(n) * (read + 4)
@@ -564,12 +528,16 @@ def run_crcq(a, rank, world, local, device, backend):
     --crcq-chunks blocks per step (md5_batch_submit_device_fixed, ABI 4: no
     per-block descriptor crosses PCIe), each its own launch on the queue's
     slot streams, pipelined as --config c3q (step k submitted before step
-    k-1's tickets are waited for).  CRC-32 with --fastcrc F (default 128):
+    k-1's tickets are waited for).  CRC-32 with --crcq-fastcrc F (default 128, 0 = whole block):
     blk_make_crc reads F bytes at each end of a block (blk_io.c:408-424), so
     the algorithmic bytes are 2F + 4 per block."""
     L = a.len
-    F = a.fastcrc if a.fastcrc else 128
+    F = a.crcq_fastcrc
     K, n = max(1, a.crcq_subs), a.crcq_chunks
+    need, (free, _) = K * n * L, torch.cuda.mem_get_info()
+    if need > free:
+        raise SystemExit(f"bench.py --config crcq: {K} x {n} x {L} B = {need / GIB:.1f} GiB of blocks, "
+                         f"{free / GIB:.1f} GiB free on the device (lower --crcq-chunks or --crcq-subs)")
     data = torch.empty(K * n * L, dtype=torch.uint8, device="cuda")
     m.fill_synthetic(data, seed=0xC4C0 + rank)
     torch.cuda.synchronize()
@@ -591,13 +559,13 @@ def run_crcq(a, rank, world, local, device, backend):
 
     def timed(fn):
         torch.cuda.synchronize()
-        barrier(world)
+        shard.barrier()
         t0 = time.perf_counter()
         fn()
         torch.cuda.synchronize()
         wall = time.perf_counter() - t0
-        barrier(world)
-        return wall, max_over_ranks(wall, world)
+        shard.barrier()
+        return wall, shard.max_over_ranks(wall)
 
     def pipelined():
         prev = submit(0)
@@ -662,7 +630,7 @@ def crc_sample(data, n, L, F, out, k, rank):
     O = ctypes.CDLL(lib)
     O.oracle_crc32_batch.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                      ctypes.c_uint64, ctypes.c_uint32, ctypes.c_void_p]
-    idx = np.unique(np.concatenate([[0, n - 1], np.random.default_rng(77 + rank).integers(0, n, k)]))
+    idx = np.unique(np.concatenate([[0, n - 1], np.random.default_rng(77 + rank).choice(n, min(k, n), replace=False)]))
     rows = data.view(n, L)[torch.from_numpy(idx).to(data.device)].cpu().numpy()
     offs = np.arange(idx.size, dtype=np.uint64) * np.uint64(L)
     lens = np.full(idx.size, L, dtype=np.uint32)
@@ -780,7 +748,7 @@ def run_c3(a, rank, world, local, device, backend):
     out = torch.empty((lens.size, 16), dtype=torch.uint8, device="cuda")
     fn = lambda: m.digest_desc(data, d_off, d_len, d_ord, out=out, variant=dvar)  # noqa: E731
     wall, dev_ms = timed_steps(fn, a.steps, a.warmup, world)
-    wall_max = max_over_ranks(wall, world)
+    wall_max = shard.max_over_ranks(wall)
     payload = float(lens.sum())
     value = payload * world * a.steps / wall_max / GIB
     par = sample_desc(data, offs, lens, out, c3_sample(lens, order, a.parity_sample // 2, 91 + rank)) \
@@ -813,12 +781,12 @@ def run_c3(a, rank, world, local, device, backend):
 
     streamed(a.warmup)
     torch.cuda.synchronize()
-    barrier(world)
+    shard.barrier()
     t0 = time.perf_counter()
     streamed(a.steps)
     torch.cuda.synchronize()
-    s_wall = max_over_ranks(time.perf_counter() - t0, world)
-    barrier(world)
+    s_wall = shard.max_over_ranks(time.perf_counter() - t0)
+    shard.barrier()
     ok = all(torch.equal(o, out) for o in outs[:min(ns, a.steps)])
     del outs
     # coalesced: K such batches (own lengths, own bytes) planned and launched
@@ -915,13 +883,13 @@ def run_c3q(a, rank, world, local, device, backend):
 
     def timed(fn):
         torch.cuda.synchronize()
-        barrier(world)
+        shard.barrier()
         t0 = time.perf_counter()
         fn()
         torch.cuda.synchronize()
         wall = time.perf_counter() - t0
-        barrier(world)
-        return wall, max_over_ranks(wall, world)
+        shard.barrier()
+        return wall, shard.max_over_ranks(wall)
 
     def pipelined():
         # step k submits its K vectors, then waits for step k-1's: the queue
@@ -997,8 +965,8 @@ def run_ctx(a, rank, world, local, device, backend):
     lens = torch.full((n,), L, dtype=torch.int32, device="cuda")
     fn = lambda: m.update_ctx(ctx, ptrs, lens)  # noqa: E731
     wall, dev_ms = timed_steps(fn, a.steps, a.warmup, world)
-    wall_max = max_over_ranks(wall, world)
-    dev_ms_max = max_over_ranks(dev_ms, world)
+    wall_max = shard.max_over_ranks(wall)
+    dev_ms_max = shard.max_over_ranks(dev_ms)
     dig = m.final_ctx(ctx)
     # parity: each object hashed (warmup + steps) times its block -> the same
     # digest as MD5 over the block repeated; checked on a sample by the host reference
@@ -1027,6 +995,20 @@ def run_ctx(a, rank, world, local, device, backend):
                         "alg_bytes_note": "block bytes + the 88-B context read and written",
                         "traffic": traffic, "traffic_source": tnote, "valu_busy_pmc": vbusy}}
     return per_rank_line(res, rank, world, local, device, backend, float(n) * L * a.steps, wall, par)
+
+
+def c5_sample(arr, dig, n, L, per, k, seed):
+    """C5 parity: the first and last chunk, both sides of every slot
+    boundary (a slot holds `per` chunks: the batcher's slice / L), and k
+    distinct random chunks, re-digested from the host buffer after timing."""
+    import numpy as np
+    b = np.arange(per, n, per, dtype=np.int64)
+    rnd = np.random.default_rng(seed).choice(n, size=min(k, n), replace=False)
+    idx = np.unique(np.concatenate([[0, n - 1], b - 1, b, rnd]))
+    par = check_sample(arr, idx * L, np.full(idx.size, L), dig[idx])
+    par["sample"] = (f"first + last + both sides of {b.size} slot boundaries + {min(k, n)} distinct "
+                     f"random chunks, re-digested on the host after the timed region")
+    return par
 
 
 def run_c5(a, rank, world, local, device, backend):
@@ -1064,9 +1046,7 @@ def run_c5(a, rank, world, local, device, backend):
             dig = b.host_fixed(arr, n, L)
         wall = time.perf_counter() - t0
     gbs = n * L * a.steps / wall / 1e9
-    import numpy as np
-    k = min(n, a.parity_sample)
-    par = check_sample(arr, np.arange(k) * L, np.full(k, L), dig[:k]) if k else None
+    par = c5_sample(arr, dig, n, L, a.c5_slice // L, a.parity_sample, 55 + rank) if a.parity_sample else None
     res = {"metric": "end-to-end MD5 GiB/s from pinned host memory (C5)",
            "value": round(n * L * a.steps / wall / GIB, 2), "unit": "GiB/s", "n_gpus": world,
            "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(wall / a.steps * 1e3, 3),
@@ -1082,8 +1062,29 @@ def run_c5(a, rank, world, local, device, backend):
     return per_rank_line(res, rank, world, local, device, backend, n * L * a.steps, wall, par)
 
 
+EXTRA_STEPS = {"c3q": (8, 3), "c5": (5, 2)}     # (steps, warmup) of a sub-record
+
+
+def run_extra(name, a, rank, world, local, device, backend):
+    """A BASELINE config beside the headline (C3 as the queue streams it, C5
+    end to end), run after C2's timed region and parity in the same process,
+    so the driver's own run carries it: the config's own timing, roofline and
+    parity, nothing of it inside C2's measurement."""
+    import copy
+    b = copy.copy(a)
+    b.steps, b.warmup = EXTRA_STEPS[name]
+    torch.cuda.empty_cache()
+    t0 = time.perf_counter()
+    r = {"c3q": run_c3q, "c5": run_c5}[name](b, rank, world, local, device, backend)
+    keep = ("metric", "value", "unit", "steps", "warmup", "ms_per_step", "tb_s", "roofline", "drained",
+            "parity", "config")
+    out = {k: r[k] for k in keep if k in r}
+    out["run_s"] = round(time.perf_counter() - t0, 2)
+    return out
+
+
 def main(argv=None):
-    global torch, m
+    global torch, m, shard
     argv = sys.argv[1:] if argv is None else list(argv)
     a = parse_args(argv)
     if a.gpus < 1:
@@ -1093,14 +1094,19 @@ def main(argv=None):
     import torch as _torch
     torch = _torch
     sys.path.insert(0, REPO)
-    from sproxy_amd import md5 as _m
-    m = _m
+    from sproxy_amd import md5 as _m, shard as _shard
+    m, shard = _m, _shard
     rank, world, local, device, backend = dist_setup(a)
     if a.dry_run:
         res = run_dry(a, rank, world, local, device, backend)
     else:
         res = {"c2": run_c2, "c3": run_c3, "c3q": run_c3q, "c5": run_c5, "crc": run_crc,
                "crcq": run_crcq, "ctx": run_ctx}[a.config](a, rank, world, local, device, backend)
+    if a.config == "c2" and world == 1 and not a.dry_run and a.extras != "none":
+        for name in [x for x in a.extras.split(",") if x]:
+            if name not in EXTRA_STEPS:
+                raise SystemExit(f"bench.py: --extras {name}: one of {sorted(EXTRA_STEPS)} or none")
+            res[name] = run_extra(name, a, rank, world, local, device, backend)
     if rank == 0 and world == 1 and not a.dry_run and not a.no_cpu_baseline:
         if a.config == "c2":
             res["cpu_baseline"] = cpu_baseline()
@@ -1110,10 +1116,7 @@ def main(argv=None):
             res["cpu_baseline"] = cpu_baseline_crc()
     if rank == 0:
         print(json.dumps(res), flush=True)
-    if COLL_ON:
-        import torch.distributed as dist
-        dist.barrier()
-        dist.destroy_process_group()
+    shard.close_group()
 
 
 if __name__ == "__main__":

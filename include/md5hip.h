@@ -307,13 +307,20 @@ int md5hip_batcher_set_linger(md5hip_batcher *b, uint32_t max_us);
 int md5hip_batcher_set_chain(md5hip_batcher *b, int mode);
 
 /* ABI 4: device failure.  blk_make_crc cannot fail (blk_io.c:354-430); a
- * batcher can.  When a launch's completion event reports an error (a kernel
- * fault, a lost or reset device), or an enqueue fails and the slot's stream
- * then reports one, the batcher is FAILED for good:
+ * batcher can.  When HIP reports an error back -- a launch's completion
+ * event does (a lost or reset device), or an enqueue fails and the slot's
+ * stream then reports one -- the batcher is FAILED for good:
  *   - the tickets of that launch complete with -EIO;
  *   - tickets still coalescing in the open slot complete with -ENODEV;
  *   - every later submission returns -ENODEV at once, touching nothing;
- *   - no digest of a failed launch is written anywhere.
+ *   - no digest of a failed launch is copied into a HOST digest array; a
+ *     DEVICE digest array (digests_on_device) the launch wrote in place, or
+ *     the scatter kernel had filled, is undefined after -EIO / -ENODEV.
+ * A kernel memory fault on ROCm usually ends the process through the HSA
+ * queue's error handler before any event reports it, so the policy covers
+ * what the runtime returns, and was checked by injection
+ * (md5hip_batcher_inject_fault, the fake runtime of tests/c/), not against
+ * a real fault.
  * Launches already in flight complete as their own events say.  The library
  * never falls back to the host: what the call site does instead (and that a
  * device error is never a checksum mismatch) is INTEGRATION.md §2j.
@@ -330,7 +337,8 @@ struct md5hip_batcher_stats {
     uint64_t launches;                /* slots launched */
     uint64_t coalesced_launches;      /* launches holding chunks of > 1 ticket */
     uint64_t chunks;                  /* chunks launched */
-    uint64_t bytes_staged;            /* host bytes moved through staging */
+    uint64_t bytes_staged;            /* host bytes moved through staging (host_fixed: a pageable
+                                         source's; a wholly pinned one is DMA'd in place, 0) */
     uint64_t max_chunks_per_launch;
     uint64_t max_tickets_per_launch;
     uint64_t inflight_target, nslots, max_chunks_per_slot;
@@ -456,8 +464,12 @@ int md5hip_host_register(void *base, uint64_t bytes);
 int md5hip_host_unregister(void *base);
 int md5hip_batcher_set_gather(md5hip_batcher *b, int mode);
 
-/* digests[i] = MD5(h_base + i*stride, len) from one contiguous host buffer
- * (pinned for full PCIe rate), copied slice by slice with no host gather. */
+/* digests[i] = MD5(h_base + i*stride, len) from one contiguous host buffer,
+ * copied slice by slice with no host gather.  A source the runtime has
+ * page-locked over its WHOLE range (hipHostMalloc, hipHostRegister, or
+ * md5hip_host_register) is DMA'd in place at full PCIe rate; any other --
+ * pageable, or pinned only in part -- is copied through the slot's pinned
+ * staging by the calling thread first. */
 int md5hip_batch_host_fixed(md5hip_batcher *b, const void *h_base, uint64_t n, uint32_t len,
                             uint64_t stride, unsigned char *digests);
 

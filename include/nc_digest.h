@@ -66,13 +66,19 @@ int nc_digest_compare(const void *arr, uint64_t arr_size, uint32_t dsz, const ui
 uint32_t nc_crc32(const void *data, uint64_t len);
 
 /* CRC of a header as written/verified: header_size (from the header) bytes
- * with crc, disk_header_size and flag read as zero.  0 for a header whose
- * header_size < NC_HDR_MIN_SIZE. */
+ * with crc, disk_header_size and flag read as zero wherever they fall inside
+ * them -- for 0 <= header_size < NC_HDR_MIN_SIZE only part of the fixed part,
+ * as dm_verify_header does (diskcache.c:3676-3686); header_size 0 gives 0.
+ * 0 for a negative header_size, which the reference would pass on to
+ * crc32_8bytes as a huge size_t.  Reads max(NC_HDR_MIN_SIZE, header_size)
+ * bytes of `header`. */
 uint32_t nc_header_crc(const void *header);
-/* Write side: header->crc := nc_header_crc(header).  -EINVAL on a bad size. */
+/* Write side: header->crc := nc_header_crc(header).  -EINVAL on a negative
+ * header_size. */
 int nc_header_seal(void *header);
 /* dm_verify_header (diskcache.c:3660-3690): 1 if the magic is V30 and the
- * stored crc matches, else 0. */
+ * stored crc matches, else 0 (also 0 for a negative header_size, the one
+ * input the reference reads past the header on). */
 int nc_header_verify(const void *header);
 
 /* dm_verify_header over a batch of in-memory (decompressed) headers on the

@@ -13,7 +13,7 @@ run() {  # name workload bench-args...
   for c in FETCH_SIZE WRITE_SIZE VALU; do
     local cs=$c
     [ $c = VALU ] && cs="SQ_ACTIVE_INST_VALU SQ_INSTS_VALU GRBM_GUI_ACTIVE"
-    timeout -s KILL 240 rocprofv3 --pmc $cs --output-format csv -d $O/pmc_${name}_$c -o pmc -- python3 bench.py "$@" --steps 4 --warmup 1 --no-cpu-baseline --parity-sample 0 > $O/pmc_${name}_$c.log 2>&1 || { echo "pmc $name $c failed"; return 1; }
+    timeout -s KILL 240 rocprofv3 --pmc $cs --output-format csv -d $O/pmc_${name}_$c -o pmc -- python3 bench.py "$@" --steps 4 --warmup 1 --no-cpu-baseline --parity-sample 0 --extras none > $O/pmc_${name}_$c.log 2>&1 || { echo "pmc $name $c failed"; return 1; }
   done
   python3 scripts/traffic_json.py $O/pmc_${name}_FETCH_SIZE $O/pmc_${name}_WRITE_SIZE $wl --valu $O/pmc_${name}_VALU --out $O/traffic.json --source "$(basename $O): bench.py $*" > /dev/null || return 1
   echo "pmc $name ok"

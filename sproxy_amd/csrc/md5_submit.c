@@ -1905,20 +1905,44 @@ int md5_batch_submit_device(md5hip_batcher *b, const uint64_t *d_ptrs, const uin
     return submit(b, &src, n, digests, digests_on_device != 0, 0, NULL, -1, 0, NULL);
 }
 
-/* Is [p, p + len) page-locked host memory the DMA engine can read in place
- * (hipHostMalloc'd, hipHostRegister'ed, or registered here)? */
-static int host_pinned(const void *p, uint64_t len)
+/* Is the byte at p page-locked host memory known to the runtime? */
+static int pinned_at(const void *p)
 {
-    pthread_rwlock_rdlock(&g_reg_lock);
-    const int reg = reg_find((uintptr_t)p, len) >= 0;
-    pthread_rwlock_unlock(&g_reg_lock);
-    if (reg) return 1;
     hipPointerAttribute_t a;
     if (hipPointerGetAttributes(&a, p) != hipSuccess) {
         (void)hipGetLastError();                  /* pageable: not an error of ours */
         return 0;
     }
     return a.type == hipMemoryTypeHost;
+}
+
+/* Is [p, p + len) page-locked host memory the DMA engine can read in place
+ * (hipHostMalloc'd, hipHostRegister'ed, or registered here)?  The whole
+ * range, not its first byte: a source that starts in a pinned block and runs
+ * on into pageable memory is staged.  Both ends must be pinned, and the
+ * runtime's allocation holding the first byte must hold the last too (HIP's
+ * RANGE_START/RANGE_SIZE attribute, else hipMemGetAddressRange); a range
+ * whose extent the runtime will not tell is staged. */
+static int host_pinned(const void *p, uint64_t len)
+{
+    if (!len) return 0;
+    pthread_rwlock_rdlock(&g_reg_lock);
+    const int reg = reg_find((uintptr_t)p, len) >= 0;
+    pthread_rwlock_unlock(&g_reg_lock);
+    if (reg) return 1;
+    const uintptr_t lo = (uintptr_t)p, hi = lo + len;      /* [lo, hi) */
+    if (!pinned_at(p) || !pinned_at((const void *)(hi - 1))) return 0;
+    void *start = NULL;
+    size_t size = 0;
+    if (hipPointerGetAttribute(&start, HIP_POINTER_ATTRIBUTE_RANGE_START_ADDR, (hipDeviceptr_t)p) == hipSuccess &&
+        hipPointerGetAttribute(&size, HIP_POINTER_ATTRIBUTE_RANGE_SIZE, (hipDeviceptr_t)p) == hipSuccess &&
+        start && size)
+        return (uintptr_t)start <= lo && hi <= (uintptr_t)start + size;
+    (void)hipGetLastError();
+    if (hipMemGetAddressRange((hipDeviceptr_t *)&start, &size, (hipDeviceptr_t)p) == hipSuccess && start && size)
+        return (uintptr_t)start <= lo && hi <= (uintptr_t)start + size;
+    (void)hipGetLastError();
+    return 0;
 }
 
 /* memcpy of `bytes` on MD5HIP_GATHER_THREADS threads (gather_range's rule:
@@ -2045,6 +2069,7 @@ static int fixed_submit(md5hip_batcher *b, int kind, uint32_t fastcrc, const voi
             const hipError_t ce = hipMemcpyAsync(sl->d_data, from, sl->fx_bytes, hipMemcpyHostToDevice, sl->stream);
             pthread_mutex_lock(&b->mu);
             sl->writers--;
+            if (!pinned) b->st.bytes_staged += sl->fx_bytes;
             if (ce != hipSuccess && !sl->err) sl->err = -EIO;
             if (ce != hipSuccess && hip_lost(hipStreamQuery(sl->stream))) batcher_fail(b);
         }

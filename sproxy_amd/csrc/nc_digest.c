@@ -113,37 +113,67 @@ static int32_t hdr_size(const void *header)
     return hs;
 }
 
+/* The pieces dm_verify_header CRCs (diskcache.c:3676-3686): the first
+ * header_size bytes of the header as it lies, except disk_header_size, flag
+ * and crc, which it zeroes first -- wherever they fall inside those bytes,
+ * since header_size has no lower bound there (a header_size of 0..19 covers
+ * only part of the 20-byte fixed part).  Fills up to 5 (pointer, length)
+ * pieces; header_size >= 0 (a negative one the reference would pass to
+ * crc32_8bytes as a huge size_t: refused by the callers). */
+static int hdr_pieces(const unsigned char *h, int32_t hs, const unsigned char **ptr, uint32_t *len)
+{
+    static const unsigned char zero[8];
+    const struct { const unsigned char *p; uint32_t off, len; } fixed[4] = {
+        {h + NC_HDR_OFF_MAGIC, NC_HDR_OFF_MAGIC, 4},
+        {zero, NC_HDR_OFF_DISK_HEADER_SIZE, 4},                /* disk_header_size := 0 */
+        {h + NC_HDR_OFF_HEADER_SIZE, NC_HDR_OFF_HEADER_SIZE, 4},
+        {zero, NC_HDR_OFF_FLAG, 8},                            /* flag, crc := 0 */
+    };
+    int k = 0;
+    for (int i = 0; i < 4; i++) {
+        if ((int64_t)hs <= fixed[i].off) break;
+        const uint32_t take = (uint32_t)hs - fixed[i].off < fixed[i].len ? (uint32_t)hs - fixed[i].off : fixed[i].len;
+        ptr[k] = fixed[i].p;
+        len[k++] = take;
+    }
+    if (hs > NC_HDR_MIN_SIZE) {
+        ptr[k] = h + NC_HDR_MIN_SIZE;
+        len[k++] = (uint32_t)hs - NC_HDR_MIN_SIZE;
+    }
+    return k;
+}
+
 uint32_t nc_header_crc(const void *header)
 {
     if (!header) return 0;
     const int32_t hs = hdr_size(header);
-    if (hs < NC_HDR_MIN_SIZE) return 0;
+    if (hs < 0) return 0;
     pthread_once(&crc_once, crc_init);
-    static const unsigned char zero[8];
-    const unsigned char *h = header;
+    const unsigned char *ptr[5];
+    uint32_t len[5];
+    const int k = hdr_pieces(header, hs, ptr, len);
     uint32_t c = 0xFFFFFFFFu;
-    c = crc_run(c, h + NC_HDR_OFF_MAGIC, 4);
-    c = crc_run(c, zero, 4);                                   /* disk_header_size */
-    c = crc_run(c, h + NC_HDR_OFF_HEADER_SIZE, 4);
-    c = crc_run(c, zero, 8);                                   /* flag, crc */
-    c = crc_run(c, h + NC_HDR_MIN_SIZE, (uint64_t)hs - NC_HDR_MIN_SIZE);
+    for (int i = 0; i < k; i++) c = crc_run(c, ptr[i], len[i]);
     return ~c;
 }
 
 int nc_header_seal(void *header)
 {
-    if (!header || hdr_size(header) < NC_HDR_MIN_SIZE) return -EINVAL;
+    if (!header || hdr_size(header) < 0) return -EINVAL;
     const uint32_t c = nc_header_crc(header);
     memcpy((unsigned char *)header + NC_HDR_OFF_CRC, &c, 4);
     return 0;
 }
 
+/* dm_check_magic (diskcache.c:594-602), and a header_size crc32_8bytes can
+ * take: the reference passes a negative one on as a huge size_t (a read far
+ * past the header), which is the only input refused here */
 static int hdr_plausible(const void *header)
 {
     uint32_t magic;
     if (!header) return 0;
     memcpy(&magic, header, 4);
-    return magic == NC_MAGIC_V30 && hdr_size(header) >= NC_HDR_MIN_SIZE;
+    return magic == NC_MAGIC_V30 && hdr_size(header) >= 0;
 }
 
 static uint32_t hdr_stored_crc(const void *header)
@@ -159,12 +189,13 @@ int nc_header_verify(const void *header)
     return nc_header_crc(header) == hdr_stored_crc(header);
 }
 
-/* Each header becomes a 5-segment chunk whose skipped fields point at zeros,
- * so the batcher's gather builds exactly the bytes the CRC is defined over. */
+/* Each header becomes a chunk of up to 5 segments whose skipped fields point
+ * at zeros (hdr_pieces), so the batcher's gather builds exactly the bytes
+ * dm_verify_header's CRC is defined over -- none at all for header_size 0
+ * (CRC 0, as crc32_8bytes of nothing). */
 int md5hip_batch_verify_headers(md5hip_batcher *b, const void *const *headers, uint64_t n,
                                 unsigned char *ok)
 {
-    static const unsigned char zero[8];
     if (!b) return -EINVAL;
     if (n == 0) return 0;
     if (!headers || !ok) return -EINVAL;
@@ -179,11 +210,10 @@ int md5hip_batch_verify_headers(md5hip_batcher *b, const void *const *headers, u
     for (uint64_t i = 0; i < n; i++) {
         const unsigned char *h = headers[i];
         if (hdr_plausible(h)) {
-            segs[s++] = (struct md5hip_iov){h + NC_HDR_OFF_MAGIC, 4};
-            segs[s++] = (struct md5hip_iov){zero, 4};
-            segs[s++] = (struct md5hip_iov){h + NC_HDR_OFF_HEADER_SIZE, 4};
-            segs[s++] = (struct md5hip_iov){zero, 8};
-            segs[s++] = (struct md5hip_iov){h + NC_HDR_MIN_SIZE, (uint32_t)(hdr_size(h) - NC_HDR_MIN_SIZE)};
+            const unsigned char *ptr[5];
+            uint32_t len[5];
+            const int k = hdr_pieces(h, hdr_size(h), ptr, len);
+            for (int j = 0; j < k; j++) segs[s++] = (struct md5hip_iov){ptr[j], len[j]};
             want[i] = hdr_stored_crc(h);
         } else {
             want[i] = 0;                 /* empty chunk: crc 0, forced to fail below */

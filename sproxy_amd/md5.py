@@ -568,7 +568,7 @@ class Batcher:
         batcher's device, read in place -- no per-chunk descriptor; digests in
         the batcher's kind into `out` (a device tensor, or by default a host
         array returned by .wait()); `after` as submit_device_async."""
-        stride = stride or length
+        stride = length if stride is None else stride
         if n and length > stride:
             raise ValueError("length > stride")
         if torch is not None and isinstance(base, torch.Tensor):

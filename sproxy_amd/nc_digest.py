@@ -69,19 +69,34 @@ def crc32(data) -> int:
     return lib().nc_crc32(a, memoryview(data).nbytes)
 
 
+def _hdr(header):
+    """(address, keep-alive) of a header buffer that holds every byte the C
+    entry reads: the 20-byte fixed part and header_size bytes (the C ABI,
+    like dm_verify_header, takes no buffer size)."""
+    nb = memoryview(header).nbytes
+    if nb < HDR_MIN_SIZE:
+        raise ValueError(f"header buffer of {nb} B: the fixed part is {HDR_MIN_SIZE} B")
+    hs = int.from_bytes(bytes(memoryview(header).cast("B")[8:12]), "little", signed=True)
+    if hs > nb:
+        raise ValueError(f"header_size {hs} exceeds the {nb}-B buffer")
+    return _addr(header)
+
+
 def header_crc(header) -> int:
-    a, keep = _addr(header)
+    """dm_verify_header's CRC: header_size bytes, disk_header_size / flag /
+    crc read as zero wherever they fall inside them (0 for header_size < 0)."""
+    a, keep = _hdr(header)
     return lib().nc_header_crc(a)
 
 
 def header_seal(header: bytearray) -> None:
     """Write side (diskcache.c:1391-1393): header.crc := header_crc(header), in place."""
-    a, keep = _addr(header)
+    a, keep = _hdr(header)
     check("nc_header_seal", lib().nc_header_seal(a))
 
 
 def header_verify(header) -> bool:
-    a, keep = _addr(header)
+    a, keep = _hdr(header)
     return lib().nc_header_verify(a) == 1
 
 
@@ -90,7 +105,7 @@ def verify_headers(batcher, headers):
     n = len(headers)
     keep, ptrs = [], (ctypes.c_void_p * max(n, 1))()
     for i, h in enumerate(headers):
-        a, k = _addr(h)
+        a, k = _hdr(h)
         keep.append(k)
         ptrs[i] = a
     ok = np.empty(max(n, 1), np.uint8)

@@ -66,6 +66,11 @@ extern int fake_hip_hold, fake_hip_slow_query;
 void fake_hip_mark_thread(void);
 void fake_hip_lose_device(int dev, int after_kernels, int how);
 int fake_hip_device_faulted(int dev);
+void fake_hip_pin(const void *p, size_t len);
+void fake_hip_unpin(const void *p);
+void fake_hip_watch(const void *p, size_t len);
+extern unsigned long fake_hip_pageable_dma, fake_hip_watched_h2d;
+extern int fake_hip_no_range;
 static int g_stop;
 #define STOPPED() __atomic_load_n(&g_stop, __ATOMIC_RELAXED)
 #define STOP() __atomic_store_n(&g_stop, 1, __ATOMIC_RELAXED)
@@ -218,24 +223,28 @@ static void *worker(void *arg)
         }
         case 9: {
             /* netcache headers on the MD5 batcher (a CRC-32 call that must
-             * leave the shared batcher's kind alone); every 3rd one broken */
+             * leave the shared batcher's kind alone); every 4th a header_size
+             * of 0..19 (dm_verify_header's partial fixed part), every 3rd
+             * of the others broken */
             enum { NH = 24 };
             unsigned char hb[NH][256];
             const void *hp[NH];
-            unsigned char ok[NH];
+            unsigned char ok[NH], want[NH];
             int bad = 0;
             for (int i = 0; i < NH; i++) {
-                const uint32_t hs = 20 + (uint32_t)(rnd(&s) % 236), magic = NC_MAGIC_V30;
+                const uint32_t hs = i % 4 == 3 ? (uint32_t)(rnd(&s) % 20) : 20 + (uint32_t)(rnd(&s) % 236),
+                               magic = NC_MAGIC_V30;
                 for (int k = 0; k < 256; k++) hb[i][k] = (unsigned char)rnd(&s);
                 memcpy(hb[i] + NC_HDR_OFF_MAGIC, &magic, 4);
                 memcpy(hb[i] + NC_HDR_OFF_HEADER_SIZE, &hs, 4);
                 if (nc_header_seal(hb[i])) { rc = -1; break; }
-                if (i % 3 == 2) hb[i][hs - 1] ^= 0x40, bad++;
+                want[i] = 1;
+                if (i % 3 == 2 && hs >= 20) hb[i][hs - 1] ^= 0x40, bad++, want[i] = 0;
                 hp[i] = hb[i];
             }
             if (!rc) rc = md5hip_batch_verify_headers(g_b, hp, NH, ok);
             for (int i = 0; i < NH && rc == bad; i++)
-                if (ok[i] != (i % 3 != 2)) rc = -3000 - i;
+                if (ok[i] != want[i] || nc_header_verify(hb[i]) != want[i]) rc = -3000 - i;
             if (rc != bad) fail("verify_headers", t, rc);
             rc = 0;
             break;
@@ -863,6 +872,66 @@ static int fragmented(void)
     return 0;
 }
 
+/* md5hip_batch_host_fixed's in-place DMA is for a source the runtime pins
+ * over its whole range (host_pinned): a buffer whose first half only is
+ * page-locked, one made of two adjacent page-locked blocks, and a pinned one
+ * whose extent the runtime will not tell are all staged -- no H2D copy reads
+ * past a page-locked range (fake_hip_pageable_dma) -- and a wholly pinned
+ * one is read in place; every digest right, n not a multiple of the slot's
+ * chunk count. */
+static int partly_pinned(void)
+{
+    enum { L = 4096, N = 77, PER = (1u << 18) / L };   /* 64 chunks a slot: one full, one of 13 */
+    unsigned char *buf = malloc((size_t)N * L);
+    static unsigned char want[N][16], got[N][16];
+    uint64_t s = 0xFEED;
+    for (size_t k = 0; k < (size_t)N * L; k++) buf[k] = (unsigned char)(rnd(&s) >> 13);
+    for (int i = 0; i < N; i++) {
+        struct MD5Context c;
+        MD5Init(&c);
+        MD5Update(&c, buf + (size_t)i * L, L);
+        MD5Final(want[i], &c);
+    }
+    md5hip_batcher *b = NULL;
+    int rc = md5hip_batcher_create(0, (uint64_t)PER * L, 2, &b);
+    if (rc) { printf("FAIL partly pinned batcher %d\n", rc); free(buf); return 1; }
+    fake_hip_watch(buf, (size_t)N * L);
+    const char *what[5] = {"first half pinned", "two adjacent pinned blocks", "extent unknown",
+                           "wholly pinned", "pageable"};
+    int bad = 0;
+    for (int c = 0; c < 5 && !bad; c++) {
+        const size_t half = (size_t)N * L / 2, all = (size_t)N * L;
+        if (c == 0) fake_hip_pin(buf, half);
+        if (c == 1) fake_hip_pin(buf + half, all - half);      /* beside case 0's block */
+        if (c == 2) {
+            fake_hip_unpin(buf);
+            fake_hip_unpin(buf + half);
+            fake_hip_pin(buf, all);
+            __atomic_store_n(&fake_hip_no_range, 1, __ATOMIC_RELAXED);
+        }
+        if (c == 3) __atomic_store_n(&fake_hip_no_range, 0, __ATOMIC_RELAXED);
+        if (c == 4) fake_hip_unpin(buf);
+        const unsigned long before = __atomic_load_n(&fake_hip_pageable_dma, __ATOMIC_RELAXED),
+                            in0 = __atomic_load_n(&fake_hip_watched_h2d, __ATOMIC_RELAXED);
+        memset(got, 0, sizeof got);
+        rc = md5hip_batch_host_fixed(b, buf, N, L, L, &got[0][0]);
+        const unsigned long dma = __atomic_load_n(&fake_hip_pageable_dma, __ATOMIC_RELAXED) - before,
+                            inplace = __atomic_load_n(&fake_hip_watched_h2d, __ATOMIC_RELAXED) - in0;
+        /* in place: one H2D per slot (2) straight from buf; staged: none */
+        if (rc || memcmp(got, want, sizeof want) || dma || inplace != (c == 3 ? 2u : 0u)) {
+            printf("FAIL host_fixed, %s: rc %d, digests %s, %lu H2D copies read past a page-locked range, "
+                   "%lu read buf in place\n",
+                   what[c], rc, memcmp(got, want, sizeof want) ? "wrong" : "ok", dma, inplace);
+            bad = 1;
+        }
+    }
+    fake_hip_watch(NULL, 0);
+    md5hip_batcher_destroy(b);
+    free(buf);
+    if (!bad) printf("host_fixed: partly pinned, split, extent-unknown and pageable sources staged, pinned read in place, digests ok\n");
+    return bad;
+}
+
 /* a hang is a failure, not a stuck test */
 static void *watchdog(void *arg)
 {
@@ -952,6 +1021,7 @@ int main(int argc, char **argv)
         }
     }
     if (fragmented()) return 1;
+    if (partly_pinned()) return 1;
     const int devs[3] = {0, 1, 2};
     if ((rc = md5hip_pool_create(devs, 3, 1u << 20, 2, &g_pool))) { printf("FAIL pool %d\n", rc); return 1; }
     enum { T = 10 };

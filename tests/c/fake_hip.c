@@ -134,15 +134,123 @@ hipError_t hipGetDevice(int *deviceId) { *deviceId = t_device; return hipSuccess
 hipError_t hipSetDevice(int deviceId) { if (deviceId < 0 || deviceId > 7) return hipErrorInvalidDevice; t_device = deviceId; return hipSuccess; }
 hipError_t hipGetDeviceCount(int *count) { *count = 8; return hipSuccess; }
 
+/* page-locked host ranges the "runtime" knows (hipHostMalloc, hipHostRegister):
+ * what hipPointerGetAttributes / the RANGE attributes / hipMemGetAddressRange
+ * answer from.  An H2D copy whose source overlaps a watched range
+ * (fake_hip_watch) but is not wholly inside one page-locked range is DMA
+ * from pageable memory, counted in fake_hip_pageable_dma (every H2D copy
+ * from the watched range: fake_hip_watched_h2d). */
+#define NPIN 256
+static pthread_mutex_t g_pin_mu = PTHREAD_MUTEX_INITIALIZER;
+static uintptr_t g_pin_lo[NPIN], g_pin_hi[NPIN];
+static uintptr_t g_watch_lo, g_watch_hi;
+unsigned long fake_hip_pageable_dma, fake_hip_watched_h2d;
+
+static void pin_add(const void *p, size_t len)
+{
+    pthread_mutex_lock(&g_pin_mu);
+    for (int i = 0; i < NPIN; i++)
+        if (!g_pin_hi[i]) {
+            g_pin_lo[i] = (uintptr_t)p;
+            g_pin_hi[i] = (uintptr_t)p + (len ? len : 1);
+            break;
+        }
+    pthread_mutex_unlock(&g_pin_mu);
+}
+
+static void pin_del(const void *p)
+{
+    pthread_mutex_lock(&g_pin_mu);
+    for (int i = 0; i < NPIN; i++)
+        if (g_pin_hi[i] && g_pin_lo[i] == (uintptr_t)p) g_pin_lo[i] = g_pin_hi[i] = 0;
+    pthread_mutex_unlock(&g_pin_mu);
+}
+
+/* the page-locked range holding p: its index, or -1 */
+static int pin_find(uintptr_t p)
+{
+    for (int i = 0; i < NPIN; i++)
+        if (g_pin_hi[i] && g_pin_lo[i] <= p && p < g_pin_hi[i]) return i;
+    return -1;
+}
+
+/* test controls: a page-locked range with no allocation of its own (a block
+ * pinned by someone else), and the range whose H2D copies are checked */
+void fake_hip_pin(const void *p, size_t len) { pin_add(p, len); }
+void fake_hip_unpin(const void *p) { pin_del(p); }
+void fake_hip_watch(const void *p, size_t len)
+{
+    pthread_mutex_lock(&g_pin_mu);
+    g_watch_lo = (uintptr_t)p;
+    g_watch_hi = (uintptr_t)p + len;
+    pthread_mutex_unlock(&g_pin_mu);
+}
+
+static void h2d_check(const void *src, size_t len)
+{
+    const uintptr_t lo = (uintptr_t)src, hi = lo + len;
+    pthread_mutex_lock(&g_pin_mu);
+    if (len && lo < g_watch_hi && g_watch_lo < hi) {
+        fake_hip_watched_h2d++;
+        const int i = pin_find(lo);
+        if (i < 0 || hi > g_pin_hi[i]) fake_hip_pageable_dma++;
+    }
+    pthread_mutex_unlock(&g_pin_mu);
+}
+
 hipError_t hipMalloc(void **ptr, size_t size) { *ptr = malloc(size ? size : 1); return *ptr ? hipSuccess : hipErrorOutOfMemory; }
-hipError_t hipHostMalloc(void **ptr, size_t size, unsigned int flags) { (void)flags; return hipMalloc(ptr, size); }
+hipError_t hipHostMalloc(void **ptr, size_t size, unsigned int flags)
+{
+    (void)flags;
+    const hipError_t e = hipMalloc(ptr, size);
+    if (e == hipSuccess) pin_add(*ptr, size);
+    return e;
+}
 hipError_t hipFree(void *ptr) { free(ptr); return hipSuccess; }
-hipError_t hipHostFree(void *ptr) { free(ptr); return hipSuccess; }
-hipError_t hipHostRegister(void *hostPtr, size_t sizeBytes, unsigned int flags) { (void)hostPtr; (void)sizeBytes; (void)flags; return hipSuccess; }
-hipError_t hipHostUnregister(void *hostPtr) { (void)hostPtr; return hipSuccess; }
+hipError_t hipHostFree(void *ptr) { pin_del(ptr); free(ptr); return hipSuccess; }
+hipError_t hipHostRegister(void *hostPtr, size_t sizeBytes, unsigned int flags) { (void)flags; pin_add(hostPtr, sizeBytes); return hipSuccess; }
+hipError_t hipHostUnregister(void *hostPtr) { pin_del(hostPtr); return hipSuccess; }
 hipError_t hipHostGetDevicePointer(void **devPtr, void *hstPtr, unsigned int flags) { (void)flags; *devPtr = hstPtr; return hipSuccess; }
-/* every host pointer looks pageable (host_fixed then stages through pinned) */
-hipError_t hipPointerGetAttributes(hipPointerAttribute_t *attributes, const void *ptr) { (void)attributes; (void)ptr; return hipErrorInvalidValue; }
+/* page-locked memory answers hipMemoryTypeHost; any other pointer is unknown
+ * to the runtime (pageable malloc memory: hipErrorInvalidValue) */
+hipError_t hipPointerGetAttributes(hipPointerAttribute_t *attributes, const void *ptr)
+{
+    pthread_mutex_lock(&g_pin_mu);
+    const int i = pin_find((uintptr_t)ptr);
+    pthread_mutex_unlock(&g_pin_mu);
+    if (i < 0) return hipErrorInvalidValue;
+    memset(attributes, 0, sizeof *attributes);
+    attributes->type = hipMemoryTypeHost;
+    attributes->hostPointer = (void *)ptr;
+    attributes->devicePointer = (void *)ptr;
+    return hipSuccess;
+}
+/* extent of the page-locked allocation holding ptr; fake_hip_no_range: the
+ * runtime will not say (the batcher then stages) */
+int fake_hip_no_range;
+hipError_t hipPointerGetAttribute(void *data, hipPointer_attribute attribute, hipDeviceptr_t ptr)
+{
+    pthread_mutex_lock(&g_pin_mu);
+    const int i = pin_find((uintptr_t)ptr);
+    const uintptr_t lo = i < 0 ? 0 : g_pin_lo[i], hi = i < 0 ? 0 : g_pin_hi[i];
+    pthread_mutex_unlock(&g_pin_mu);
+    if (i < 0 || __atomic_load_n(&fake_hip_no_range, __ATOMIC_RELAXED)) return hipErrorInvalidValue;
+    if (attribute == HIP_POINTER_ATTRIBUTE_RANGE_START_ADDR) *(void **)data = (void *)lo;
+    else if (attribute == HIP_POINTER_ATTRIBUTE_RANGE_SIZE) *(size_t *)data = hi - lo;
+    else return hipErrorInvalidValue;
+    return hipSuccess;
+}
+hipError_t hipMemGetAddressRange(hipDeviceptr_t *pbase, size_t *psize, hipDeviceptr_t dptr)
+{
+    pthread_mutex_lock(&g_pin_mu);
+    const int i = pin_find((uintptr_t)dptr);
+    const uintptr_t lo = i < 0 ? 0 : g_pin_lo[i], hi = i < 0 ? 0 : g_pin_hi[i];
+    pthread_mutex_unlock(&g_pin_mu);
+    if (i < 0 || __atomic_load_n(&fake_hip_no_range, __ATOMIC_RELAXED)) return hipErrorInvalidValue;
+    *pbase = (hipDeviceptr_t)lo;
+    *psize = hi - lo;
+    return hipSuccess;
+}
 hipError_t hipGetLastError(void) { return hipSuccess; }
 
 hipError_t hipStreamCreateWithFlags(hipStream_t *stream, unsigned int flags)
@@ -234,10 +342,10 @@ hipError_t hipEventSynchronize(hipEvent_t event)
 
 hipError_t hipMemcpyAsync(void *dst, const void *src, size_t sizeBytes, hipMemcpyKind kind, hipStream_t stream)
 {
-    (void)kind;
     on_stream(stream);
     const hipError_t e = enqueue_ok(stream);
     if (e != hipSuccess) return e;
+    if (kind == hipMemcpyHostToDevice) h2d_check(src, sizeBytes);
     if (sizeBytes) memmove(dst, src, sizeBytes);
     return hipSuccess;
 }

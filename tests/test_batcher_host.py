@@ -23,7 +23,10 @@ every device failed, and 8 threads keep getting correct digests while a
 device dies under them.  Then large device-resident vectors (md5_submit.c
 reserve_device), three coalesced in one slot with their device digests
 scattered in pieces; the fake planner rejects a histogram that misses a
-chunk.  Runs under ASan+UBSan and under ThreadSanitizer
+chunk.  Then host_fixed over a source pinned only in part (first half,
+two adjacent pinned blocks, an extent the runtime will not tell): staged,
+never DMA'd from past a page-locked range; wholly pinned: read in place.
+Runs under ASan+UBSan and under ThreadSanitizer
 (which found the unlocked gather-mode read in submit(), now atomic)."""
 import os
 import shutil
@@ -55,6 +58,7 @@ def _build_and_run(name, san, env_extra, secs):
     assert "blocked callers: 12 rounds x 64 waiters on one slot ok" in out.stdout
     assert "large device submissions ok" in out.stdout
     assert "device lost: -EIO / -ENODEV / failover ok" in out.stdout
+    assert "host_fixed: partly pinned, split, extent-unknown and pageable sources staged" in out.stdout
 
 
 def test_batcher_under_asan():

@@ -42,12 +42,12 @@ def test_fixed_golden_batches(golden, cuda, variant):
 def test_fixed_edge_lengths(golden, cuda, variant):
     """Every golden edge length as a fixed-length batch of the same message
     repeated at a 16-B-aligned stride (ragged tails, 55/56/63/64-byte
-    padding boundaries, 1 MiB)."""
+    padding boundaries, 1 MiB -- every variant, the product C2 kernel
+    xdma1nt included)."""
     e = golden["edge"]
     big = np.frombuffer(gen.mul_pattern(max(e["lengths"])), dtype=np.uint8)
+    assert max(e["lengths"]) >= 1 << 20
     for L, want in zip(e["lengths"], e["md5"]):
-        if L > (1 << 18) and variant != "direct2":
-            continue
         stride = max(16, (L + 15) // 16 * 16)
         n = 130                                  # > 2 waves, ragged last wave
         host = np.zeros(n * stride, dtype=np.uint8)

@@ -1,5 +1,6 @@
-"""N>1 path on CPU: world_size-2 gloo groups exercise the same sharding and
-timing aggregation bench.py uses under RCCL (sproxy_amd/shard.py)."""
+"""N>1 path on CPU: world_size-2 gloo groups run the control plane bench.py
+itself runs (sproxy_amd/shard.py: init_group, barrier, MAX/SUM, object
+gathers, close_group) and its sharding."""
 import os
 import socket
 import time
@@ -8,7 +9,8 @@ import numpy as np
 import torch.multiprocessing as mp
 
 import gen
-from sproxy_amd.shard import aggregate_rate, barrier, max_over_ranks, shard_range
+from sproxy_amd.shard import (aggregate_rate, barrier, close_group, gather_objects, group_on, init_group,
+                              max_over_ranks, shard_range)
 
 
 def _free_port():
@@ -20,9 +22,9 @@ def _free_port():
 
 
 def _worker(rank, world, port, q):
-    import torch.distributed as dist
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    assert init_group(world, "gloo") and group_on()
     try:
         # 1. each rank digests its shard of a fixed-length batch with the oracle
         n, L = 37, 1000
@@ -30,15 +32,16 @@ def _worker(rank, world, port, q):
         lo, hi = shard_range(n, rank, world)
         dig = gen.oracle_digests_fixed(buf[lo * L:hi * L], hi - lo, L)
         # 2. timing: ranks take different times; the job time is the max
-        barrier(world)
+        barrier()
         t0 = time.perf_counter()
         time.sleep(0.05 * (rank + 1))
         dt = time.perf_counter() - t0
-        barrier(world)
-        agg = aggregate_rate((hi - lo) * L, dt, world)
-        q.put((rank, lo, hi, dig.tobytes(), dt, max_over_ranks(dt, world), agg))
+        barrier()
+        agg = aggregate_rate((hi - lo) * L, dt)
+        seen = gather_objects({"rank": rank, "lo": lo})           # bench.py's per-rank line
+        q.put((rank, lo, hi, dig.tobytes(), dt, max_over_ranks(dt), agg, seen))
     finally:
-        dist.destroy_process_group()
+        close_group()
 
 
 def test_shard_range_partitions():
@@ -73,5 +76,16 @@ def test_gloo_world2_shards_and_max_time():
         agg = r[6]
         assert agg["total_bytes"] == n * L
         assert abs(agg["bytes_per_s"] - n * L / tmax) < 1e-6 * n * L / tmax
+        assert r[7] == [{"rank": 0, "lo": 0}, {"rank": 1, "lo": 18}]   # rank order, every rank
     assert tmax >= 0.1 - 1e-3
     np.testing.assert_array_less(0, [r[4] for r in res])
+
+
+def test_no_group_is_one_rank():
+    """Without a group (one rank, no --dist-always) every call is local."""
+    assert not init_group(1, "gloo")
+    assert not group_on()
+    barrier()
+    assert max_over_ranks(2.5) == 2.5 and gather_objects("x") == ["x"]
+    assert aggregate_rate(10, 2.0)["bytes_per_s"] == 5.0
+    close_group()

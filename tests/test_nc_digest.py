@@ -57,30 +57,78 @@ def test_header_verify_rules():
     g[4:8] = struct.pack("<i", 12345)                         # disk_header_size: ignored
     g[12:16] = struct.pack("<I", 0x10000000)                  # flag (COMPRESSED): ignored
     assert nd.header_verify(g)
-    for pos in (0, 9, 20, len(h) - 1):                        # anything else is covered
+    for pos in (0, 20, len(h) - 1):                           # anything else is covered
         g = bytearray(h)
         g[pos] ^= 0x40
         assert not nd.header_verify(g), pos
+    g = bytearray(h)
+    struct.pack_into("<i", g, 8, len(h) - 1)                  # header_size covered too
+    assert not nd.header_verify(g)
+    g[9] ^= 0x40                                              # a size past the buffer: refused
+    with pytest.raises(ValueError):                           # before C reads past it
+        nd.header_verify(g)
     g = bytearray(h)
     g[16] ^= 1                                                # stored crc itself
     assert not nd.header_verify(g)
     assert nd.header_crc(bytearray(h) + b"trailing") == nd.header_crc(h)   # only header_size bytes
 
 
-def test_header_size_below_fixed_part_is_a_deliberate_divergence():
-    """DELIBERATE DIVERGENCE from the reference (DESIGN.md
-    §9): dm_verify_header (diskcache.c:3676-3689) CRCs header_size bytes with
-    no lower bound -- for 0 <= header_size < 20 a CRC over only part of the
-    fixed header (the zeroed crc / disk_header_size / flag fields partly
-    outside it), and for a negative header_size a length the reference never
-    guards.  Here a header whose header_size is below the 20-byte fixed part
-    (or negative) is rejected: header_verify false, header_crc 0, seal
-    -EINVAL.  Not parity: a corrupt size field is refused, not hashed."""
-    h, _ = _golden_headers()[3]
-    for hs in (19, 4, 0, -1, -(1 << 31)):
-        g = bytearray(h)
-        g[8:12] = struct.pack("<i", hs)
+def _small_header(hs, seed=5):
+    """A V30 header whose header_size field reads hs, with random other
+    fields and a body after the fixed part."""
+    rng = np.random.default_rng(seed + (hs & 0xFFFF))
+    return bytearray(struct.pack("<IiiII", nd.NC_MAGIC_V30, int(rng.integers(0, 1 << 30)), hs,
+                                 int(rng.integers(0, 2)) << 28, int(rng.integers(0, 1 << 32)))
+                     + gen.xorshift_bytes(64, seed=seed))
+
+
+def test_header_size_below_fixed_part_follows_the_reference():
+    """dm_verify_header (diskcache.c:3676-3686) CRCs header_size bytes with no
+    lower bound: for 0 <= header_size < 20 the CRC covers only the first
+    header_size bytes of the fixed part, with disk_header_size, flag and crc
+    zeroed wherever they fall inside them (header_size 0: crc32_8bytes of
+    nothing, 0 -- so a header with a zero crc field verifies).  The CRC of
+    those bytes is the oracle's (pinned to crc32.c); the zeroing rule itself
+    is restated from diskcache.c, which cannot be built here (it needs
+    autoconf's generated config.h): parity unpinned for that rule.  Only a
+    negative header_size is refused -- the reference would hand it to
+    crc32_8bytes as a huge size_t and read far past the header."""
+    for hs in (19, 18, 17, 16, 13, 12, 11, 9, 8, 5, 4, 3, 1, 0):
+        g = _small_header(hs)
+        z = bytearray(g[:20])
+        z[4:8] = bytes(4)
+        z[12:20] = bytes(8)
+        want = _oracle_crc(bytes(z[:hs]))
+        assert nd.header_crc(g) == want, hs
+        assert nd.header_verify(g) == (want == struct.unpack_from("<I", g, 16)[0]), hs
+        nd.header_seal(g)
+        assert struct.unpack_from("<I", g, 16)[0] == want and nd.header_verify(g), hs
+        g[24] ^= 0x55                                          # past header_size: not covered
+        assert nd.header_verify(g), hs
+        for pos in (0, 3):                                     # magic: dm_check_magic fails first
+            b = bytearray(g)
+            b[pos] ^= 0x01
+            assert not nd.header_verify(b), (hs, pos)
+        if hs > 8:                                             # header_size's own bytes are covered
+            b = bytearray(g)
+            b[8] ^= 0x01                                       # hs +- 1: other bytes, other CRC
+            assert not nd.header_verify(b), hs
+        for pos in [p for p in (4, 7, 12, 15) if p < 20]:      # zeroed fields: never covered
+            b = bytearray(g)
+            b[pos] ^= 0x80
+            assert nd.header_verify(b), (hs, pos)
+    z = _small_header(0)
+    z[16:20] = bytes(4)
+    assert nd.header_crc(z) == 0 and nd.header_verify(z)        # crc field 0 == CRC of nothing
+    for hs in (-1, -20, -(1 << 31)):
+        g = _small_header(hs)
         assert not nd.header_verify(g) and nd.header_crc(g) == 0, hs
+        with pytest.raises(m.MD5HipError):
+            nd.header_seal(g)
+    with pytest.raises(ValueError):
+        nd.header_verify(bytes(19))                            # the fixed part is 20 B
+    with pytest.raises(ValueError):
+        nd.header_verify(_small_header(200))                   # header_size past the buffer
 
 
 def test_host_crc32_matches_reference_vectors():
@@ -130,7 +178,8 @@ def test_digest_array_batched():
 def test_gpu_batch_verify_headers(cuda):
     """dm_verify_header for a batch of headers through a batcher (CRC-32 over
     the gathered, field-zeroed header bytes on the GPU), with corrupted,
-    wrong-magic and undersized headers mixed in; the batcher keeps its mode."""
+    wrong-magic, negative-size and 0..20-byte header_size headers (the
+    reference's partial-fixed-part rule) mixed in; the batcher keeps its mode."""
     rng = np.random.default_rng(8)
     heads = [bytearray(h) for h, _ in _golden_headers()]
     for k in range(300):
@@ -144,7 +193,14 @@ def test_gpu_batch_verify_headers(cuda):
     for i in (9, 40, 77):
         heads[i][int(rng.integers(20, len(heads[i])))] ^= 0x01; want[i] = False
     heads[100][0] ^= 0xFF; want[100] = False                # bad magic
-    heads[150][8:12] = struct.pack("<i", 3); want[150] = False
+    heads[150][8:12] = struct.pack("<i", 3); want[150] = False   # CRC of 3 bytes != the stored one
+    for hs in (0, 1, 4, 5, 12, 13, 19, 20):                 # the reference's small-size rule, sealed
+        h = _small_header(hs, seed=9)
+        nd.header_seal(h)
+        h[4:8] = struct.pack("<i", 77)
+        heads.append(h)
+        want = np.append(want, True)
+    heads.append(_small_header(-5)); want = np.append(want, False)
     assert [nd.header_verify(h) for h in heads] == want.tolist()
     with m.Batcher(device=0, slice_bytes=2 << 20, nslots=3) as b:
         ok, nbad = nd.verify_headers(b, heads)

@@ -1,7 +1,8 @@
 """The multi-GPU pool as a router over per-device coalescing batchers
-(md5_pool.c, include/md5hip.h md5hip_pool_*), on the box's one device listed
-several times (each entry is its own batcher, so routing, split tickets and
-digest placement are exercised as on an 8-GPU node).
+(md5_pool.c, include/md5hip.h md5hip_pool_*).  On a node with more than one
+GPU every pool spans distinct devices (all of them for the 8-thread router
+test); on a one-GPU box the device is listed several times (each entry is its
+own batcher, so routing, split tickets and digest placement still run).
 
 The reference calls its block checksum from every ASIO thread at once
 (asio_mgr.c:205, :1050-1057) with one vector of blocks each: here 8 threads
@@ -21,6 +22,15 @@ import sproxy_amd.md5 as m
 pytestmark = pytest.mark.gpu
 
 MT_BIT = 1 << 63
+
+
+def _devs(k=None):
+    """k pool entries: distinct devices when more than one is visible (every
+    device for k None), else device 0 listed k times (4 for k None)."""
+    ndev = torch.cuda.device_count()
+    if ndev > 1:
+        return tuple(range(ndev)) if k is None else tuple(g % ndev for g in range(k))
+    return (0,) * (4 if k is None else k)
 
 
 def _vectors(k, seed):
@@ -44,7 +54,8 @@ def _bufs(lens, seed):
 
 
 def test_pool_router_eight_threads(cuda):
-    """8 threads x 6 async vectors each through a pool over (0,0,0,0), the
+    """8 threads x 6 async vectors each through a pool over every device (or
+    (0,0,0,0) on one GPU), the
     blocks in a registered page heap (zero-copy, as INTEGRATION.md asks of
     netcache): every ticket equals the oracle, every vector went whole to one
     device, every device took work, and vectors arriving while launches run
@@ -70,7 +81,8 @@ def test_pool_router_eight_threads(cuda):
     errors, results = [], {}
     m.register_host(heap)
     try:
-        with m.Pool((0, 0, 0, 0)) as p:
+        devs = _devs()
+        with m.Pool(devs) as p:
             start = threading.Barrier(8)
 
             def worker(t):
@@ -93,7 +105,7 @@ def test_pool_router_eight_threads(cuda):
                 assert np.array_equal(results[j], data[j][1]), j
             st = p.stats()
             assert st["submissions"] == 48 and st["routed_whole"] == 48 and st["split"] == 0
-            dev = [p.device_stats(g) for g in range(4)]
+            dev = [p.device_stats(g) for g in range(len(devs))]
             assert sum(d["submissions"] for d in dev) == 48
             assert all(d["submissions"] > 0 for d in dev), dev        # load spread
             assert sum(d["launches"] for d in dev) < 48, dev          # vectors coalesced
@@ -103,7 +115,7 @@ def test_pool_router_eight_threads(cuda):
     # netcache-sized vectors of 16 KiB blocks from pageable memory (host
     # gather): correct, and whole
     small = [_bufs(lens, 600 + j) for j, lens in enumerate(_vectors(8, seed=303))]
-    with m.Pool((0, 0)) as p:
+    with m.Pool(_devs(2)) as p:
         pend = [p.submit_async(d[0]) for d in small]
         for d, pn in zip(small, pend):
             assert np.array_equal(pn.wait(), d[1])
@@ -116,7 +128,7 @@ def test_pool_sync_submit_from_threads(cuda):
     vecs = _vectors(16, seed=311)
     data = [_bufs(lens, 500 + j) for j, lens in enumerate(vecs)]
     got, errors = {}, []
-    with m.Pool((0, 0)) as p:
+    with m.Pool(_devs(2)) as p:
         def worker(t):
             try:
                 for j in range(t, 16, 4):
@@ -140,7 +152,7 @@ def test_pool_split_tickets(cuda):
     lens = gen.mixed_lengths(600, seed=321, max_len=1 << 18) + [0, 1, 64, 16384]
     bufs, want, blob, offs = _bufs(lens, 322)
     pages = [[b[:5000], b[5000:]] for b in bufs]
-    with m.Pool((0, 0, 0), slice_bytes=8 << 20, nslots=3) as p:
+    with m.Pool(_devs(3), slice_bytes=8 << 20, nslots=3) as p:
         p.set_split(1 << 20)
         a = p.submit_async(bufs)
         b = p.submit_iov_async(pages)
@@ -165,7 +177,7 @@ def test_pool_crc32_and_verify(cuda):
     lens = gen.mixed_lengths(300, seed=331, max_len=1 << 17)
     bufs, want, blob, offs = _bufs(lens, 332)
     pages = [[b] for b in bufs]
-    with m.Pool((0, 0)) as p:
+    with m.Pool(_devs(2)) as p:
         p.set_digest(m.Pool.CRC32, 0)
         got = p.submit_async(bufs).wait()
         assert np.array_equal(got, gen.oracle_crc32_batch(blob, offs, lens, 0))
@@ -182,7 +194,7 @@ def test_pool_ticket_errors(cuda):
     import ctypes
     import errno
     from sproxy_amd._lib import lib
-    with m.Pool((0, 0)) as p:
+    with m.Pool(_devs(2)) as p:
         L = lib()
         assert L.md5hip_pool_wait(p._h, 0) == 0 and L.md5hip_pool_poll(p._h, 0) == 1
         assert L.md5hip_pool_wait(p._h, (12345 << 6) | 1) == -errno.EINVAL     # never issued
@@ -203,7 +215,7 @@ def test_pool_failed_submission_then_good_ones(cuda):
     lens = [200000] * 40
     bufs, want, blob, offs = _bufs(lens, 361)
     big = bufs[:10] + [np.zeros(3 << 20, np.uint8)] + bufs[10:20]          # 3 MiB > 2 MiB slice
-    with m.Pool((0, 0), slice_bytes=2 << 20, nslots=2) as p:
+    with m.Pool(_devs(2), slice_bytes=2 << 20, nslots=2) as p:
         for split in (0, 1 << 20):
             p.set_split(split)
             with pytest.raises(m.MD5HipError) as ei:
