@@ -83,8 +83,10 @@ def parse_args(argv):
     p.add_argument("--c3-bytes", type=int, default=16 << 30)
     p.add_argument("--c3-variant", default="plan",
                    help="descriptor kernel for C3 (plan = md5hip_plan_desc's choice)")
-    p.add_argument("--c3-coalesce", type=int, default=3,
-                   help="C3 batches planned and launched together for the coalesced rate (0/1 = off)")
+    p.add_argument("--c3-coalesce", type=int, default=0,
+                   help="C3 batches planned and launched together for the coalesced rate; 0 = sized "
+                        "by the list-scheduling rule (the fewest batches, up to 8, whose LPT makespan "
+                        "is within 5 %% of the mean SIMD load, lpt_schedule); 1 = off")
     p.add_argument("--c3-streams", type=int, default=3,
                    help="streams for C3's streamed rate (batches in flight)")
     p.add_argument("--c3-legs", default="all", choices=["all", "main", "coalesced"],
@@ -681,13 +683,47 @@ def c3_sample(lens, order, k, seed):
     return np.unique(np.concatenate([np.asarray(p, dtype=np.int64) for p in pick]))
 
 
+LPT_SIMDS, LPT_GROUP = 1024, 64      # BALANCED: one wave per SIMD, 64-chunk groups
+
+
+def lpt_schedule(lens, simds=LPT_SIMDS):
+    """The list schedule of one BALANCED launch (md5_desc_balanced_t): 64-chunk
+    groups in md5hip_plan_desc's longest-first order, taken by whichever of
+    the `simds` waves is free first; a group costs its longest chunk's
+    compressions (its lanes run in lockstep; floor((len+8)/64)+1, md5.c:221-265).
+    Returns mean load, makespan (both in compressions) and util = mean /
+    makespan, the share of SIMD-time the launch can keep busy: a 1 MiB chunk
+    is a serial chain of 16,385 compressions, so a launch with too little
+    work beside its longest chains idles SIMDs in its tail."""
+    import heapq
+    import numpy as np
+    c = np.sort((np.asarray(lens, dtype=np.int64) + 8) // 64 + 1)[::-1]
+    groups = c[::LPT_GROUP]
+    free = [0] * simds
+    for g in groups.tolist():
+        heapq.heappush(free, heapq.heappop(free) + g)
+    mean, makespan = float(groups.sum()) / simds, float(max(free))
+    return {"mean_compressions": round(mean, 1), "makespan_compressions": makespan,
+            "util": round(mean / makespan, 4), "groups": int(groups.size)}
+
+
 def c3_coalesced(a, lens, rank, world):
     """K C3 batches (the main batch's lengths + K-1 more, own bytes) planned
     and launched as one descriptor batch -- what md5hip_queue does with K
-    pending submissions (--config c3q) -- timed with HIP events."""
+    pending submissions (--config c3q) -- timed with HIP events.  K =
+    --c3-coalesce, or (0) the fewest batches whose list schedule keeps 95 %
+    of SIMD-time busy (lpt_schedule): at 3 batches the 1 MiB chains set the
+    makespan and a quarter of the SIMD-time idles in the tail."""
     import numpy as np
-    K = a.c3_coalesce
-    lk = [lens] + [c3_lens(a.c3_bytes, 2000 + 17 * j + rank) for j in range(1, K)]
+    lk = [lens]
+    if a.c3_coalesce:
+        K = a.c3_coalesce
+        lk += [c3_lens(a.c3_bytes, 2000 + 17 * j + rank) for j in range(1, K)]
+    else:
+        while len(lk) < 8 and lpt_schedule(np.concatenate(lk))["util"] < 0.95:
+            lk.append(c3_lens(a.c3_bytes, 2000 + 17 * len(lk) + rank))
+        K = len(lk)
+    lpt = lpt_schedule(np.concatenate(lk))
     ok_ = [c3_offsets(x)[0] for x in lk]
     spans = [(c3_offsets(x)[1] + 15) // 16 * 16 for x in lk]
     starts = np.concatenate([[0], np.cumsum(spans)[:-1]])
@@ -711,9 +747,12 @@ def c3_coalesced(a, lens, rank, world):
     return {"batches": K, "chunks": int(L_all.size), "payload_bytes": int(pay), "kernel": varK,
             "ms_per_launch": round(k_ms, 4), "ms_per_batch": round(k_ms / K, 4),
             "value": round(pay * world / (k_ms * 1e-3) / GIB, 2), "unit": "GiB/s",
+            "sized_by": "--c3-coalesce" if a.c3_coalesce else "lpt util >= 0.95",
+            "lpt": lpt,
             "roofline": {"bound": "hbm", "achieved": round(alg / (k_ms * 1e-3) / 1e9, 1),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(alg / (k_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                         "frac_of_lpt_ceiling": round(alg / (k_ms * 1e-3) / 1e9 / HBM_PEAK_GBS / lpt["util"], 4),
                          "traffic": traffic, "traffic_source": tnote, "valu_busy_pmc": vbusy, "kernel": "md5hip::" + kname,
                          "alg_bytes_per_launch": int(alg)},
             "parity": par,
@@ -791,7 +830,7 @@ def run_c3(a, rank, world, local, device, backend):
     del outs
     # coalesced: K such batches (own lengths, own bytes) planned and launched
     # as one descriptor batch by hand (what md5hip_queue does, --config c3q)
-    coal = c3_coalesced(a, lens, rank, world) if a.c3_coalesce > 1 else None
+    coal = c3_coalesced(a, lens, rank, world) if a.c3_coalesce != 1 else None
     # imbalance vs uniform -- the same payload bytes of the
     # same arena hashed as uniform 16 KiB chunks by the fixed-length kernel
     n_u = int(payload) // 16384

@@ -14,6 +14,7 @@ ACTIVE_INST_ANY ~ WAVE_CYCLES, disjoint):
                       ACTIVE_INST_ANY (issuing) as fractions of WAVE_CYCLES
   active_split        ACTIVE_INST_{VALU,SCA,LDS,MISC,VMEM,FLAT} / WAVE_CYCLES
   insts_per_wave      SQ_INSTS_* / SQ_WAVES
+  wave_occupancy      4 x SQ_WAVE_CYCLES / (SIMDs x GRBM_GUI_ACTIVE / 8)
 usage: pmc_stall.py --kernel balanced PASS_DIR... [--out FILE]"""
 import argparse
 import csv
@@ -47,6 +48,7 @@ def main():
     ap.add_argument("--kernel", required=True)
     ap.add_argument("dirs", nargs="+")
     ap.add_argument("--out")
+    ap.add_argument("--simds", type=int, default=1024, help="SIMDs of the device (wave_occupancy)")
     a = ap.parse_args()
     mean, n, kernels = load(a.dirs, a.kernel)
     res = {"kernel_filter": a.kernel, "kernels": kernels, "dispatches": n, "per_dispatch": mean}
@@ -63,6 +65,14 @@ def main():
         other = sum(v for k, v in mean.items() if k.startswith("SQ_INSTS_") and k != "SQ_INSTS_VALU"
                     and k not in ("SQ_INSTS_VMEM_RD", "SQ_INSTS_VMEM_WR"))   # sub-counts of VMEM
         res["non_valu_per_valu"] = round(other / mean["SQ_INSTS_VALU"], 4)
+    g = mean.get("GRBM_GUI_ACTIVE")
+    if wc and g:
+        # wave occupancy of the launch: wave lifetimes (quad-cycles x 4) over
+        # SIMDs x span (GRBM_GUI_ACTIVE is summed over the 8 XCDs).  For a
+        # persistent one-wave-per-SIMD kernel (BALANCED) this is the share of
+        # SIMD-time with a wave still holding work -- the list schedule's util.
+        res["wave_occupancy"] = round(4 * wc / (a.simds * g / 8), 4)
+        res["span_cycles"] = round(g / 8)
     txt = json.dumps(res, indent=1)
     print(txt)
     if a.out:
