@@ -109,6 +109,9 @@ def parse_args(argv):
                         "timed region and parity, as sub-records of the same line (c3q = the C3 "
                         "stream through md5hip_queue, c5 = end to end from pinned host memory); "
                         "'none' for the headline alone (profiling passes)")
+    p.add_argument("--no-board-probe", action="store_true",
+                   help="skip the C2 board probe (clock / power / PPT residency under the kernel, "
+                        "after the timed region)")
     p.add_argument("--c5-chunks", type=int, default=1 << 18)
     p.add_argument("--c5-slice", type=int, default=64 << 20)
     return p.parse_args(argv)
@@ -479,6 +482,8 @@ def run_c2(a, rank, world, local, device, backend):
                      "alg_bytes_per_launch": int(alg_bytes)},
     }
     par = sample_fixed(data, out, n, L, a.parity_sample, seed=77 + rank)
+    if world == 1 and not a.no_board_probe:
+        res["board"] = board_probe(fn, device, dev_ms_max)
     return per_rank_line(res, rank, world, local, device, backend, float(n) * L * a.steps, wall, par)
 
 
@@ -1099,6 +1104,84 @@ def run_c5(a, rank, world, local, device, backend):
                                       f"on {nsl} streams; spec {PCIE_PEAK_GBS} GB/s"),
                         "traffic": None}}
     return per_rank_line(res, rank, world, local, device, backend, n * L * a.steps, wall, par)
+
+
+def board_probe(fn, device, ms_per_launch, seconds=1.5):
+    """What the board does under the C2 kernel (the line
+    had no way to show the power cap): after the timed region, the same
+    launches again for ~`seconds` while amdsmi's gpu_metrics are sampled
+    every 10 ms -- the current gfx clock (mean over the XCDs), socket power,
+    and the share of the window the package-power limit (PPT) held the
+    clock down.  Never part of `value`; {"error": ...} where amdsmi cannot
+    read the board (a box that hides the metrics)."""
+    import statistics
+    try:
+        import amdsmi
+        amdsmi.amdsmi_init()
+    except Exception as e:  # pragma: no cover - depends on the box
+        return {"error": f"amdsmi: {e!r}"[:200]}
+    try:
+        p = torch.cuda.get_device_properties(device)
+        want = (getattr(p, "pci_domain_id", 0), getattr(p, "pci_bus_id", 0), getattr(p, "pci_device_id", 0))
+        handle = None
+        for h in amdsmi.amdsmi_get_processor_handles():
+            b = amdsmi.amdsmi_get_gpu_device_bdf(h)            # "dddd:bb:dd.f"
+            dom, bus, rest = b.split(":")
+            if (int(dom, 16), int(bus, 16), int(rest.split(".")[0], 16)) == want:
+                handle = h
+        if handle is None:
+            return {"error": f"no amdsmi device at {want}"}
+        met = lambda: amdsmi.amdsmi_get_gpu_metrics_info(handle)  # noqa: E731
+
+        def num(x):
+            return float(x) if isinstance(x, (int, float)) and x not in (0xFFFF, 0xFFFFFFFF) else None
+
+        m0 = met()
+        launches = max(10, int(seconds * 1e3 / max(ms_per_launch, 0.05)))
+        stream = torch.cuda.current_stream()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize()
+        e0.record(stream)
+        for _ in range(launches):
+            fn()
+        e1.record(stream)
+        clk, pw = [], []
+        t_end = time.perf_counter() + seconds * 3
+        while not e1.query() and time.perf_counter() < t_end:
+            mm = met()
+            cs = [num(c) for c in (mm.get("current_gfxclks") or []) if num(c)]
+            c = statistics.fmean(cs) if cs else num(mm.get("current_gfxclk"))
+            w = num(mm.get("current_socket_power")) or num(mm.get("average_socket_power"))
+            if c:
+                clk.append(c)
+            if w:
+                pw.append(w)
+            time.sleep(0.01)
+        torch.cuda.synchronize()
+        m1 = met()
+        acc0, acc1 = num(m0.get("accumulation_counter")), num(m1.get("accumulation_counter"))
+        ppt0, ppt1 = num(m0.get("ppt_residency_acc")), num(m1.get("ppt_residency_acc"))
+        ppt = (round((ppt1 - ppt0) / (acc1 - acc0), 3)
+               if None not in (acc0, acc1, ppt0, ppt1) and acc1 > acc0 else None)
+        # trim the first and last fifth of the samples (clock ramp, drain)
+        k = len(clk) // 5
+        mid = clk[k:len(clk) - k] or clk
+        kp = len(pw) // 5
+        midp = pw[kp:len(pw) - kp] or pw
+        return {"launches": launches, "ms_per_launch": round(e0.elapsed_time(e1) / launches, 4),
+                "samples": len(clk),
+                "gfxclk_mhz_median": round(statistics.median(mid), 1) if mid else None,
+                "socket_power_w_median": round(statistics.median(midp), 1) if midp else None,
+                "ppt_limited_frac": ppt,
+                "note": "the C2 launches again after the timed region; amdsmi gpu_metrics every 10 ms "
+                        "(current_gfxclks mean over XCDs, current_socket_power, ppt_residency_acc)"}
+    except Exception as e:  # pragma: no cover - depends on the box
+        return {"error": repr(e)[:200]}
+    finally:
+        try:
+            amdsmi.amdsmi_shut_down()
+        except Exception:
+            pass
 
 
 EXTRA_STEPS = {"c3q": (8, 3), "c5": (5, 2)}     # (steps, warmup) of a sub-record

@@ -168,6 +168,17 @@ def test_producer_default_without_torch(monkeypatch):
     assert m.Batcher._producer(b, 1234) == (1234, 1)
 
 
+def test_device_fixed_explicit_stride_zero_is_kept():
+    """submit_device_fixed_async(stride=0) passes stride 0 on as the C entry
+    reads it (len 0 only), instead of turning it into stride = length:
+    length 16 at stride 0 is refused before any device work."""
+    import types
+    b = types.SimpleNamespace(device=0)
+    import pytest
+    with pytest.raises(ValueError):
+        m.Batcher.submit_device_fixed_async(b, 0x1000, 4, 16, stride=0)
+
+
 def test_plan_order_longest_first():
     rng = np.random.default_rng(1)
     lens = rng.integers(0, 1 << 20, 5000).astype(np.uint32)
