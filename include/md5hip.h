@@ -30,7 +30,10 @@
 extern "C" {
 #endif
 
-/* ABI 4 (round 5): device failure -- md5hip_batcher_health /
+/* ABI 5 (round 6): md5hip_order_stable_scratch / md5hip_order_device_stable
+ * (appended; the batcher's large slots use them); md5hip_batch_host_fixed
+ * reads a source in place only if it is pinned over its whole range.
+ * ABI 4 (round 5): device failure -- md5hip_batcher_health /
  * md5hip_batcher_inject_fault, md5hip_pool_get_health / _device_health /
  * _inject_fault -- and md5_batch_submit_device_fixed (appended); md5hip_batcher_set_chain rejects modes outside
  * 0..2 with -EINVAL.
@@ -40,7 +43,7 @@ extern "C" {
  * already grown MD5HIP_DESC_NUM_VARIANTS 6 -> 7 (FED) and CRC32HIP_NUM_VARIANTS
  * 7 -> 8 (SPLIT) -- appended values, compatible -- and made the pool route a
  * submission whole (same results; set_digest no longer drains). */
-#define MD5HIP_ABI_VERSION 4
+#define MD5HIP_ABI_VERSION 5
 
 /* Fixed-length kernels for md5hip_digest_fixed_variant.  ABI 2: the round-1
  * A/B variants (values 2-9) moved to the diagnostic library (removed in round 4;
@@ -235,6 +238,19 @@ int md5hip_plan_desc_at(const uint32_t *lens, const uint64_t *addrs, uint64_t n,
 int md5hip_plan_hist(const uint32_t *hist, uint32_t kmax, uint64_t n, uint32_t *bucket_start);
 int md5hip_order_device(const uint32_t *d_lens, uint64_t n, uint32_t kmax, uint32_t *d_bucket_next,
                         uint32_t *d_order, void *stream);
+/* ABI 5: the same order, STABLE -- equal keys in chunk-index order, exactly
+ * md5hip_plan_desc's host order -- built by a device radix sort (rocPRIM)
+ * of (kmax - key, index) pairs.  The positions within a key matter after
+ * all: BALANCED over 6 coalesced C3 batches ran 5-6 % longer with
+ * md5hip_order_device's wave-arrival order; the batcher
+ * uses this one.  Device scratch of md5hip_order_stable_scratch(n, kmax)
+ * bytes (0 = unsupported n or kmax; kmax 0 sizes for any kmax up to
+ * MD5HIP_HIST_KMAX); a chunk whose key exceeds kmax goes after every
+ * bucket.  Asynchronous on `stream`; 0, -EINVAL, -ENOSPC (scratch too
+ * small), -ENODEV, -EIO. */
+uint64_t md5hip_order_stable_scratch(uint64_t n, uint32_t kmax);
+int md5hip_order_device_stable(const uint32_t *d_lens, uint64_t n, uint32_t kmax, void *d_scratch,
+                               uint64_t scratch_bytes, uint32_t *d_order, void *stream);
 
 /*
  * Synthetic-data generator for benches/tests: fills nbytes (multiple of 16)

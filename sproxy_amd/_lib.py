@@ -101,6 +101,8 @@ def lib():
         "md5hip_batcher_set_chain": (i, [vp, i]),
         "md5hip_plan_hist": (i, [vp, u32, u64, vp]),
         "md5hip_order_device": (i, [vp, u64, u32, vp, vp, vp]),
+        "md5hip_order_stable_scratch": (u64, [u64, u32]),
+        "md5hip_order_device_stable": (i, [vp, u64, u32, vp, u64, vp, vp]),
         "md5hip_batcher_get_stats": (i, [vp, ctypes.POINTER(MD5HipBatcherStats)]),
         "md5_batch_submit_device_async": (i, [vp, vp, vp, u64, vp, i, vp]),
         "md5_batch_submit_device": (i, [vp, vp, vp, u64, vp, i]),
@@ -186,6 +188,7 @@ EXPORTS = ["MD5Init", "MD5Update", "MD5Final", "nc_MD5Init", "nc_MD5Update", "nc
            "md5hip_batch_verify_headers", "md5hip_host_register", "md5hip_host_unregister",
            "md5hip_batcher_set_gather", "md5hip_pool_set_gather", "md5hip_queue_create",
            "md5hip_batcher_set_inflight", "md5hip_batcher_set_linger", "md5hip_plan_hist", "md5hip_order_device",
+           "md5hip_order_stable_scratch", "md5hip_order_device_stable",
            "md5hip_batcher_get_stats", "md5_batch_submit_device_async",
            "md5_batch_submit_device", "md5_batch_flush", "md5hip_init_ctx", "md5hip_update_ctx",
            "md5hip_final_ctx", "md5hip_pool_set_split", "md5hip_pool_submit_async",

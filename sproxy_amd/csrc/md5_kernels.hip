@@ -29,6 +29,10 @@ template __global__ void crc32_desc<true>(const uint8_t*, const uint64_t*, const
 #include <thread>
 #include <vector>
 
+#include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/iterator/counting_iterator.hpp>
+#include <rocprim/iterator/transform_iterator.hpp>
+
 #include "../../include/md5hip.h"
 #include "md5_internal.h"
 
@@ -740,6 +744,63 @@ int md5hip_order_device(const uint32_t* d_lens, uint64_t n, uint32_t kmax, uint3
   if (g > 0x7fffffffull) return -EINVAL;
   hipLaunchKernelGGL(order_scatter, dim3((uint32_t)g), dim3(256), 0, (hipStream_t)stream, d_lens, n,
                      kmax, d_next, d_order);
+  return launched();
+}
+
+// The stable longest-first order (ABI 5): rocPRIM's LSD radix sort of
+// (kmax - key, chunk index) pairs, the key computed from the length as it is
+// read (no key array), the index from a counting iterator; radix sort is
+// stable, so equal keys keep chunk-index (= address) order -- exactly
+// md5hip_plan_desc's host order.  order_scatter's wave-arrival order within a
+// key cost a 6-batch C3 BALANCED launch 5-6 % against this order
+// (profiles/r06d/, r06e/ order_ab.json).  Scratch: the sorted keys (4 n B,
+// 256-B aligned) then rocPRIM's temporary storage.
+}  // extern "C"
+
+namespace {
+struct BucketOf {
+  uint32_t kmax;
+  __host__ __device__ uint32_t operator()(uint32_t len) const {
+    const uint32_t k = (len >> 6) + 1u;
+    return k <= kmax ? kmax - k : kmax;        // a key past kmax: after every bucket
+  }
+};
+unsigned sort_bits(uint32_t kmax) { return 32u - (unsigned)__builtin_clz(kmax | 1u); }
+uint64_t keys_bytes(uint64_t n) { return (4 * n + 255) & ~255ull; }
+hipError_t order_sort(void* temp, size_t& temp_bytes, const uint32_t* d_lens, uint32_t n, uint32_t kmax,
+                      uint32_t* keys_out, uint32_t* d_order, hipStream_t s) {
+  auto keys_in = rocprim::make_transform_iterator(d_lens, BucketOf{kmax});
+  return rocprim::radix_sort_pairs(temp, temp_bytes, keys_in, keys_out, rocprim::counting_iterator<uint32_t>(0u),
+                                   d_order, n, 0u, sort_bits(kmax), s);
+}
+}  // namespace
+
+extern "C" {
+
+uint64_t md5hip_order_stable_scratch(uint64_t n, uint32_t kmax) {
+  if (n == 0) return 0;
+  if (n > 0x7fffffffull || kmax > MD5HIP_HIST_KMAX) return 0;
+  size_t temp = 0;
+  if (order_sort(nullptr, temp, nullptr, (uint32_t)n, kmax ? kmax : MD5HIP_HIST_KMAX, nullptr, nullptr,
+                 nullptr) != hipSuccess)
+    return 0;
+  return keys_bytes(n) + temp;
+}
+
+int md5hip_order_device_stable(const uint32_t* d_lens, uint64_t n, uint32_t kmax, void* d_scratch,
+                               uint64_t scratch_bytes, uint32_t* d_order, void* stream) {
+  if (n == 0) return 0;
+  if (!d_lens || !d_order || !d_scratch || kmax == 0 || kmax > MD5HIP_HIST_KMAX || n > 0x7fffffffull)
+    return -EINVAL;
+  if (int e = device_ok()) return e;
+  size_t temp = 0;
+  if (order_sort(nullptr, temp, d_lens, (uint32_t)n, kmax, nullptr, d_order, (hipStream_t)stream) != hipSuccess)
+    return -EINVAL;
+  if (scratch_bytes < keys_bytes(n) + temp) return -ENOSPC;
+  uint32_t* keys_out = (uint32_t*)d_scratch;
+  void* tmp = (uint8_t*)d_scratch + keys_bytes(n);
+  if (order_sort(tmp, temp, d_lens, (uint32_t)n, kmax, keys_out, d_order, (hipStream_t)stream) != hipSuccess)
+    return -EIO;
   return launched();
 }
 

@@ -223,6 +223,8 @@ struct slot {
      * md5hip_plan_hist): the plan is made from counts and the order built on
      * the device; hovf = a chunk past MD5HIP_HIST_KMAX (host sort instead) */
     uint32_t *hh, hkmax, *h_bkt, *d_bkt;
+    void *d_sort;                     /* md5hip_order_device_stable scratch (NULL: order_scatter) */
+    uint64_t sort_bytes;
     int hovf;
     /* keys already non-increasing in reservation order (a vector of full
      * blocks with a short last one, a single equal-length batch): then the
@@ -393,8 +395,19 @@ static int slot_prepare(md5hip_batcher *b, struct slot *sl)
                         : md5hip_plan_hist(sl->hh, sl->hkmax, n, NULL);
         if (dvar < 0) return dvar;
         sl->use_order = 0;
+    } else if (!sl->hovf && !sl->desc_direct && sl->d_sort) {
+        /* from the histogram: O(keys) on the host; the STABLE order on the
+         * device (equal keys in chunk order: a 6-batch C3 BALANCED launch
+         * ran 5-6 % longer in order_scatter's wave-arrival order,
+         * profiles/r06e/order_ab.json) */
+        dvar = md5hip_plan_hist(sl->hh, sl->hkmax, n, NULL);
+        if (dvar < 0) return dvar;
+        const int e = md5hip_order_device_stable(sl->d_len, n, sl->hkmax, sl->d_sort, sl->sort_bytes,
+                                                 sl->d_ord, sl->stream);
+        if (e) return e;
     } else if (!sl->hovf) {
-        /* from the histogram: O(keys) on the host, the order on the device */
+        /* small slots (lengths read in place from mapped host memory): one
+         * scatter launch, call latency first */
         dvar = md5hip_plan_hist(sl->hh, sl->hkmax, n, sl->h_bkt);
         if (dvar < 0) return dvar;
         if (hipMemcpyAsync(sl->d_bkt, sl->h_bkt, 4 * ((size_t)sl->hkmax + 1), hipMemcpyHostToDevice,
@@ -1006,6 +1019,7 @@ static void batcher_free(md5hip_batcher *b)
         free(sl->segs);
         free(sl->hh);
         hipHostFree(sl->h_bkt); hipFree(sl->d_bkt);
+        if (sl->d_sort) hipFree(sl->d_sort);
         pthread_cond_destroy(&sl->cv);
     }
     free(b->s);
@@ -1113,6 +1127,13 @@ static int batcher_new(int device, uint64_t slice_bytes, uint32_t nslots, uint64
         CK(hipHostMalloc((void **)&sl->h_bkt, sizeof(uint32_t) * ((size_t)MD5HIP_HIST_KMAX + 2),
                          hipHostMallocDefault));
         CK(hipMalloc((void **)&sl->d_bkt, sizeof(uint32_t) * ((size_t)MD5HIP_HIST_KMAX + 2)));
+        /* the stable order's scratch for slots past DESC_DIRECT_MAX chunks
+         * (none: those slots keep order_scatter) */
+        sl->sort_bytes = b->maxn > DESC_DIRECT_MAX ? md5hip_order_stable_scratch(b->maxn, 0) : 0;
+        if (sl->sort_bytes && hipMalloc(&sl->d_sort, sl->sort_bytes) != hipSuccess) {
+            (void)hipGetLastError();
+            sl->d_sort = NULL;
+        }
         if (!sl->b_dst || !sl->b_src || !sl->b_len || !sl->b_reg || !sl->hh) { rc = -ENOMEM; goto fail; }
     }
     if (pthread_create(&b->progress, NULL, progress_main, b) != 0) { rc = -EAGAIN; goto fail; }

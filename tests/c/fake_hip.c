@@ -481,3 +481,34 @@ int md5hip_order_device(const uint32_t *d_lens, uint64_t n, uint32_t kmax, uint3
     }
     return 0;
 }
+
+/* the stable longest-first order: a counting sort by key, equal keys in
+ * chunk order (md5hip_order_device_stable's contract) */
+uint64_t md5hip_order_stable_scratch(uint64_t n, uint32_t kmax)
+{
+    (void)kmax;
+    return n ? 4 * n + 256 : 0;
+}
+
+int md5hip_order_device_stable(const uint32_t *d_lens, uint64_t n, uint32_t kmax, void *d_scratch,
+                               uint64_t scratch_bytes, uint32_t *d_order, void *stream)
+{
+    on_stream((hipStream_t)stream);
+    if (enqueue_ok((hipStream_t)stream) != hipSuccess) return -EIO;
+    if (n == 0) return 0;
+    if (!d_lens || !d_order || !d_scratch || !kmax || scratch_bytes < 4 * n) return -EINVAL;
+    uint64_t *start = calloc((size_t)kmax + 2, sizeof *start);     /* by bucket kmax - key */
+    if (!start) return -ENOMEM;
+    for (uint64_t i = 0; i < n; i++) {
+        const uint32_t k = (d_lens[i] >> 6) + 1;
+        start[(k <= kmax ? kmax - k : kmax) + 1]++;
+    }
+    for (uint32_t b = 1; b <= kmax + 1; b++) start[b] += start[b - 1];
+    for (uint64_t i = 0; i < n; i++) {
+        const uint32_t k = (d_lens[i] >> 6) + 1;
+        d_order[start[k <= kmax ? kmax - k : kmax]++] = (uint32_t)i;
+    }
+    free(start);
+    return 0;
+}
+

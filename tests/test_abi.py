@@ -44,7 +44,7 @@ def test_exports_every_declared_symbol():
 
 def test_abi_version_and_names():
     L = _lib.lib()
-    assert L.md5hip_abi_version() == 4
+    assert L.md5hip_abi_version() == 5
     assert [m.variant_name(v) for v in m.VARIANTS.values()] == list(m.VARIANTS)
 
 

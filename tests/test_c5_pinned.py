@@ -7,6 +7,9 @@ ragged 1,013) is checked against the oracle, for
 
   * a torch pin_memory buffer (hipHostMalloc -- what bench.py --config c5 uses),
   * a numpy buffer pinned by md5hip_host_register,
+  * a numpy buffer pinned by someone else's hipHostRegister (not in the
+    library's table: the runtime's RANGE attributes decide), and a
+    sub-range of it,
   * the same through a two-device pool, whose parts start inside the pinned
     allocation (the RANGE check must accept a sub-range),
   * a numpy buffer whose first half only is registered: it starts pinned and
@@ -95,3 +98,25 @@ def test_partly_pinned_source_is_staged(cuda, batch):
         assert np.array_equal(got, want)
     finally:
         m.lib().md5hip_host_unregister(arr.ctypes.data)
+
+
+def test_host_registered_outside_the_library_dma_in_place(cuda, batch):
+    """A buffer page-locked by someone else's hipHostRegister (torch's
+    cudaHostRegister binding here) -- not in the library's registration table,
+    so host_pinned asks the runtime for both ends and the allocation's extent."""
+    host, want = batch
+    arr = host.copy()
+    cudart = torch.cuda.cudart()
+    assert int(cudart.cudaHostRegister(arr.ctypes.data, arr.nbytes, 0)) == 0
+    try:
+        with m.Batcher(device=0, slice_bytes=SLICE, nslots=3) as b:
+            got, staged = _run(b, arr)
+            assert np.array_equal(got, want)
+            # a sub-range starting inside the registration is pinned too
+            s0 = b.stats()["bytes_staged"]
+            sub = b.host_fixed(arr[L * 5:], N - 5, L)
+            assert b.stats()["bytes_staged"] == s0
+        assert staged == 0
+        assert np.array_equal(sub, want[5:])
+    finally:
+        cudart.cudaHostUnregister(arr.ctypes.data)

@@ -784,6 +784,63 @@ def test_order_device_is_a_longest_first_permutation(cuda):
             assert np.array_equal(got.cpu().numpy(), gen.oracle_digests(host, offs, [int(x) for x in lens]))
 
 
+def test_order_device_stable_equals_host_order(cuda):
+    """md5hip_order_device_stable (ABI 5, the batcher's order for large
+    slots): exactly md5hip_plan_desc's host order -- longest key first, equal
+    keys in chunk-index order -- for random, single-key, two-key and
+    C3-shaped lengths; a chunk past kmax goes last; scratch too small is
+    -ENOSPC; a BALANCED launch with it gives the oracle digests."""
+    import errno
+    import torch
+    from sproxy_amd import _lib
+    L = _lib.lib()
+    rng = np.random.default_rng(2025)
+    cases = [rng.integers(0, 300000, 200003).astype(np.uint32),
+             np.full(70000, 16384, np.uint32),
+             np.where(rng.integers(0, 2, 100001) == 1, 4096, 65536).astype(np.uint32),
+             np.asarray(gen.mixed_lengths(150000, seed=9), np.uint32),
+             rng.integers(0, 1 << 20, 5000).astype(np.uint32)]
+    s = torch.cuda.current_stream().cuda_stream
+    for lens in cases:
+        n = lens.size
+        kmax = int(((lens >> 6) + 1).max())
+        need = L.md5hip_order_stable_scratch(n, kmax)
+        assert need > 0 and L.md5hip_order_stable_scratch(n, 0) >= need
+        scratch = torch.empty(need, dtype=torch.uint8, device=cuda)
+        d_len = torch.from_numpy(lens.view(np.int32)).to(cuda)
+        d_ord = torch.full((n,), -1, dtype=torch.int32, device=cuda)
+        assert L.md5hip_order_device_stable(d_len.data_ptr(), n, kmax, scratch.data_ptr(), need,
+                                            d_ord.data_ptr(), s) == 0
+        host, _ = m.plan_desc(lens)
+        assert np.array_equal(d_ord.cpu().numpy().view(np.uint32), host), n
+        assert L.md5hip_order_device_stable(d_len.data_ptr(), n, kmax, scratch.data_ptr(), need - 1,
+                                            d_ord.data_ptr(), s) == -errno.ENOSPC
+    # a key past kmax: after every bucket, not dropped
+    lens = np.array([100, 5000, 70000, 64, 5000], np.uint32)
+    kmax = int(((np.array([100, 5000, 64, 5000]) >> 6) + 1).max())
+    need = L.md5hip_order_stable_scratch(lens.size, kmax)
+    scratch = torch.empty(need, dtype=torch.uint8, device=cuda)
+    d_len = torch.from_numpy(lens.view(np.int32)).to(cuda)
+    d_ord = torch.full((lens.size,), -1, dtype=torch.int32, device=cuda)
+    assert L.md5hip_order_device_stable(d_len.data_ptr(), lens.size, kmax, scratch.data_ptr(), need,
+                                        d_ord.data_ptr(), s) == 0
+    assert d_ord.cpu().numpy().tolist() == [1, 4, 0, 3, 2]
+    # a BALANCED launch in that order
+    lens = np.asarray(gen.mixed_lengths(40000, seed=10, max_len=1 << 18), np.uint32)
+    offs, total = gen.pack_offsets([int(x) for x in lens], align=16)
+    host = gen.xorshift_array(total + 64, seed=11)
+    kmax = int(((lens >> 6) + 1).max())
+    need = L.md5hip_order_stable_scratch(lens.size, kmax)
+    scratch = torch.empty(need, dtype=torch.uint8, device=cuda)
+    d_len = torch.from_numpy(lens.view(np.int32)).to(cuda)
+    d_ord = torch.empty(lens.size, dtype=torch.int32, device=cuda)
+    assert L.md5hip_order_device_stable(d_len.data_ptr(), lens.size, kmax, scratch.data_ptr(), need,
+                                        d_ord.data_ptr(), s) == 0
+    got = m.digest_desc(torch.from_numpy(host).to(cuda), torch.tensor(offs, dtype=torch.int64, device=cuda),
+                        d_len, d_ord, variant="balanced")
+    assert np.array_equal(got.cpu().numpy(), gen.oracle_digests(host, offs, [int(x) for x in lens]))
+
+
 def test_fixed_auto_small_batches_run_fed(golden, cuda):
     """md5hip_digest_fixed's AUTO launch sends a batch of at most one 64-chunk
     group per CU to fed pairs (md5_desc_fed, implicit layout) when its chunks
