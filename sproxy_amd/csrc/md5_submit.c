@@ -376,6 +376,18 @@ static int seg_has(const struct slot *sl, uint64_t t)
  * instead of two copy operations ahead of the launch on the slot's stream. */
 enum { DESC_DIRECT_MAX = 4096, EARLY_COPY_MIN = 8192 };
 
+/* The stable device order of a large slot: 0 done; 1 = refused before any
+ * device work (scratch sized at creation too small for this slot's n /
+ * kmax, an argument the sort does not take): fall back to order_scatter,
+ * never a failed ticket for it; < 0 = the sort's launch failed (-EIO): the
+ * slot fails, and no hash kernel runs on an order never written. */
+static int stable_order(struct slot *sl, uint64_t n)
+{
+    const int e = md5hip_order_device_stable(sl->d_len, n, sl->hkmax, sl->d_sort, sl->sort_bytes,
+                                             sl->d_ord, sl->stream);
+    return e == -ENOSPC || e == -EINVAL ? 1 : e;
+}
+
 static int slot_prepare(md5hip_batcher *b, struct slot *sl)
 {
     (void)b;
@@ -389,32 +401,30 @@ static int slot_prepare(md5hip_batcher *b, struct slot *sl)
             return -EIO;
         sl->copied_n = n;
     }
-    int dvar;
+    int dvar, e = 0;
     if (!sl->unsorted) {
         dvar = sl->hovf ? md5hip_plan_desc(sl->h_len, n, sl->h_ord)
                         : md5hip_plan_hist(sl->hh, sl->hkmax, n, NULL);
         if (dvar < 0) return dvar;
         sl->use_order = 0;
-    } else if (!sl->hovf && !sl->desc_direct && sl->d_sort) {
+    } else if (!sl->hovf && !sl->desc_direct && sl->d_sort &&
+               (dvar = md5hip_plan_hist(sl->hh, sl->hkmax, n, NULL)) >= 0 &&
+               (e = stable_order(sl, n)) <= 0) {
         /* from the histogram: O(keys) on the host; the STABLE order on the
          * device (equal keys in chunk order: a 6-batch C3 BALANCED launch
          * ran 5-6 % longer in order_scatter's wave-arrival order,
          * profiles/r06e/order_ab.json) */
-        dvar = md5hip_plan_hist(sl->hh, sl->hkmax, n, NULL);
-        if (dvar < 0) return dvar;
-        const int e = md5hip_order_device_stable(sl->d_len, n, sl->hkmax, sl->d_sort, sl->sort_bytes,
-                                                 sl->d_ord, sl->stream);
         if (e) return e;
     } else if (!sl->hovf) {
-        /* small slots (lengths read in place from mapped host memory): one
-         * scatter launch, call latency first */
+        /* small slots (lengths read in place from mapped host memory), and
+         * large ones whose stable sort was refused: one scatter launch */
         dvar = md5hip_plan_hist(sl->hh, sl->hkmax, n, sl->h_bkt);
         if (dvar < 0) return dvar;
         if (hipMemcpyAsync(sl->d_bkt, sl->h_bkt, 4 * ((size_t)sl->hkmax + 1), hipMemcpyHostToDevice,
                            sl->stream))
             return -EIO;
-        const int e = md5hip_order_device(sl->desc_direct ? sl->dh_len : sl->d_len, n, sl->hkmax,
-                                          sl->d_bkt, sl->d_ord, sl->stream);
+        e = md5hip_order_device(sl->desc_direct ? sl->dh_len : sl->d_len, n, sl->hkmax, sl->d_bkt,
+                                sl->d_ord, sl->stream);
         if (e) return e;
     } else {
         dvar = md5hip_plan_desc(sl->h_len, n, sl->h_ord);

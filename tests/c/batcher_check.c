@@ -71,6 +71,7 @@ void fake_hip_unpin(const void *p);
 void fake_hip_watch(const void *p, size_t len);
 extern unsigned long fake_hip_pageable_dma, fake_hip_watched_h2d;
 extern int fake_hip_no_range;
+extern unsigned long fake_hip_sort_refused;
 static int g_stop;
 #define STOPPED() __atomic_load_n(&g_stop, __ATOMIC_RELAXED)
 #define STOP() __atomic_store_n(&g_stop, 1, __ATOMIC_RELAXED)
@@ -1062,6 +1063,11 @@ int main(int argc, char **argv)
            (unsigned long long)bs.coalesced_launches, (unsigned long long)qs.submissions,
            (unsigned long long)qs.launches, (unsigned long long)qs.coalesced_launches,
            (unsigned long long)ps.routed_whole, (unsigned long long)ps.split);
+    printf("stable order refused (order_scatter fallback) %lu times\n", fake_hip_sort_refused);
+    if (!fake_hip_sort_refused) {
+        printf("FAIL the stable order's fallback never ran\n");
+        return 1;
+    }
     printf("batcher ok\n");
     return 0;
 }

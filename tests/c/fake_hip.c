@@ -483,7 +483,11 @@ int md5hip_order_device(const uint32_t *d_lens, uint64_t n, uint32_t kmax, uint3
 }
 
 /* the stable longest-first order: a counting sort by key, equal keys in
- * chunk order (md5hip_order_device_stable's contract) */
+ * chunk order (md5hip_order_device_stable's contract).  Every third call is
+ * refused with -ENOSPC (scratch too small), so the batcher's fallback to
+ * order_scatter runs too. */
+static unsigned long g_sort_calls;
+unsigned long fake_hip_sort_refused;
 uint64_t md5hip_order_stable_scratch(uint64_t n, uint32_t kmax)
 {
     (void)kmax;
@@ -497,6 +501,10 @@ int md5hip_order_device_stable(const uint32_t *d_lens, uint64_t n, uint32_t kmax
     if (enqueue_ok((hipStream_t)stream) != hipSuccess) return -EIO;
     if (n == 0) return 0;
     if (!d_lens || !d_order || !d_scratch || !kmax || scratch_bytes < 4 * n) return -EINVAL;
+    if (__atomic_add_fetch(&g_sort_calls, 1, __ATOMIC_RELAXED) % 3 == 0) {
+        __atomic_fetch_add(&fake_hip_sort_refused, 1, __ATOMIC_RELAXED);
+        return -ENOSPC;
+    }
     uint64_t *start = calloc((size_t)kmax + 2, sizeof *start);     /* by bucket kmax - key */
     if (!start) return -ENOMEM;
     for (uint64_t i = 0; i < n; i++) {
