@@ -8,8 +8,10 @@ choosing at random per step among
   the thread's own torch stream, and the same through a CRC-32 queue
   (blk_make_crc digests; small and long-block vectors pick the split kernel),
   device-resident fixed-length runs on the queue (md5_batch_submit_device_fixed,
-  host or device digests), and fastcrc = 128 page lists through a CRC-32
-  batcher that stages only each block's windows,
+  host or device digests), fastcrc = 128 page lists through a CRC-32
+  batcher that stages only each block's windows, and vectors past 4,096
+  chunks (device-resident on the queue, and <= 1 KiB host chunks on the pool),
+  whose slots take the stable device order (md5hip_order_device_stable),
 over random vectors (1-300 chunks, 0 B - 1 MiB, tails, zero-length) cut from
 a registered page heap or from pageable memory.  Every digest is checked
 against digests the oracle computed up front.  Prints one JSON summary; exits
@@ -56,6 +58,7 @@ def main():
     heap = gen.xorshift_array(total + 64, seed=77)
     want = gen.oracle_digests(heap, offs, lens)
     want_crc = gen.oracle_crc32_batch(heap, offs, lens)
+    small = [i for i in range(nchunks) if lens[i] <= 1024]   # 9,000 of them stay under the 8 MiB split
     pageable = heap.copy()                      # the same bytes, never registered
     dev = torch.from_numpy(heap).cuda()
     torch.cuda.synchronize()
@@ -88,7 +91,16 @@ def main():
                 bufs = [src[offs[i]:offs[i] + lens[i]] for i in idx]
                 exp = want[idx]
                 op = r.choice(["sync", "async", "iov", "iov_async", "verify", "qdev", "qdev_async", "fixed",
-                               "crc_qdev", "crc_qdev_async", "qfixed", "fastcrc_iov"])
+                               "crc_qdev", "crc_qdev_async", "qfixed", "fastcrc_iov", "qdev_big", "many_small"])
+                if op == "qdev_big":              # past 4,096 chunks: the stable device order (ABI 5)
+                    k = r.randint(4097, 20000)
+                    idx = [r.randrange(nchunks) for _ in range(k)]
+                    exp = want[idx]
+                elif op == "many_small":          # a host vector past 4,096 chunks of <= 1 KiB
+                    k = r.randint(4097, 9000)
+                    idx = [small[r.randrange(len(small))] for _ in range(k)]
+                    bufs = [src[offs[i]:offs[i] + lens[i]] for i in idx]
+                    exp = want[idx]
                 if op == "sync":
                     assert np.array_equal(pool.submit(bufs), exp), op
                 elif op == "async":
@@ -105,6 +117,16 @@ def main():
                     bad[j, 0] ^= 1
                     ok, nbad = pool.verify_iov([[b] for b in bufs], bad)
                     assert nbad == 1 and not ok[j], op
+                elif op == "many_small":
+                    assert np.array_equal(pool.submit(bufs), exp), op
+                elif op == "qdev_big":
+                    ptrs = np.asarray([dev.data_ptr() + offs[i] for i in idx], np.uint64)
+                    L = np.asarray([lens[i] for i in idx], np.uint32)
+                    with torch.cuda.stream(stream):
+                        if r.random() < 0.5:
+                            assert np.array_equal(q.submit_device(ptrs, L), exp), op
+                        else:
+                            held.append((q.submit_device_async(ptrs, L), exp))
                 elif op in ("qdev", "qdev_async"):
                     ptrs = np.asarray([dev.data_ptr() + offs[i] for i in idx], np.uint64)
                     L = np.asarray([lens[i] for i in idx], np.uint32)
