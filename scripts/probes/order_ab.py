@@ -12,6 +12,8 @@ run_c3q, one BALANCED launch each with
 
   device_sorted  the device order with each key bucket sorted by index
   device_stable  md5hip_order_device_stable (ABI 5, rocPRIM radix sort)
+  host_rev       equal keys in descending chunk order
+  batch_rr       equal keys round-robin over the batches
 
 interleaved over rounds in a shuffled order with the same 50 ms idle before
 each launch, timed with HIP events on the launch stream (queue: wall clock
@@ -78,6 +80,19 @@ def main():
     perm = rng.permutation(n)
     sh = perm[np.argsort(-keys[perm].astype(np.int64), kind="stable")]
     orders["shuffle"] = torch.from_numpy(sh.astype(np.int32)).cuda()
+    # equal keys in DESCENDING chunk order, and equal keys round-robin over
+    # the batches (chunk k of batch 0, of batch 1, ...)
+    kk = -keys.astype(np.int64)
+    idx = np.arange(n, dtype=np.int64)
+    orders["host_rev"] = torch.from_numpy(np.lexsort((-idx, kk)).astype(np.int32)).cuda()
+    bat = np.concatenate([np.full(x.size, j, np.int64) for j, x in enumerate(lk)])
+    rank_in_batch_key = np.zeros(n, np.int64)
+    o = np.lexsort((idx, bat, kk))                  # by key, batch, index
+    kb = np.stack([kk[o], bat[o]])
+    starts_kb = np.flatnonzero(np.r_[True, (kb[:, 1:] != kb[:, :-1]).any(axis=0)])
+    run_id = np.repeat(np.arange(starts_kb.size), np.diff(np.r_[starts_kb, n]))
+    rank_in_batch_key[o] = np.arange(n) - starts_kb[run_id]
+    orders["batch_rr"] = torch.from_numpy(np.lexsort((bat, rank_in_batch_key, kk)).astype(np.int32)).cuda()
     # the device order with each key bucket sorted by chunk index (= host's)
     dv = d_ord.cpu().numpy().view(np.uint32).astype(np.int64)
     ds = dv[np.lexsort((dv, -keys[dv].astype(np.int64)))]
