@@ -96,6 +96,7 @@ static int dev_enter(struct dev_guard *g, int device)
 {
     g->ok = hipGetDevice(&g->prev) == hipSuccess;
     if (hipSetDevice(device) != hipSuccess) {
+        (void)hipGetLastError();      /* ours: returned as -ENODEV, not left for the caller's next check */
         if (g->ok) (void)hipSetDevice(g->prev);
         return -ENODEV;
     }
@@ -1152,6 +1153,7 @@ static int batcher_new(int device, uint64_t slice_bytes, uint32_t nslots, uint64
     dev_leave(&g);
     return 0;
 fail:
+    (void)hipGetLastError();          /* a failed allocation is returned as rc, not left sticky */
     batcher_free(b);
     dev_leave(&g);
     return rc;

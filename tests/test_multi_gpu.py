@@ -1,6 +1,6 @@
-"""The multi-GPU code on distinct devices.  Each test needs
-more than one visible GPU and skips cleanly on a one-GPU box; on a node
-with several it runs
+"""The multi-GPU code on distinct devices.  The first three
+tests need more than one visible GPU and skip cleanly on a one-GPU box; on
+a node with several they run
 
   * bench.py --gpus N (N = min(devices, 8)) as the driver does: N ranks on N
     distinct devices, every rank's rate and parity sample in the line;
@@ -12,7 +12,8 @@ with several it runs
     current devices untouched (md5_submit.c dev_enter/dev_leave).
 
 The reference calls its checksum from every ASIO pool thread at once
-(netcache/common/asio_mgr.c:205, :1414)."""
+(netcache/common/asio_mgr.c:205, :1414).  The last test runs anywhere: a
+device index past the last visible one is refused at creation."""
 import json
 import os
 import subprocess
@@ -126,3 +127,24 @@ def test_pool_over_every_device_from_threads():
     for t in range(2 * ndev):
         assert np.array_equal(got[("fixed", t)], wants[t]), t
     assert all(d["launches"] > 0 for d in dev), dev
+
+
+def test_a_device_past_the_last_is_refused(cuda):
+    """Runs on any box: a pool or batcher naming a device index past the last
+    visible one fails with -ENODEV at creation (md5_submit.c dev_enter), frees
+    what it had built, leaves the caller's current device as it was, and
+    leaves no sticky HIP error for torch's next launch check."""
+    import errno
+    ndev = _ndev()
+    torch.cuda.set_device(0)
+    for make in (lambda: m.Batcher(device=ndev), lambda: m.Queue(device=ndev),
+                 lambda: m.Pool((0, ndev)), lambda: m.Pool((ndev,) * 2)):
+        with pytest.raises(m.MD5HipError) as ei:
+            make()
+        assert ei.value.rc == -errno.ENODEV
+        assert torch.cuda.current_device() == 0
+        # no sticky HIP error left behind for torch's next launch check
+        assert float((torch.ones(1024, device="cuda") * 2).sum().item()) == 2048.0
+    with m.Pool((0,)) as p:                          # the library still works afterwards
+        host = gen.xorshift_array(64 * 4096, seed=0x63)
+        assert np.array_equal(p.host_fixed(host, 64, 4096), gen.oracle_digests_fixed(host, 64, 4096))
